@@ -1,0 +1,167 @@
+/*
+ * rt.h — C ABI of librtmi355x.so, the MI355X-native primary-ray tracer.
+ *
+ * The reference (insomnick/raytracingdemo) has no FFI; its natural seam is
+ * one whole frame, `calculateScreen(StackBVH&, Camera&)` (src/main.cpp:322),
+ * which the caller `runTest` times (src/main.cpp:253-257) and follows with
+ * `shadeScreen` (src/main.cpp:351-381).  This ABI replaces that frame call
+ * and the objects it needs; each entry point names the reference interface it
+ * stands in for.  Plain pointers and sizes only; caller owns host buffers,
+ * the library owns device memory unless an *_device entry point is used.
+ *
+ * Semantics are the reference's, bit for bit: per-pixel hit-IDs (loader
+ * order), hit positions (fp64 o + d*t) and PPM bytes are identical to
+ * StackBVH::traverse + shadeScreen on the same tree.
+ *
+ * Errors: every int-returning call returns RT_OK (0) or a status below; the
+ * message is in rt_last_error() (thread-local).  Where the reference throws
+ * (stack_bvh.hpp:543,550 std::out_of_range; main.cpp:159,180,201
+ * std::invalid_argument "Unsupported bvh degree"; main.cpp:204
+ * std::out_of_range "Unknown algorithm"; object_loader.hpp:17
+ * std::runtime_error "Failed to load OBJ file") the same message text is
+ * returned with the matching status.  Nothing crosses the ABI as an exception.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* status codes */
+#define RT_OK 0
+#define RT_ERR_INVALID_ARGUMENT 1 /* std::invalid_argument in the reference */
+#define RT_ERR_OUT_OF_RANGE 2     /* std::out_of_range in the reference    */
+#define RT_ERR_RUNTIME 3          /* std::runtime_error (OBJ load failure)  */
+#define RT_ERR_HIP 4              /* HIP runtime failure                    */
+#define RT_ERR_NO_DEVICE 5        /* no gfx950 device / scene not uploaded  */
+
+/* BVH partition algorithms (main.cpp:128-205; stack_bvh.hpp:453-499) */
+#define RT_ALGO_MEDIAN 0
+#define RT_ALGO_SAH 1
+#define RT_ALGO_BSAH 2
+
+/* traversal modes: both are exact (identical results); they differ in speed */
+#define RT_MODE_EXACT 0 /* fp32 conservative traversal + fp64 reference leaf tests */
+#define RT_MODE_FP64 1  /* fp64 traversal throughout (simple, slower)          */
+
+/* render flags */
+#define RT_FLAG_COUNT 1u /* also count node/triangle fetches (rt_frame_stats) */
+
+#define RT_MISS 0xFFFFFFFFu
+
+typedef struct rt_scene rt_scene;
+
+/* A camera pose plus image geometry.  pos/dir as produced by
+ * rt_camera_path (CameraPath::circularPath, camera_path.hpp:18-26). */
+typedef struct {
+    double pos[3];
+    double dir[3];
+    int32_t width, height; /* the reference hard-codes 500x500 (main.cpp:36-37) */
+} rt_camera;
+
+/* Host-side frame outputs (any pointer may be NULL).  Pixel (i, j) — i the
+ * column (left->right), j the row (top->bottom) as in main.cpp:331-334 — is
+ * stored row-major at j*width + i (the reference stores idx=j+i*H, a layout
+ * choice; PPM order is row-major, benchmark.hpp:105-114). */
+typedef struct {
+    uint32_t *hit_id;   /* W*H, loader-order triangle index, RT_MISS = none  */
+    double *dist;       /* W*H, |hit - o| (stack_bvh.hpp:631), -1 on a miss */
+    double *pos;        /* 3*W*H, hit position o + d*t (triangle.hpp:86)      */
+    uint8_t *rgb;       /* 3*W*H, shadeScreen colour as PPM bytes             */
+    uint64_t hit_count; /* out: shadeScreen's return value (main.cpp:380)    */
+    double seconds;     /* out: device time of ray generation + traversal   */
+} rt_frame_out;
+
+/* Device-side outputs for rt_render_rows_device (pointers on the scene's
+ * device; any may be NULL).  Row r of the shard is image row
+ * row0 + r*row_stride; its pixels are at r*width + i. */
+typedef struct {
+    uint32_t *hit_id;
+    double *dist;
+    double *pos;
+    uint8_t *rgb;
+    unsigned long long *hit_count; /* one counter, atomically incremented */
+} rt_device_out;
+
+typedef struct {
+    uint64_t triangles;
+    uint64_t real_nodes, real_inner, real_leaves;
+    uint32_t depth, max_children, max_leaf_size;
+    uint32_t wide_width;      /* W of the device node format (2/4/8/16) */
+    uint64_t wide_nodes;      /* device wide nodes (incl. virtual ones) */
+    uint64_t device_bytes;    /* scene bytes resident per device        */
+    uint32_t stack_bound;     /* worst-case traversal stack entries     */
+    double node_bytes;        /* bytes of one wide node                 */
+} rt_scene_stats_t;
+
+typedef struct {
+    uint64_t rays;
+    uint64_t node_fetches;  /* wide nodes loaded                     */
+    uint64_t tri_tests;     /* fp64 Moller-Trumbore tests             */
+    uint64_t chain_checks;  /* fp64 ancestor-chain re-verifications  */
+    uint64_t hits;
+    uint64_t chain_nodes;   /* fp64 ancestor boxes loaded by those checks */
+} rt_frame_stats_t;
+
+/* objl::Loader + ObjectLoader::loadFromFile (object_loader.hpp:14-70,
+ * lib/OBJ_Loader.h:431-713): N*9 doubles (v0,v1,v2), loader order, each
+ * coordinate double(float) * scale.  *tris is malloc'd; free with rt_free. */
+int rt_load_obj(const char *path, double scale, double **tris, uint64_t *n_tris);
+void rt_free(void *p);
+
+/* runTest's scene centre (main.cpp:118-122). */
+int rt_scene_center(const double *tri_v, uint64_t n_tris, double center[3]);
+
+/* CameraPath(centre, resolution).circularPath(step) with the path centre
+ * recomputed as runTest does (main.cpp:123,235; camera_path.hpp:18-26). */
+int rt_camera_path(const double scene_center[3], int resolution, int step, double pos[3], double dir[3]);
+
+/* StackBVH::build(prims, partitionFn) (+ collapse passes for the "-c"
+ * variants: 2-way partition then log2(k)-1 collapse passes, main.cpp:208,
+ * 219-221).  algo = RT_ALGO_*, k in {2,4,8,16}.  The tree is identical to the
+ * reference's.  The scene is host-only until rt_scene_upload. */
+int rt_scene_create(const double *tri_v, uint64_t n_tris, int algo, int k, int collapse, rt_scene **out);
+
+/* Replicate the flattened scene on each listed HIP device (ordinal). */
+int rt_scene_upload(rt_scene *s, const int *devices, int n_devices);
+
+/* One whole frame on the first uploaded device, blocking; replaces
+ * calculateScreen + shadeScreen (main.cpp:253-262). */
+int rt_render_frame(rt_scene *s, const rt_camera *cam, int mode, rt_frame_out *out);
+
+/* Asynchronous shard render into caller device buffers on a caller stream
+ * (hipStream_t passed as void*; NULL = the null stream).  Used by the
+ * multi-GPU driver (one process per GPU, RCCL gather of the shards).
+ * flags: RT_FLAG_COUNT accumulates into the scene's per-device counters. */
+int rt_render_rows_device(rt_scene *s, int device, const rt_camera *cam, int mode, int row0, int row_stride,
+                          int nrows, const rt_device_out *out, void *stream, uint32_t flags);
+
+/* Read (and optionally reset) the per-device counters filled by
+ * RT_FLAG_COUNT renders (synchronises the device). */
+int rt_frame_stats(rt_scene *s, int device, int reset, rt_frame_stats_t *out);
+
+int rt_scene_stats(const rt_scene *s, rt_scene_stats_t *out);
+
+/* Reference visit order rank of every triangle (loader index -> rank) and
+ * the real tree in reference visit order, for tree-parity tests:
+ * boxes[6*nodes], meta[3*nodes] = (begin, end, nchildren), order[n_tris]
+ * (the BVH's owned primitive vector as loader indices). */
+int rt_scene_tree_dump(const rt_scene *s, double *boxes, int64_t *meta, int64_t *order);
+
+void rt_scene_destroy(rt_scene *s);
+
+const char *rt_last_error(void);
+int rt_abi_version(void);
+/* device name of ordinal `device` (for reports); "" when unavailable */
+const char *rt_device_name(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MI355X_H */

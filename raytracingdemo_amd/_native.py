@@ -1,0 +1,108 @@
+"""ctypes binding of librtmi355x.so (include/rt.h).
+
+The shared library is built in-tree (raytracingdemo_amd/librtmi355x.so) by
+``__graft_entry__.build()`` / ``make -C raytracingdemo_amd/csrc``.  There is no
+fallback: if the library is missing or no gfx950 device is present, calls fail
+loudly with :class:`RTError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtmi355x.so")
+
+# include/rt.h status codes
+RT_OK = 0
+RT_ERR_INVALID_ARGUMENT = 1
+RT_ERR_OUT_OF_RANGE = 2
+RT_ERR_RUNTIME = 3
+RT_ERR_HIP = 4
+RT_ERR_NO_DEVICE = 5
+STATUS_NAMES = {1: "invalid_argument", 2: "out_of_range", 3: "runtime_error", 4: "hip_error", 5: "no_device"}
+
+RT_MODE_EXACT = 0
+RT_MODE_FP64 = 1
+RT_FLAG_COUNT = 1
+RT_MISS = 0xFFFFFFFF
+
+# Every symbol include/rt.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "rt_load_obj", "rt_free", "rt_scene_center", "rt_camera_path", "rt_scene_create", "rt_scene_upload",
+    "rt_render_frame", "rt_render_rows_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
+    "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name",
+]
+
+
+class RTError(RuntimeError):
+    """A non-OK status from the C ABI (the reference would have thrown)."""
+
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"[{STATUS_NAMES.get(status, status)}] {msg}")
+        self.status = status
+        self.msg = msg
+
+
+class rt_camera(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("dir", C.c_double * 3), ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class rt_frame_out(C.Structure):
+    _fields_ = [("hit_id", C.POINTER(C.c_uint32)), ("dist", C.POINTER(C.c_double)), ("pos", C.POINTER(C.c_double)),
+                ("rgb", C.POINTER(C.c_uint8)), ("hit_count", C.c_uint64), ("seconds", C.c_double)]
+
+
+class rt_device_out(C.Structure):
+    _fields_ = [("hit_id", C.c_void_p), ("dist", C.c_void_p), ("pos", C.c_void_p), ("rgb", C.c_void_p),
+                ("hit_count", C.c_void_p)]
+
+
+class rt_scene_stats_t(C.Structure):
+    _fields_ = [("triangles", C.c_uint64), ("real_nodes", C.c_uint64), ("real_inner", C.c_uint64),
+                ("real_leaves", C.c_uint64), ("depth", C.c_uint32), ("max_children", C.c_uint32),
+                ("max_leaf_size", C.c_uint32), ("wide_width", C.c_uint32), ("wide_nodes", C.c_uint64),
+                ("device_bytes", C.c_uint64), ("stack_bound", C.c_uint32), ("node_bytes", C.c_double)]
+
+
+class rt_frame_stats_t(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("node_fetches", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("chain_checks", C.c_uint64), ("hits", C.c_uint64), ("chain_nodes", C.c_uint64)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load librtmi355x.so once (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RTError(RT_ERR_NO_DEVICE, f"{LIB_PATH} is not built (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    dp, u64p = C.POINTER(C.c_double), C.POINTER(C.c_uint64)
+    L.rt_last_error.restype = C.c_char_p
+    L.rt_device_name.restype = C.c_char_p
+    L.rt_device_name.argtypes = [C.c_int]
+    L.rt_abi_version.restype = C.c_int
+    L.rt_load_obj.argtypes = [C.c_char_p, C.c_double, C.POINTER(dp), u64p]
+    L.rt_free.argtypes = [C.c_void_p]
+    L.rt_scene_center.argtypes = [C.c_void_p, C.c_uint64, dp]
+    L.rt_camera_path.argtypes = [dp, C.c_int, C.c_int, dp, dp]
+    L.rt_scene_create.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.rt_scene_upload.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    L.rt_render_frame.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.POINTER(rt_frame_out)]
+    L.rt_render_rows_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
+    L.rt_frame_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(rt_frame_stats_t)]
+    L.rt_scene_stats.argtypes = [C.c_void_p, C.POINTER(rt_scene_stats_t)]
+    L.rt_scene_tree_dump.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.rt_scene_destroy.argtypes = [C.c_void_p]
+    _lib = L
+    return L
+
+
+def check(status: int) -> None:
+    if status != RT_OK:
+        raise RTError(status, lib().rt_last_error().decode(errors="replace"))

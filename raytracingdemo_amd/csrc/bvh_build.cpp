@@ -1,0 +1,531 @@
+// Host BVH feeder: rebuilds the reference's StackBVH tree exactly
+// (src/stack_bvh.hpp:26-608) and flattens it into the device format.
+//
+// The tree has to be *the same tree* as the reference's, not merely a good
+// one: the reference only reports a triangle if every ancestor's fp64 slab
+// test passes (stack_bvh.hpp:623), so exact parity on grazing rays depends on
+// the ancestor boxes.  The partition arithmetic below therefore keeps the
+// reference's operation order, and the sorts use libstdc++'s std::sort /
+// std::nth_element with the same comparator on the same input sequence, which
+// yields the same permutation as sorting the reference's Primitive* vector.
+// Compiled with -ffp-contract=off (the reference's x86-64 -O0 build had no FMA).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+
+#include "rt_internal.h"
+
+namespace rt {
+namespace {
+
+constexpr double DMAX = std::numeric_limits<double>::max();
+constexpr double DLOW = std::numeric_limits<double>::lowest();
+
+inline double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+inline double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+
+struct Box {
+    double mn[3] = {DMAX, DMAX, DMAX};
+    double mx[3] = {DLOW, DLOW, DLOW};
+    void grow(const Box& o) {
+        for (int a = 0; a < 3; a++) { mn[a] = smin(mn[a], o.mn[a]); mx[a] = smax(mx[a], o.mx[a]); }
+    }
+};
+// calculateSurfaceArea (stack_bvh.hpp:65-69)
+inline double area(const Box& b) {
+    double ex = b.mx[0] - b.mn[0], ey = b.mx[1] - b.mn[1], ez = b.mx[2] - b.mn[2];
+    return 2.0 * (ex * ey + ey * ez + ez * ex);
+}
+
+struct Builder {
+    const Soup& s;
+    std::vector<uint32_t> order;
+
+    explicit Builder(const Soup& soup) : s(soup) {}
+
+    Box tri_box(uint32_t t) const {
+        Box b;
+        for (int a = 0; a < 3; a++) { b.mn[a] = s.lo[a][t]; b.mx[a] = s.hi[a][t]; }
+        return b;
+    }
+    // findBounds (stack_bvh.hpp:26-52): the per-axis min/max chain; an empty
+    // range is the zero box.
+    Box bounds(int64_t lo, int64_t hi) const {
+        Box b;
+        if (lo == hi) { for (int a = 0; a < 3; a++) b.mn[a] = b.mx[a] = 0.0; return b; }
+        for (int64_t i = lo; i < hi; i++) {
+            uint32_t t = order[i];
+            for (int a = 0; a < 3; a++) { b.mn[a] = smin(b.mn[a], s.lo[a][t]); b.mx[a] = smax(b.mx[a], s.hi[a][t]); }
+        }
+        return b;
+    }
+    void sort_range(int64_t lo, int64_t hi, int axis) {
+        const double* c = s.c[axis].data();
+        std::sort(order.begin() + lo, order.begin() + hi, [c](uint32_t p, uint32_t q) { return c[p] < c[q]; });
+    }
+    static bool leaf(int64_t n, int k) { return n <= (int64_t)k || k < 2; }  // isLeaf :71-76
+
+    // medianSplit (:79-100)
+    std::vector<size_t> median(int64_t lo, int64_t hi, int axis, int k) {
+        const int64_t n = hi - lo;
+        if (leaf(n, k)) return {};
+        std::vector<size_t> sp;
+        for (int i = 1; i < k; ++i) {
+            size_t x = (size_t)(n * i) / k;
+            if (x == 0 || x >= (size_t)n) break;
+            sp.push_back(x);
+        }
+        const double* c = s.c[axis].data();
+        auto base = order.begin() + lo;
+        auto from = base;
+        for (size_t x : sp) {
+            std::nth_element(from, base + (std::ptrdiff_t)x, order.begin() + hi,
+                             [c](uint32_t p, uint32_t q) { return c[p] < c[q]; });
+            from = base + x + 1;
+        }
+        return sp;
+    }
+
+    // Greedy "split the most expensive segment" over `cells` (:153-236 and
+    // :342-438).  cost(seg) = area(bounds of cells) * count(cells); the split
+    // minimises left area*count + right area*count over cell boundaries.
+    template <bool BINNED>
+    std::vector<size_t> greedy(const std::vector<Box>& cell, const std::vector<int>& cnt, int k) {
+        struct Seg { size_t b, e; };
+        std::vector<Seg> segs{{0, cell.size()}};
+        auto seg_cost = [&](const Seg& g) {
+            Box b;
+            int64_t n = 0;
+            for (size_t i = g.b; i < g.e; ++i) b.grow(cell[i]);
+            if (BINNED) { for (size_t i = g.b; i < g.e; ++i) n += cnt[i]; }
+            else n = (int64_t)(g.e - g.b);
+            return area(b) * (double)n;
+        };
+        std::vector<size_t> splits;
+        std::vector<Box> pre, suf;
+        while (segs.size() < (size_t)k) {
+            size_t pick = SIZE_MAX;
+            double worst = -1.0;
+            for (size_t i = 0; i < segs.size(); ++i) {
+                if (segs[i].e - segs[i].b < 2) continue;
+                double c = seg_cost(segs[i]);
+                if (c > worst) { worst = c; pick = i; }
+            }
+            if (pick == SIZE_MAX) break;
+            const Seg g = segs[pick];
+            const size_t m = g.e - g.b;
+            pre.assign(m, Box{});
+            suf.assign(m, Box{});
+            pre[0] = cell[g.b];
+            for (size_t q = 1; q < m; ++q) { pre[q] = pre[q - 1]; pre[q].grow(cell[g.b + q]); }
+            suf[m - 1] = cell[g.e - 1];
+            for (size_t q = m - 1; q-- > 0;) { suf[q] = suf[q + 1]; suf[q].grow(cell[g.b + q]); }
+            size_t best_at = 1;
+            double best = DMAX;
+            if (BINNED) {
+                int left = 0, right = 0;
+                for (size_t q = 0; q < m; ++q) right += cnt[g.b + q];
+                for (size_t x = 1; x < m; ++x) {
+                    left += cnt[g.b + x - 1];
+                    right -= cnt[g.b + x - 1];
+                    double c = area(pre[x - 1]) * left + area(suf[x]) * right;
+                    if (c < best) { best = c; best_at = x; }
+                }
+                size_t prims = 0;  // primitives in cells [0, g.b + best_at)
+                for (size_t q = 0; q < g.b + best_at; ++q) prims += (size_t)cnt[q];
+                splits.push_back(prims);
+            } else {
+                for (size_t x = 1; x < m; ++x) {
+                    double c = area(pre[x - 1]) * x + area(suf[x]) * (m - x);
+                    if (c < best) { best = c; best_at = x; }
+                }
+                splits.push_back(g.b + best_at);
+            }
+            segs.erase(segs.begin() + pick);
+            segs.push_back({g.b, g.b + best_at});
+            segs.push_back({g.b + best_at, g.e});
+        }
+        return splits;
+    }
+
+    // sahSplit (:103-239): cells are the sorted primitives.
+    std::vector<size_t> sah(int64_t lo, int64_t hi, int axis, int k) {
+        if (leaf(hi - lo, k)) return {};
+        sort_range(lo, hi, axis);
+        std::vector<Box> cell((size_t)(hi - lo));
+        for (int64_t i = lo; i < hi; i++) cell[i - lo] = tri_box(order[i]);
+        return greedy<false>(cell, {}, k);
+    }
+
+    // binnedSahSplit (:241-449): 16 centre bins on `axis`.
+    std::vector<size_t> binned(int64_t lo, int64_t hi, int axis, int k) {
+        constexpr int NB = 16;
+        if (leaf(hi - lo, k)) return {};
+        sort_range(lo, hi, axis);
+        const double* c = s.c[axis].data();
+        double cmin = DMAX, cmax = DLOW;
+        for (int64_t i = lo; i < hi; ++i) { cmin = smin(cmin, c[order[i]]); cmax = smax(cmax, c[order[i]]); }
+        double range = cmax - cmin;
+        if (range < 1e-10) range = 1.0;
+        std::vector<Box> bin(NB);
+        std::vector<int> cnt(NB, 0);
+        for (int64_t i = lo; i < hi; ++i) {
+            uint32_t t = order[i];
+            int b = static_cast<int>(((c[t] - cmin) / range) * NB);
+            b = std::clamp(b, 0, NB - 1);
+            bin[b].grow(tri_box(t));
+            cnt[b]++;
+        }
+        std::vector<size_t> sp = greedy<true>(bin, cnt, k);
+        std::sort(sp.begin(), sp.end());
+        sp.erase(std::unique(sp.begin(), sp.end()), sp.end());
+        return sp;
+    }
+};
+
+// calculateLongestAxis (:54-63)
+int longest_axis(const double mn[3], const double mx[3]) {
+    double ex = mx[0] - mn[0], ey = mx[1] - mn[1], ez = mx[2] - mn[2];
+    if (ey > ex && ey >= ez) return 1;
+    if (ez > ex && ez >= ey) return 2;
+    return 0;
+}
+
+}  // namespace
+
+Soup make_soup(const double* tri_v, uint64_t n) {
+    Soup s;
+    s.n = n;
+    s.v.assign(tri_v, tri_v + n * 9);
+    for (int a = 0; a < 3; a++) { s.c[a].resize(n); s.lo[a].resize(n); s.hi[a].resize(n); }
+    s.normal.resize(n * 3);
+    for (uint64_t i = 0; i < n; i++) {
+        const double* p = tri_v + i * 9;
+        for (int a = 0; a < 3; a++) {
+            double x0 = p[a], x1 = p[3 + a], x2 = p[6 + a];
+            // centre = (v0 + v1 + v2) * (1.0/3)  (triangle.hpp:18)
+            s.c[a][i] = ((x0 + x1) + x2) * (1.0 / 3);
+            // std::min({..}) / std::max({..}): first extreme wins
+            double m = x0; if (x1 < m) m = x1; if (x2 < m) m = x2;
+            double M = x0; if (M < x1) M = x1; if (M < x2) M = x2;
+            s.lo[a][i] = m;
+            s.hi[a][i] = M;
+        }
+        // normal = cross(v1 - v0, v2 - v0).normalize()  (triangle.hpp:17)
+        double ax = p[3] - p[0], ay = p[4] - p[1], az = p[5] - p[2];
+        double bx = p[6] - p[0], by = p[7] - p[1], bz = p[8] - p[2];
+        double nx = ay * bz - az * by, ny = az * bx - ax * bz, nz = ax * by - ay * bx;
+        double len = std::sqrt(nx * nx + ny * ny + nz * nz);
+        if (len == 0) { nx = ny = nz = 0; } else { nx = nx / len; ny = ny / len; nz = nz / len; }
+        s.normal[i * 3] = nx; s.normal[i * 3 + 1] = ny; s.normal[i * 3 + 2] = nz;
+    }
+    return s;
+}
+
+Tree build_tree(const Soup& s, int algo, int k, int collapse) {
+    if (algo < 0 || algo > 2) throw Error{RT_ERR_OUT_OF_RANGE, "Unknown algorithm"};
+    if (!(k == 2 || k == 4 || k == 8 || k == 16)) throw Error{RT_ERR_INVALID_ARGUMENT, "Unsupported bvh degree"};
+    const int pk = collapse ? 2 : k;  // the -c variants partition 2-way (main.cpp:128-139)
+    Builder B(s);
+    B.order.resize(s.n);
+    std::iota(B.order.begin(), B.order.end(), 0u);
+    Tree t;
+    RNode root;
+    root.begin = 0;
+    root.end = (int64_t)s.n;
+    if (s.n == 0) {
+        for (int a = 0; a < 3; a++) root.mn[a] = root.mx[a] = 0.0;
+        t.nodes.push_back(root);
+        return t;
+    }
+    {
+        Box b = B.bounds(0, root.end);
+        std::memcpy(root.mn, b.mn, sizeof b.mn);
+        std::memcpy(root.mx, b.mx, sizeof b.mx);
+    }
+    t.nodes.push_back(root);
+    std::vector<int32_t> work{0};  // build work stack (:520-568)
+    while (!work.empty()) {
+        int32_t ni = work.back();
+        work.pop_back();
+        const int64_t lo = t.nodes[ni].begin, hi = t.nodes[ni].end;
+        if (hi - lo <= 1) continue;
+        const int axis = longest_axis(t.nodes[ni].mn, t.nodes[ni].mx);
+        std::vector<size_t> sp = algo == RT_ALGO_MEDIAN ? B.median(lo, hi, axis, pk)
+                                 : algo == RT_ALGO_SAH  ? B.sah(lo, hi, axis, pk)
+                                                         : B.binned(lo, hi, axis, pk);
+        if (sp.empty()) continue;
+        std::sort(sp.begin(), sp.end());
+        std::vector<int32_t> kids;
+        int64_t from = lo;
+        auto add_child = [&](int64_t a, int64_t b) {
+            RNode c;
+            c.begin = a;
+            c.end = b;
+            c.parent = ni;
+            Box bx = B.bounds(a, b);
+            std::memcpy(c.mn, bx.mn, sizeof bx.mn);
+            std::memcpy(c.mx, bx.mx, sizeof bx.mx);
+            kids.push_back((int32_t)t.nodes.size());
+            t.nodes.push_back(std::move(c));
+        };
+        for (size_t x : sp) {
+            if (x == 0 || x >= (size_t)(hi - lo)) throw Error{RT_ERR_OUT_OF_RANGE, "invalid split position"};
+            int64_t to = lo + (int64_t)x;
+            if (from >= to) throw Error{RT_ERR_OUT_OF_RANGE, "Invalid iterator range"};
+            add_child(from, to);
+            from = to;
+        }
+        add_child(from, hi);
+        t.nodes[ni].kids = kids;
+        for (int32_t c : kids) work.push_back(c);
+    }
+    if (collapse) {
+        // collapse (:574-608), log2(k)-1 passes (main.cpp:208)
+        const int passes = static_cast<int>(std::log2(k)) - 1;
+        for (int p = 0; p < passes; p++) {
+            std::vector<int32_t> st{0};
+            while (!st.empty()) {
+                int32_t ni = st.back();
+                st.pop_back();
+                if (t.nodes[ni].kids.empty()) continue;
+                std::vector<int32_t> nk;
+                for (int32_t c : t.nodes[ni].kids) {
+                    if (!t.nodes[c].kids.empty()) nk.insert(nk.end(), t.nodes[c].kids.begin(), t.nodes[c].kids.end());
+                    else nk.push_back(c);
+                }
+                t.nodes[ni].kids = nk;
+                for (int32_t c : nk) { t.nodes[c].parent = ni; st.push_back(c); }
+            }
+        }
+    }
+    t.order = std::move(B.order);
+    return t;
+}
+
+// ------------------------------------------------------------------ flatten
+namespace {
+
+inline float round_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+inline float round_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+}
+
+struct Flattener {
+    const Soup& s;
+    const Tree& t;
+    Flat& f;
+    int W;
+    uint32_t nb;
+    uint32_t wide_depth = 0;             // max wide nodes on a root-leaf path
+
+    Flattener(const Soup& s_, const Tree& t_, Flat& f_) : s(s_), t(t_), f(f_), W(f_.width), nb(rt_node_bytes(f_.width)) {}
+
+    // fp32 conservative box of a real node, padded by f.pad in world units
+    void box32(const double mn[3], const double mx[3], float out[6]) const {
+        for (int a = 0; a < 3; a++) {
+            out[2 * a] = round_down(mn[a] - f.pad);
+            out[2 * a + 1] = round_up(mx[a] + f.pad);
+        }
+    }
+
+    uint32_t alloc_node() {
+        uint32_t id = (uint32_t)f.n_wide++;
+        f.wide.resize(f.n_wide * nb, 0);
+        uint8_t* p = f.wide.data() + (size_t)id * nb;
+        float* b = reinterpret_cast<float*>(p);
+        for (int c = 0; c < W; c++) {  // empty slot: inverted box, never hit
+            b[0 * W + c] = std::numeric_limits<float>::infinity();
+            b[1 * W + c] = -std::numeric_limits<float>::infinity();
+            b[2 * W + c] = std::numeric_limits<float>::infinity();
+            b[3 * W + c] = -std::numeric_limits<float>::infinity();
+            b[4 * W + c] = std::numeric_limits<float>::infinity();
+            b[5 * W + c] = -std::numeric_limits<float>::infinity();
+        }
+        uint32_t* r = reinterpret_cast<uint32_t*>(p + 24 * W);
+        for (int c = 0; c < W; c++) r[c] = RT_INVALID_REF;
+        return id;
+    }
+    void set_slot(uint32_t node, int c, const float b6[6], uint32_t ref) {
+        uint8_t* p = f.wide.data() + (size_t)node * nb;
+        float* b = reinterpret_cast<float*>(p);
+        b[0 * W + c] = b6[0];
+        b[1 * W + c] = b6[1];
+        b[2 * W + c] = b6[2];
+        b[3 * W + c] = b6[3];
+        b[4 * W + c] = b6[4];
+        b[5 * W + c] = b6[5];
+        reinterpret_cast<uint32_t*>(p + 24 * W)[c] = ref;
+    }
+
+    // reference of a real node as a child slot value
+    uint32_t ref_of(int32_t ni, uint32_t depth) {
+        const RNode& n = t.nodes[ni];
+        if (n.kids.empty()) {
+            uint64_t cnt = (uint64_t)(n.end - n.begin);
+            if (cnt == 0) return RT_INVALID_REF;  // only the empty scene's root
+            if (cnt > 16) throw Error{RT_ERR_INVALID_ARGUMENT, "leaf larger than 16 primitives"};
+            if ((uint64_t)n.begin > RT_LEAF_MAX_FIRST) throw Error{RT_ERR_INVALID_ARGUMENT, "scene too large"};
+            return rt_make_leaf((uint32_t)n.begin, (uint32_t)cnt);
+        }
+        return emit_inner(n.kids, depth);
+    }
+
+    // Emits one wide node for a list of real children.  When a real node has
+    // more children than W (collapsed trees reach 16..256), the children are
+    // grouped under virtual wide nodes whose slot box is the union of the
+    // group's boxes (a conservative superset; the exact ancestor chain used by
+    // the fp64 re-verification only contains real nodes).
+    uint32_t emit_inner(const std::vector<int32_t>& kids, uint32_t depth) {
+        uint32_t id = alloc_node();
+        wide_depth = std::max(wide_depth, depth + 1);
+        if ((int)kids.size() <= W) {
+            for (size_t c = 0; c < kids.size(); c++) {
+                float b6[6];
+                box32(t.nodes[kids[c]].mn, t.nodes[kids[c]].mx, b6);
+                uint32_t r = ref_of(kids[c], depth + 1);
+                set_slot(id, (int)c, b6, r);
+            }
+            return id;
+        }
+        size_t groups = std::min<size_t>((size_t)W, (kids.size() + W - 1) / W);
+        size_t per = (kids.size() + groups - 1) / groups;
+        for (size_t g = 0; g < groups; g++) {
+            size_t a = g * per, b = std::min(kids.size(), a + per);
+            if (a >= b) break;
+            std::vector<int32_t> sub(kids.begin() + a, kids.begin() + b);
+            float b6[6] = {std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                           std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                           std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity()};
+            for (int32_t k : sub) {
+                float c6[6];
+                box32(t.nodes[k].mn, t.nodes[k].mx, c6);
+                for (int q = 0; q < 3; q++) {
+                    b6[2 * q] = std::min(b6[2 * q], c6[2 * q]);
+                    b6[2 * q + 1] = std::max(b6[2 * q + 1], c6[2 * q + 1]);
+                }
+            }
+            uint32_t r = sub.size() == 1 ? ref_of(sub[0], depth + 1) : emit_inner(sub, depth + 1);
+            set_slot(id, (int)g, b6, r);
+        }
+        return id;
+    }
+};
+
+}  // namespace
+
+Flat flatten(const Soup& s, const Tree& t, int width_hint) {
+    Flat f;
+    // --- tree statistics
+    uint32_t maxk = 0, maxleaf = 0, depth = 0, stack_bound = 1;
+    {
+        struct It { int32_t n; uint32_t d; uint32_t sb; };
+        std::vector<It> st{{0, 0, 1}};
+        while (!st.empty()) {
+            It it = st.back();
+            st.pop_back();
+            const RNode& n = t.nodes[it.n];
+            depth = std::max(depth, it.d);
+            if (n.kids.empty()) {
+                f.real_leaves++;
+                maxleaf = std::max<uint32_t>(maxleaf, (uint32_t)(n.end - n.begin));
+                stack_bound = std::max(stack_bound, it.sb);
+            } else {
+                f.real_inner++;
+                maxk = std::max<uint32_t>(maxk, (uint32_t)n.kids.size());
+                for (int32_t c : n.kids) st.push_back({c, it.d + 1, it.sb + (uint32_t)n.kids.size() - 1});
+            }
+        }
+    }
+    f.depth = depth;
+    f.max_children = maxk;
+    f.max_leaf = maxleaf;
+    int W = width_hint;
+    if (W <= 0) {
+        W = 2;
+        while (W < (int)maxk && W < 16) W *= 2;
+    }
+    if (!(W == 2 || W == 4 || W == 8 || W == 16)) throw Error{RT_ERR_INVALID_ARGUMENT, "wide node width must be 2/4/8/16"};
+    f.width = W;
+    (void)stack_bound;  // real-tree bound: used by the literal kernel (rt_api.cpp)
+
+    // --- padding of the fp32 boxes: 2^-18 * max |coordinate| (DESIGN.md
+    // "exactness").  Valid for camera origins within 3x that magnitude.
+    double cm = 0;
+    for (double x : s.v) cm = std::max(cm, std::fabs(x));
+    f.coord_max = cm;
+    f.pad = std::ldexp(cm > 0 ? cm : 1.0, -18);
+
+    // --- per-triangle data in BVH order
+    const uint64_t n = s.n;
+    f.tri64.resize(n * 9);
+    f.tri32.resize(n * 12, 0.0f);
+    f.tri_id.resize(n);
+    f.tri_rank.resize(n);
+    f.tri_leaf.resize(n);
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t id = t.order[i];
+        const double* p = s.v.data() + (size_t)id * 9;
+        double* q = f.tri64.data() + i * 9;
+        q[0] = p[0]; q[1] = p[1]; q[2] = p[2];
+        q[3] = p[3] - p[0]; q[4] = p[4] - p[1]; q[5] = p[5] - p[2];  // edge1 = v1 - v0 (triangle.hpp:42)
+        q[6] = p[6] - p[0]; q[7] = p[7] - p[1]; q[8] = p[8] - p[2];  // edge2 = v2 - v0
+        float* r = f.tri32.data() + i * 12;
+        for (int k = 0; k < 9; k++) r[k] = (float)q[k];
+        f.tri_id[i] = id;
+    }
+    // --- real nodes (fp64 box + parent) and reference visit ranks
+    const size_t R = t.nodes.size();
+    f.rbox.resize(R * 6);
+    f.rparent.resize(R);
+    for (size_t i = 0; i < R; i++) {
+        for (int a = 0; a < 3; a++) { f.rbox[i * 6 + a] = t.nodes[i].mn[a]; f.rbox[i * 6 + 3 + a] = t.nodes[i].mx[a]; }
+        f.rparent[i] = t.nodes[i].parent;
+    }
+    f.rkid_off.assign(R + 1, 0);
+    f.rrange.resize(R * 2);
+    for (size_t i = 0; i < R; i++) {
+        f.rkid_off[i + 1] = f.rkid_off[i] + (uint32_t)t.nodes[i].kids.size();
+        f.rrange[i * 2] = (uint32_t)t.nodes[i].begin;
+        f.rrange[i * 2 + 1] = (uint32_t)t.nodes[i].end;
+    }
+    f.rkid.reserve(f.rkid_off[R]);
+    for (size_t i = 0; i < R; i++) for (int32_t c : t.nodes[i].kids) f.rkid.push_back((uint32_t)c);
+    {
+        // visit order of StackBVH::traverse (stack_bvh.hpp:619-641): LIFO,
+        // children pushed 0..n-1 so the last child is visited first.
+        uint32_t rank = 0;
+        std::vector<int32_t> st{0};
+        while (!st.empty()) {
+            int32_t ni = st.back();
+            st.pop_back();
+            const RNode& nd = t.nodes[ni];
+            if (nd.kids.empty())
+                for (int64_t i = nd.begin; i < nd.end; i++) { f.tri_rank[i] = rank++; f.tri_leaf[i] = (uint32_t)ni; }
+            for (int32_t c : nd.kids) st.push_back(c);
+        }
+    }
+    // --- wide nodes
+    Flattener F(s, t, f);
+    F.box32(t.nodes[0].mn, t.nodes[0].mx, f.root_box);
+    if (n == 0) {
+        f.root_ref = RT_INVALID_REF;
+        F.alloc_node();
+    } else {
+        f.root_ref = F.ref_of(0, 0);
+        if (f.n_wide == 0) F.alloc_node();  // root is a leaf: keep a valid node array
+    }
+    // ordered traversal pushes at most W-1 siblings per wide level
+    f.stack_bound = F.wide_depth * (uint32_t)(W - 1) + 1;
+    return f;
+}
+
+}  // namespace rt

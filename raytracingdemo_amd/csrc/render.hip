@@ -1,0 +1,489 @@
+// gfx950 primary-ray kernels: fused ray generation + wide-BVH traversal +
+// exact fp64 resolve + head-light shading, one frame (or one row shard) per
+// launch.
+//
+// Reference semantics reproduced (bit for bit):
+//   ray generation  src/main.cpp:331-337 (+ camera.hpp:35-37 coefficients)
+//   Ray reciprocal  src/primitives/ray.hpp:13-19
+//   closest hit     src/stack_bvh.hpp:611-644 — min over detected triangles
+//                   of |(o + d t) - o| with strict '<' in visit order
+//   slab test       src/aabb.hpp:32-49 (fp64, std::min/std::max semantics)
+//   Moller-Trumbore src/primitives/triangle.hpp:40-88 (fp64, EPS 1e-8)
+//   shading         src/main.cpp:351-381 and the PPM byte cast
+//                   src/utils/benchmark.hpp:105-114
+//
+// Two traversal kernels, both exact:
+//   k_trace_exact   fp32 conservative traversal of W-wide nodes (outward-
+//                   rounded, padded boxes; ordered, distance-culled), exact
+//                   fp64 Moller-Trumbore on leaf triangles, and an fp64
+//                   re-verification of the reference ancestor chain before a
+//                   candidate may win (the reference only sees a triangle if
+//                   every ancestor's fp64 slab test passes).  Ties in distance
+//                   resolve by the reference visit rank.  See DESIGN.md.
+//   k_trace_literal the reference's own traversal (LIFO, no culling, no
+//                   ordering) in fp64 on the real tree — a cross-check.
+//
+// This TU is compiled with -ffp-contract=off: every fp64 expression must
+// round exactly like the reference's x86-64 build.  The fp32 traversal uses
+// explicit fmaf where contraction is wanted.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_device.h"
+
+namespace {
+
+struct Ray64 {
+    double ox, oy, oz;
+    double dx, dy, dz;
+    double ix, iy, iz;
+};
+
+__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+__device__ __forceinline__ double sclamp(double v, double lo, double hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
+
+// AABB::hit (aabb.hpp:32-49); b = {mn.x, mn.y, mn.z, mx.x, mx.y, mx.z}
+__device__ __forceinline__ bool box_hit64(const double* __restrict__ b, const Ray64& r) {
+    double tx1 = (b[0] - r.ox) * r.ix;
+    double tx2 = (b[3] - r.ox) * r.ix;
+    double tmin = smin(tx1, tx2);
+    double tmax = smax(tx1, tx2);
+    double ty1 = (b[1] - r.oy) * r.iy;
+    double ty2 = (b[4] - r.oy) * r.iy;
+    tmin = smax(tmin, smin(ty1, ty2));
+    tmax = smin(tmax, smax(ty1, ty2));
+    double tz1 = (b[2] - r.oz) * r.iz;
+    double tz2 = (b[5] - r.oz) * r.iz;
+    tmin = smax(tmin, smin(tz1, tz2));
+    tmax = smin(tmax, smax(tz1, tz2));
+    return tmax >= tmin;
+}
+
+// Triangle::intersect (triangle.hpp:40-62).  T = v0, edge1, edge2 (the
+// edges are precomputed with the same subtraction the reference performs).
+__device__ __forceinline__ bool mt64(const double* __restrict__ T, const Ray64& r, double& t_out) {
+    const double EPS = 1e-8;
+    const double e1x = T[3], e1y = T[4], e1z = T[5];
+    const double e2x = T[6], e2y = T[7], e2z = T[8];
+    const double hx = r.dy * e2z - r.dz * e2y;
+    const double hy = r.dz * e2x - r.dx * e2z;
+    const double hz = r.dx * e2y - r.dy * e2x;
+    const double a = e1x * hx + e1y * hy + e1z * hz;
+    if (a > -EPS && a < EPS) return false;
+    const double f = 1.0 / a;
+    const double sx = r.ox - T[0], sy = r.oy - T[1], sz = r.oz - T[2];
+    const double u = f * (sx * hx + sy * hy + sz * hz);
+    if (u < 0.0 || u > 1.0) return false;
+    const double qx = sy * e1z - sz * e1y;
+    const double qy = sz * e1x - sx * e1z;
+    const double qz = sx * e1y - sy * e1x;
+    const double v = f * (r.dx * qx + r.dy * qy + r.dz * qz);
+    if (v < 0.0 || u + v > 1.0) return false;
+    const double t = f * (e2x * qx + e2y * qy + e2z * qz);
+    if (!(t > EPS)) return false;
+    t_out = t;
+    return true;
+}
+
+// main.cpp:332-337: d = dir + up*py + right*px; d *= 1/|d|; Ray{pos, d}
+__device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) {
+    const double px = fp.px[i], py = fp.py[j];
+    double dx = (fp.dir[0] + fp.up[0] * py) + fp.right[0] * px;
+    double dy = (fp.dir[1] + fp.up[1] * py) + fp.right[1] * px;
+    double dz = (fp.dir[2] + fp.up[2] * py) + fp.right[2] * px;
+    const double s = 1.0 / __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+    dx = dx * s;
+    dy = dy * s;
+    dz = dz * s;
+    Ray64 r;
+    r.ox = fp.pos[0];
+    r.oy = fp.pos[1];
+    r.oz = fp.pos[2];
+    r.dx = dx;
+    r.dy = dy;
+    r.dz = dz;
+    const double inf = __builtin_huge_val();
+    r.ix = dx != 0.0 ? 1.0 / dx : inf;
+    r.iy = dy != 0.0 ? 1.0 / dy : inf;
+    r.iz = dz != 0.0 ? 1.0 / dz : inf;
+    return r;
+}
+
+// Candidate bookkeeping shared by both kernels.
+struct Best {
+    double dist;
+    uint32_t rank;
+    int32_t tri;  // BVH-order index, -1 = none
+    double px, py, pz;
+};
+
+// Distance of a detected hit exactly as stack_bvh.hpp:630-631 computes it.
+__device__ __forceinline__ double hit_dist(const Ray64& r, double t, double& px, double& py, double& pz) {
+    px = r.ox + r.dx * t;
+    py = r.oy + r.dy * t;
+    pz = r.oz + r.dz * t;
+    const double ex = px - r.ox, ey = py - r.oy, ez = pz - r.oz;
+    return __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+}
+
+// shadeScreen body (main.cpp:356-377) + PPM byte cast (benchmark.hpp:105-114)
+__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDevScene& sc, size_t o, const Best& b) {
+    uint8_t c0 = 0, c1 = 0, c2 = 0;
+    if (b.tri >= 0 && fp.rgb) {
+        const uint32_t id = sc.tri_id[b.tri];
+        double nx = sc.normal[3 * (size_t)id], ny = sc.normal[3 * (size_t)id + 1], nz = sc.normal[3 * (size_t)id + 2];
+        const double nl = __builtin_sqrt(nx * nx + ny * ny + nz * nz);
+        if (nl > 0.0) {
+            const double s = 1.0 / nl;
+            nx = nx * s; ny = ny * s; nz = nz * s;
+        }
+        double lx = fp.pos[0] - b.px, ly = fp.pos[1] - b.py, lz = fp.pos[2] - b.pz;
+        const double dist = __builtin_sqrt(lx * lx + ly * ly + lz * lz);
+        if (dist > 0.0) {
+            const double s = 1.0 / dist;
+            lx = lx * s; ly = ly * s; lz = lz * s;
+        }
+        const double diffuse = smax(0.0, nx * lx + ny * ly + nz * lz) * 1.35;
+        const double att = 1.0 / (1.0 + 0.05 * dist * dist);
+        const double I = sclamp((0.45 + diffuse * att) * 1.25, 0.0, 1.0);
+        c0 = (uint8_t)sclamp((0.5 * (nx + 1.0)) * I * 255.0, 0.0, 255.0);
+        c1 = (uint8_t)sclamp((0.5 * (ny + 1.0)) * I * 255.0, 0.0, 255.0);
+        c2 = (uint8_t)sclamp((0.5 * (nz + 1.0)) * I * 255.0, 0.0, 255.0);
+    }
+    if (fp.rgb) {
+        fp.rgb[3 * o] = c0;
+        fp.rgb[3 * o + 1] = c1;
+        fp.rgb[3 * o + 2] = c2;
+    }
+    if (fp.hit_id) fp.hit_id[o] = b.tri >= 0 ? sc.tri_id[b.tri] : RT_INVALID_REF;
+    if (fp.dist) fp.dist[o] = b.tri >= 0 ? b.dist : -1.0;
+    if (fp.hit_pos) {
+        fp.hit_pos[3 * o] = b.tri >= 0 ? b.px : 0.0;
+        fp.hit_pos[3 * o + 1] = b.tri >= 0 ? b.py : 0.0;
+        fp.hit_pos[3 * o + 2] = b.tri >= 0 ? b.pz : 0.0;
+    }
+    if (b.tri >= 0 && fp.hit_count) atomicAdd(fp.hit_count, 1ull);
+}
+
+// Pixel of this lane: each wave64 owns an 8x8 tile; a 256-thread block owns
+// four consecutive tiles along the row.
+__device__ __forceinline__ bool lane_pixel(const RtFrameParams& fp, int& i, int& r) {
+    const int lane = threadIdx.x & 63;
+    const int tiles_x = (fp.W + 7) >> 3;
+    const int tiles_y = (fp.nrows + 7) >> 3;
+    const int tile = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (tile >= tiles_x * tiles_y) return false;
+    i = (tile % tiles_x) * 8 + (lane & 7);
+    r = (tile / tiles_x) * 8 + (lane >> 3);
+    return i < fp.W && r < fp.nrows;
+}
+
+template <int W>
+__device__ __forceinline__ void load_w(float (&d)[W], const float* __restrict__ p) {
+    if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < W; c += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(p + c);
+            d[c] = v.x; d[c + 1] = v.y; d[c + 2] = v.z; d[c + 3] = v.w;
+        }
+    } else {
+        const float2 v = *reinterpret_cast<const float2*>(p);
+        d[0] = v.x; d[1] = v.y;
+    }
+}
+template <int W>
+__device__ __forceinline__ void load_refs(uint32_t (&d)[W], const uint32_t* __restrict__ p) {
+    if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < W; c += 4) {
+            const uint4 v = *reinterpret_cast<const uint4*>(p + c);
+            d[c] = v.x; d[c + 1] = v.y; d[c + 2] = v.z; d[c + 3] = v.w;
+        }
+    } else {
+        const uint2 v = *reinterpret_cast<const uint2*>(p);
+        d[0] = v.x; d[1] = v.y;
+    }
+}
+
+// fp32 upper bound of a positive double
+__device__ __forceinline__ float round_up_f(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+
+// The reference sees a triangle only when every box on its root path passes
+// the fp64 slab test; re-check that chain for a would-be winner.
+__device__ __forceinline__ bool chain_ok(const RtDevScene& sc, uint32_t leaf, const Ray64& r, uint32_t& loads) {
+    int32_t n = (int32_t)leaf;
+    while (n >= 0) {
+        loads++;
+        if (!box_hit64(sc.rbox + 6 * (size_t)n, r)) return false;
+        n = sc.rparent[n];
+    }
+    return true;
+}
+
+// --------------------------------------------------------------------------
+// Fast exact kernel.
+// --------------------------------------------------------------------------
+template <int W, int SMAX, bool COUNT>
+__global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParams fp) {
+    int i, r;
+    if (!lane_pixel(fp, i, r)) return;
+    const int j = fp.row0 + r * fp.row_stride;
+    const Ray64 ray = gen_ray(fp, i, j);
+
+    // fp32 ray for the conservative box tests; a zero direction component
+    // gets a large finite reciprocal (no 0*inf NaNs; same slab semantics).
+    const float ox = (float)ray.ox, oy = (float)ray.oy, oz = (float)ray.oz;
+    auto inv32 = [](double v) {
+        float f = (float)v;
+        if (!(__builtin_fabsf(f) <= 1e18f)) f = v < 0 ? -1e18f : 1e18f;
+        return f;
+    };
+    const float ix = inv32(ray.ix), iy = inv32(ray.iy), iz = inv32(ray.iz);
+    const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
+    // near/far plane selection by direction sign (ray-constant)
+    const int nxo = ix >= 0.f ? 0 : W, fxo = ix >= 0.f ? W : 0;
+    const int nyo = iy >= 0.f ? 2 * W : 3 * W, fyo = iy >= 0.f ? 3 * W : 2 * W;
+    const int nzo = iz >= 0.f ? 4 * W : 5 * W, fzo = iz >= 0.f ? 5 * W : 4 * W;
+
+    Best best;
+    best.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
+    best.rank = 0xFFFFFFFFu;
+    best.tri = -1;
+    best.px = best.py = best.pz = 0.0;
+    float tcull = __builtin_huge_valf();
+    uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
+    uint32_t chain_leaf = 0xFFFFFFFFu;
+    bool chain_res = false;
+
+    uint32_t sref[SMAX];
+    float stm[SMAX];
+    int sp = 0;
+
+    uint32_t cur = sc.root_ref;
+    {
+        const float* b = sc.root_box;
+        const float tx0 = __builtin_fmaf(ix >= 0.f ? b[0] : b[1], ix, -oix);
+        const float tx1 = __builtin_fmaf(ix >= 0.f ? b[1] : b[0], ix, -oix);
+        const float ty0 = __builtin_fmaf(iy >= 0.f ? b[2] : b[3], iy, -oiy);
+        const float ty1 = __builtin_fmaf(iy >= 0.f ? b[3] : b[2], iy, -oiy);
+        const float tz0 = __builtin_fmaf(iz >= 0.f ? b[4] : b[5], iz, -oiz);
+        const float tz1 = __builtin_fmaf(iz >= 0.f ? b[5] : b[4], iz, -oiz);
+        const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, 0.f));
+        const float tf = fminf(fminf(tx1, ty1), tz1);
+        if (!(tn <= tf) || cur == RT_INVALID_REF) cur = RT_INVALID_REF;
+    }
+
+    while (cur != RT_INVALID_REF) {
+        if (!(cur & RT_LEAF_BIT)) {
+            if (COUNT) n_nodes++;
+            const float* nb = reinterpret_cast<const float*>(sc.nodes + (size_t)cur * sc.node_bytes);
+            float nx[W], fx[W], ny[W], fy[W], nz[W], fz[W];
+            uint32_t ref[W];
+            load_w<W>(nx, nb + nxo);
+            load_w<W>(fx, nb + fxo);
+            load_w<W>(ny, nb + nyo);
+            load_w<W>(fy, nb + fyo);
+            load_w<W>(nz, nb + nzo);
+            load_w<W>(fz, nb + fzo);
+            load_refs<W>(ref, reinterpret_cast<const uint32_t*>(nb + 6 * W));
+            float tn[W];
+            uint32_t mask = 0;
+#pragma unroll
+            for (int c = 0; c < W; c++) {
+                const float a0 = __builtin_fmaf(nx[c], ix, -oix);
+                const float a1 = __builtin_fmaf(fx[c], ix, -oix);
+                const float b0 = __builtin_fmaf(ny[c], iy, -oiy);
+                const float b1 = __builtin_fmaf(fy[c], iy, -oiy);
+                const float c0 = __builtin_fmaf(nz[c], iz, -oiz);
+                const float c1 = __builtin_fmaf(fz[c], iz, -oiz);
+                const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
+                const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
+                tn[c] = t0;
+                if (t0 <= t1 && ref[c] != RT_INVALID_REF) mask |= 1u << c;
+            }
+            if (mask) {
+                // push all but the nearest, farthest first
+                while (__builtin_popcount(mask) > 1) {
+                    float far_t = -1.f;
+                    int far_c = 0;
+#pragma unroll
+                    for (int c = 0; c < W; c++)
+                        if (((mask >> c) & 1u) && tn[c] > far_t) { far_t = tn[c]; far_c = c; }
+                    uint32_t far_ref = ref[0];
+#pragma unroll
+                    for (int c = 1; c < W; c++)
+                        if (c == far_c) far_ref = ref[c];
+                    if (sp < SMAX) {
+                        sref[sp] = far_ref;
+                        stm[sp] = far_t;
+                        sp++;
+                    }
+                    mask &= ~(1u << far_c);
+                }
+                const int c0 = __builtin_ctz(mask);
+                uint32_t nxt = ref[0];
+#pragma unroll
+                for (int c = 1; c < W; c++)
+                    if (c == c0) nxt = ref[c];
+                cur = nxt;
+                continue;
+            }
+        } else {
+            const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+            const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+            for (uint32_t q = first; q < first + cnt; q++) {
+                if (COUNT) n_tris++;
+                double t;
+                if (!mt64(sc.tri64 + 9 * (size_t)q, ray, t)) continue;
+                double hx, hy, hz;
+                const double d = hit_dist(ray, t, hx, hy, hz);
+                const uint32_t rk = sc.tri_rank[q];
+                if (!(d < best.dist || (d == best.dist && rk < best.rank))) continue;
+                const uint32_t leaf = sc.tri_leaf[q];
+                if (leaf != chain_leaf) {
+                    if (COUNT) n_chain++;
+                    chain_leaf = leaf;
+                    chain_res = chain_ok(sc, leaf, ray, n_chain_nodes);
+                }
+                if (!chain_res) continue;
+                best.dist = d;
+                best.rank = rk;
+                best.tri = (int32_t)q;
+                best.px = hx;
+                best.py = hy;
+                best.pz = hz;
+                tcull = round_up_f(d * (1.0 + 0x1p-20));
+            }
+        }
+        // pop the next subtree still in front of the current best
+        cur = RT_INVALID_REF;
+        while (sp > 0) {
+            sp--;
+            if (stm[sp] <= tcull) {
+                cur = sref[sp];
+                break;
+            }
+        }
+    }
+
+    const size_t o = (size_t)r * fp.W + i;
+    shade_store(fp, sc, o, best);
+    if (COUNT && fp.counters) {
+        atomicAdd(&fp.counters[0], 1ull);
+        atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
+        atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
+        atomicAdd(&fp.counters[3], (unsigned long long)n_chain);
+        if (best.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
+        atomicAdd(&fp.counters[5], (unsigned long long)n_chain_nodes);
+    }
+}
+
+// --------------------------------------------------------------------------
+// Literal reference traversal (stack_bvh.hpp:611-644) on the real tree.
+// --------------------------------------------------------------------------
+template <int SMAX, bool COUNT>
+__global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFrameParams fp) {
+    int i, r;
+    if (!lane_pixel(fp, i, r)) return;
+    const int j = fp.row0 + r * fp.row_stride;
+    const Ray64 ray = gen_ray(fp, i, j);
+    Best best;
+    best.dist = 1.7976931348623157e308;
+    best.rank = 0;
+    best.tri = -1;
+    best.px = best.py = best.pz = 0.0;
+    uint32_t st[SMAX];
+    int sp = 0;
+    st[sp++] = 0;
+    uint32_t n_nodes = 0, n_tris = 0;
+    while (sp > 0) {
+        const uint32_t n = st[--sp];
+        if (COUNT) n_nodes++;
+        if (!box_hit64(sc.rbox + 6 * (size_t)n, ray)) continue;
+        const uint32_t k0 = sc.rkid_off[n], k1 = sc.rkid_off[n + 1];
+        if (k0 == k1) {
+            const uint32_t b = sc.rrange[2 * n], e = sc.rrange[2 * n + 1];
+            for (uint32_t q = b; q < e; q++) {
+                if (COUNT) n_tris++;
+                double t;
+                if (!mt64(sc.tri64 + 9 * (size_t)q, ray, t)) continue;
+                double hx, hy, hz;
+                const double d = hit_dist(ray, t, hx, hy, hz);
+                if (d < best.dist) {
+                    best.dist = d;
+                    best.tri = (int32_t)q;
+                    best.px = hx;
+                    best.py = hy;
+                    best.pz = hz;
+                }
+            }
+        }
+        for (uint32_t k = k0; k < k1; k++)
+            if (sp < SMAX) st[sp++] = sc.rkid[k];
+    }
+    const size_t o = (size_t)r * fp.W + i;
+    shade_store(fp, sc, o, best);
+    if (COUNT && fp.counters) {
+        atomicAdd(&fp.counters[0], 1ull);
+        atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
+        atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
+        if (best.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
+    }
+}
+
+template <int W, int SMAX>
+hipError_t launch_exact_w(const RtDevScene& sc, const RtFrameParams& fp, bool count, dim3 grid, hipStream_t s) {
+    if (count) hipLaunchKernelGGL((k_trace_exact<W, SMAX, true>), grid, dim3(256), 0, s, sc, fp);
+    else hipLaunchKernelGGL((k_trace_exact<W, SMAX, false>), grid, dim3(256), 0, s, sc, fp);
+    return hipGetLastError();
+}
+
+template <int W>
+hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, bool count, dim3 grid, hipStream_t s) {
+    const uint32_t need = sc.stack_bound;
+    if (need <= 32) return launch_exact_w<W, 32>(sc, fp, count, grid, s);
+    if (need <= 64) return launch_exact_w<W, 64>(sc, fp, count, grid, s);
+    if (need <= 128) return launch_exact_w<W, 128>(sc, fp, count, grid, s);
+    if (need <= 256) return launch_exact_w<W, 256>(sc, fp, count, grid, s);
+    return hipErrorInvalidValue;
+}
+
+template <int SMAX>
+hipError_t launch_literal_s(const RtDevScene& sc, const RtFrameParams& fp, bool count, dim3 grid, hipStream_t s) {
+    if (count) hipLaunchKernelGGL((k_trace_literal<SMAX, true>), grid, dim3(256), 0, s, sc, fp);
+    else hipLaunchKernelGGL((k_trace_literal<SMAX, false>), grid, dim3(256), 0, s, sc, fp);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+namespace rt {
+
+// Host entry: validates the launch geometry against what the kernels assume
+// and dispatches on node width / stack bound.  mode 0 = exact fast, 1 = literal.
+hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count, hipStream_t s,
+                        uint32_t literal_stack) {
+    if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
+    const long tiles = (long)((fp.W + 7) / 8) * (long)((fp.nrows + 7) / 8);
+    const dim3 grid((unsigned)((tiles + 3) / 4));
+    if (mode == 1) {
+        if (literal_stack <= 64) return launch_literal_s<64>(sc, fp, count, grid, s);
+        if (literal_stack <= 256) return launch_literal_s<256>(sc, fp, count, grid, s);
+        if (literal_stack <= 1024) return launch_literal_s<1024>(sc, fp, count, grid, s);
+        return hipErrorInvalidValue;
+    }
+    switch (sc.width) {
+        case 2: return launch_exact<2>(sc, fp, count, grid, s);
+        case 4: return launch_exact<4>(sc, fp, count, grid, s);
+        case 8: return launch_exact<8>(sc, fp, count, grid, s);
+        case 16: return launch_exact<16>(sc, fp, count, grid, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace rt

@@ -1,0 +1,455 @@
+// extern "C" surface of librtmi355x.so (include/rt.h).  Host C++ around the
+// gfx950 kernels in render.hip: scene ownership, device replicas, the frame
+// call that replaces calculateScreen + shadeScreen (src/main.cpp:253-262).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rt {
+hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count, hipStream_t s,
+                        uint32_t literal_stack);
+}
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int status, const std::string& msg) {
+    g_err = msg;
+    return status;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) throw rt::Error{RT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+
+struct DevGuard {  // restores the caller's current device
+    int prev = -1;
+    explicit DevGuard(int dev) {
+        hipGetDevice(&prev);
+        if (prev != dev) HIP_TRY(hipSetDevice(dev));
+    }
+    ~DevGuard() {
+        int now = -1;
+        hipGetDevice(&now);
+        if (prev >= 0 && now != prev) hipSetDevice(prev);
+    }
+};
+
+template <class T>
+size_t align_up(size_t x) {
+    return (x + 255) & ~size_t(255);
+}
+
+struct Replica {
+    int device = -1;
+    void* blob = nullptr;       // one allocation for the whole scene
+    size_t blob_bytes = 0;
+    RtDevScene dev{};
+    double* d_cam = nullptr;    // px[W] ++ py[H]
+    int cam_w = 0, cam_h = 0;
+    unsigned long long* d_counters = nullptr;  // 5 counters
+    // staging for the host-output frame call
+    void* frame = nullptr;
+    size_t frame_bytes = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+}  // namespace
+
+struct rt_scene {
+    rt::Soup soup;
+    rt::Tree tree;
+    rt::Flat flat;
+    std::vector<Replica> reps;
+    std::mutex mu;
+};
+
+namespace {
+
+void free_replica(Replica& r) {
+    if (r.device < 0) return;
+    int prev = -1;
+    hipGetDevice(&prev);
+    hipSetDevice(r.device);
+    if (r.blob) hipFree(r.blob);
+    if (r.d_cam) hipFree(r.d_cam);
+    if (r.d_counters) hipFree(r.d_counters);
+    if (r.frame) hipFree(r.frame);
+    if (r.ev0) hipEventDestroy(r.ev0);
+    if (r.ev1) hipEventDestroy(r.ev1);
+    if (r.stream) hipStreamDestroy(r.stream);
+    if (prev >= 0) hipSetDevice(prev);
+    r = Replica{};
+}
+
+Replica& replica_for(rt_scene* s, int device) {
+    for (auto& r : s->reps)
+        if (r.device == device) return r;
+    throw rt::Error{RT_ERR_NO_DEVICE, "scene not uploaded to device " + std::to_string(device)};
+}
+
+void upload_one(rt_scene* s, int device) {
+    DevGuard g(device);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        throw rt::Error{RT_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950"};
+    const rt::Flat& f = s->flat;
+    Replica r;
+    r.device = device;
+    // carve one allocation (256-B aligned sections)
+    struct Sec { const void* src; size_t bytes; size_t off; };
+    std::vector<Sec> secs = {
+        {f.wide.data(), f.wide.size(), 0},
+        {f.tri32.data(), f.tri32.size() * sizeof(float), 0},
+        {f.tri64.data(), f.tri64.size() * sizeof(double), 0},
+        {f.tri_id.data(), f.tri_id.size() * sizeof(uint32_t), 0},
+        {f.tri_rank.data(), f.tri_rank.size() * sizeof(uint32_t), 0},
+        {f.tri_leaf.data(), f.tri_leaf.size() * sizeof(uint32_t), 0},
+        {f.rbox.data(), f.rbox.size() * sizeof(double), 0},
+        {f.rparent.data(), f.rparent.size() * sizeof(int32_t), 0},
+        {s->soup.normal.data(), s->soup.normal.size() * sizeof(double), 0},
+        {f.rkid_off.data(), f.rkid_off.size() * sizeof(uint32_t), 0},
+        {f.rkid.data(), f.rkid.size() * sizeof(uint32_t), 0},
+        {f.rrange.data(), f.rrange.size() * sizeof(uint32_t), 0},
+    };
+    size_t off = 0;
+    for (auto& sc : secs) {
+        sc.off = off;
+        off += align_up<char>(std::max<size_t>(sc.bytes, 1));
+    }
+    r.blob_bytes = off;
+    HIP_TRY(hipMalloc(&r.blob, off));
+    std::vector<uint8_t> host(off, 0);
+    for (auto& sc : secs)
+        if (sc.bytes) std::memcpy(host.data() + sc.off, sc.src, sc.bytes);
+    HIP_TRY(hipMemcpy(r.blob, host.data(), off, hipMemcpyHostToDevice));
+    auto at = [&](int k) { return static_cast<uint8_t*>(r.blob) + secs[k].off; };
+    RtDevScene& d = r.dev;
+    d.nodes = at(0);
+    d.tri32 = reinterpret_cast<const float*>(at(1));
+    d.tri64 = reinterpret_cast<const double*>(at(2));
+    d.tri_id = reinterpret_cast<const uint32_t*>(at(3));
+    d.tri_rank = reinterpret_cast<const uint32_t*>(at(4));
+    d.tri_leaf = reinterpret_cast<const uint32_t*>(at(5));
+    d.rbox = reinterpret_cast<const double*>(at(6));
+    d.rparent = reinterpret_cast<const int32_t*>(at(7));
+    d.normal = reinterpret_cast<const double*>(at(8));
+    d.rkid_off = reinterpret_cast<const uint32_t*>(at(9));
+    d.rkid = reinterpret_cast<const uint32_t*>(at(10));
+    d.rrange = reinterpret_cast<const uint32_t*>(at(11));
+    d.root_ref = f.root_ref;
+    std::memcpy(d.root_box, f.root_box, sizeof d.root_box);
+    d.n_tris = (uint32_t)s->soup.n;
+    d.node_bytes = rt_node_bytes(f.width);
+    d.width = f.width;
+    d.stack_bound = f.stack_bound;
+    HIP_TRY(hipMalloc(&r.d_counters, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(r.d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&r.ev0));
+    HIP_TRY(hipEventCreate(&r.ev1));
+    s->reps.push_back(r);
+}
+
+// Coefficients for (W, H) on the replica's device (re-uploaded on change).
+void ensure_camera(Replica& r, int W, int H, hipStream_t stream) {
+    if (r.cam_w == W && r.cam_h == H) return;
+    std::vector<double> px, py;
+    rt::pixel_caches(W, H, px, py);
+    if (r.d_cam) HIP_TRY(hipFree(r.d_cam));
+    r.d_cam = nullptr;
+    HIP_TRY(hipMalloc(&r.d_cam, sizeof(double) * (size_t)(W + H)));
+    px.insert(px.end(), py.begin(), py.end());
+    HIP_TRY(hipMemcpyAsync(r.d_cam, px.data(), sizeof(double) * px.size(), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    r.cam_w = W;
+    r.cam_h = H;
+}
+
+void check_camera(const rt_scene* s, const rt_camera* c) {
+    if (!c) throw rt::Error{RT_ERR_INVALID_ARGUMENT, "camera is NULL"};
+    if (c->width <= 0 || c->height <= 0 || c->width > 65536 || c->height > 65536)
+        throw rt::Error{RT_ERR_INVALID_ARGUMENT, "bad image size"};
+    // the fp32 box padding covers camera origins up to 3x the scene's
+    // coordinate magnitude (exactness argument)
+    const double lim = 3.0 * std::max(s->flat.coord_max, 1.0);
+    for (int a = 0; a < 3; a++)
+        if (!(std::fabs(c->pos[a]) <= lim)) throw rt::Error{RT_ERR_OUT_OF_RANGE, "camera outside the exact-traversal envelope"};
+}
+
+RtFrameParams frame_params(Replica& r, const rt_camera* c, int row0, int row_stride, int nrows) {
+    RtFrameParams fp{};
+    for (int a = 0; a < 3; a++) {
+        fp.pos[a] = c->pos[a];
+        fp.dir[a] = c->dir[a];
+    }
+    rt::camera_basis(c->dir, fp.right, fp.up);
+    fp.px = r.d_cam;
+    fp.py = r.d_cam + c->width;
+    fp.W = c->width;
+    fp.H = c->height;
+    fp.row0 = row0;
+    fp.row_stride = row_stride;
+    fp.nrows = nrows;
+    return fp;
+}
+
+uint32_t literal_stack_bound(const rt_scene* s) {
+    // literal traversal pushes every child of a visited node
+    uint32_t best = 1;
+    struct It { int32_t n; uint32_t sb; };
+    std::vector<It> st{{0, 1}};
+    while (!st.empty()) {
+        It it = st.back();
+        st.pop_back();
+        const auto& n = s->tree.nodes[it.n];
+        best = std::max(best, it.sb);
+        for (int32_t k : n.kids) st.push_back({k, it.sb + (uint32_t)n.kids.size() - 1});
+    }
+    return best + 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_err.c_str(); }
+void rt_free(void* p) { std::free(p); }
+
+const char* rt_device_name(int device) {
+    static thread_local std::string name;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return "";
+    name = std::string(prop.name) + " (" + prop.gcnArchName + ")";
+    return name.c_str();
+}
+
+int rt_load_obj(const char* path, double scale, double** tris, uint64_t* n_tris) {
+    if (!path || !tris || !n_tris) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    try {
+        std::vector<double> v = rt::load_obj(path, scale);
+        double* buf = (double*)std::malloc(std::max<size_t>(v.size(), 1) * sizeof(double));
+        if (!buf) return fail(RT_ERR_RUNTIME, "out of memory");
+        if (!v.empty()) std::memcpy(buf, v.data(), v.size() * sizeof(double));
+        *tris = buf;
+        *n_tris = v.size() / 9;
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
+int rt_scene_center(const double* tri_v, uint64_t n, double center[3]) {
+    if (!tri_v || !center || n == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty scene");
+    rt::scene_center(tri_v, n, center);
+    return RT_OK;
+}
+
+int rt_camera_path(const double c[3], int res, int step, double pos[3], double dir[3]) {
+    if (!c || !pos || !dir || res <= 0) return fail(RT_ERR_INVALID_ARGUMENT, "bad camera path arguments");
+    rt::camera_path(c, res, step, pos, dir);
+    return RT_OK;
+}
+
+int rt_scene_create(const double* tri_v, uint64_t n, int algo, int k, int collapse, rt_scene** out) {
+    if (!out || (n && !tri_v)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out = nullptr;
+    if (algo < 0 || algo > 2) return fail(RT_ERR_OUT_OF_RANGE, "Unknown algorithm");
+    if (!(k == 2 || k == 4 || k == 8 || k == 16)) return fail(RT_ERR_INVALID_ARGUMENT, "Unsupported bvh degree");
+    if (n > RT_LEAF_MAX_FIRST) return fail(RT_ERR_INVALID_ARGUMENT, "too many triangles");
+    try {
+        std::unique_ptr<rt_scene> s(new rt_scene);
+        s->soup = rt::make_soup(tri_v, n);
+        s->tree = rt::build_tree(s->soup, algo, k, collapse);
+        s->flat = rt::flatten(s->soup, s->tree, 0);
+        *out = s.release();
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    } catch (const std::bad_alloc&) {
+        return fail(RT_ERR_RUNTIME, "out of memory");
+    }
+}
+
+int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {
+    if (!s || (n_devices > 0 && !devices)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    try {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device");
+        for (int q = 0; q < n_devices; q++) {
+            if (devices[q] < 0 || devices[q] >= count) return fail(RT_ERR_NO_DEVICE, "bad device ordinal");
+            bool have = false;
+            for (auto& r : s->reps) have |= r.device == devices[q];
+            if (!have) upload_one(s, devices[q]);
+        }
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
+int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mode, int row0, int row_stride,
+                          int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
+    if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (mode != RT_MODE_EXACT && mode != RT_MODE_FP64) return fail(RT_ERR_INVALID_ARGUMENT, "bad mode");
+    try {
+        check_camera(s, cam);
+        if (row0 < 0 || row_stride < 1 || nrows < 0 || (nrows > 0 && row0 + (int64_t)(nrows - 1) * row_stride >= cam->height))
+            return fail(RT_ERR_INVALID_ARGUMENT, "row shard outside the image");
+        Replica* r;
+        {
+            std::lock_guard<std::mutex> lk(s->mu);
+            r = &replica_for(s, device);
+        }
+        DevGuard g(device);
+        hipStream_t st = (hipStream_t)stream;
+        ensure_camera(*r, cam->width, cam->height, st);
+        RtFrameParams fp = frame_params(*r, cam, row0, row_stride, nrows);
+        fp.hit_id = out->hit_id;
+        fp.dist = out->dist;
+        fp.hit_pos = out->pos;
+        fp.rgb = out->rgb;
+        fp.hit_count = out->hit_count;
+        fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
+        HIP_TRY(rt::launch_trace(r->dev, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, literal_stack_bound(s)));
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
+int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* out) {
+    if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (s->reps.empty()) return fail(RT_ERR_NO_DEVICE, "scene not uploaded");
+    try {
+        check_camera(s, cam);
+        Replica& r = s->reps.front();
+        DevGuard g(r.device);
+        const size_t npx = (size_t)cam->width * cam->height;
+        // staging: hit_id u32 | dist f64 | pos 3xf64 | rgb 3xu8 | hit counter
+        const size_t o_id = 0, o_dist = align_up<char>(npx * 4), o_pos = o_dist + align_up<char>(npx * 8),
+                     o_rgb = o_pos + align_up<char>(npx * 24), o_cnt = o_rgb + align_up<char>(npx * 3),
+                     total = o_cnt + 256;
+        if (r.frame_bytes < total) {
+            if (r.frame) HIP_TRY(hipFree(r.frame));
+            r.frame = nullptr;
+            HIP_TRY(hipMalloc(&r.frame, total));
+            r.frame_bytes = total;
+        }
+        uint8_t* base = static_cast<uint8_t*>(r.frame);
+        rt_device_out d{};
+        d.hit_id = out->hit_id ? reinterpret_cast<uint32_t*>(base + o_id) : nullptr;
+        d.dist = out->dist ? reinterpret_cast<double*>(base + o_dist) : nullptr;
+        d.pos = out->pos ? reinterpret_cast<double*>(base + o_pos) : nullptr;
+        d.rgb = reinterpret_cast<uint8_t*>(base + o_rgb);  // always shaded (shadeScreen)
+        d.hit_count = reinterpret_cast<unsigned long long*>(base + o_cnt);
+        ensure_camera(r, cam->width, cam->height, r.stream);
+        HIP_TRY(hipMemsetAsync(d.hit_count, 0, 8, r.stream));
+        RtFrameParams fp = frame_params(r, cam, 0, 1, cam->height);
+        fp.hit_id = d.hit_id;
+        fp.dist = d.dist;
+        fp.hit_pos = d.pos;
+        fp.rgb = d.rgb;
+        fp.hit_count = d.hit_count;
+        HIP_TRY(hipEventRecord(r.ev0, r.stream));
+        HIP_TRY(rt::launch_trace(r.dev, fp, mode, false, r.stream, literal_stack_bound(s)));
+        HIP_TRY(hipEventRecord(r.ev1, r.stream));
+        if (out->hit_id) HIP_TRY(hipMemcpyAsync(out->hit_id, d.hit_id, npx * 4, hipMemcpyDeviceToHost, r.stream));
+        if (out->dist) HIP_TRY(hipMemcpyAsync(out->dist, d.dist, npx * 8, hipMemcpyDeviceToHost, r.stream));
+        if (out->pos) HIP_TRY(hipMemcpyAsync(out->pos, d.pos, npx * 24, hipMemcpyDeviceToHost, r.stream));
+        if (out->rgb) HIP_TRY(hipMemcpyAsync(out->rgb, d.rgb, npx * 3, hipMemcpyDeviceToHost, r.stream));
+        unsigned long long hc = 0;
+        HIP_TRY(hipMemcpyAsync(&hc, d.hit_count, 8, hipMemcpyDeviceToHost, r.stream));
+        HIP_TRY(hipStreamSynchronize(r.stream));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, r.ev0, r.ev1));
+        out->hit_count = hc;
+        out->seconds = ms * 1e-3;
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
+int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
+    if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    try {
+        Replica& r = replica_for(s, device);
+        DevGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        unsigned long long c[8];
+        HIP_TRY(hipMemcpy(c, r.d_counters, sizeof c, hipMemcpyDeviceToHost));
+        out->rays = c[0];
+        out->node_fetches = c[1];
+        out->tri_tests = c[2];
+        out->chain_checks = c[3];
+        out->hits = c[4];
+        out->chain_nodes = c[5];
+        if (reset) HIP_TRY(hipMemset(r.d_counters, 0, sizeof c));
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
+int rt_scene_stats(const rt_scene* s, rt_scene_stats_t* o) {
+    if (!s || !o) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    const rt::Flat& f = s->flat;
+    o->triangles = s->soup.n;
+    o->real_inner = f.real_inner;
+    o->real_leaves = f.real_leaves;
+    o->real_nodes = f.real_inner + f.real_leaves;
+    o->depth = f.depth;
+    o->max_children = f.max_children;
+    o->max_leaf_size = f.max_leaf;
+    o->wide_width = (uint32_t)f.width;
+    o->wide_nodes = f.n_wide;
+    o->node_bytes = rt_node_bytes(f.width);
+    o->stack_bound = f.stack_bound;
+    o->device_bytes = f.wide.size() + f.tri32.size() * 4 + f.tri64.size() * 8 + f.tri_id.size() * 12 +
+                      f.rbox.size() * 8 + f.rparent.size() * 4 + s->soup.normal.size() * 8 +
+                      (f.rkid_off.size() + f.rkid.size() + f.rrange.size()) * 4;
+    return RT_OK;
+}
+
+int rt_scene_tree_dump(const rt_scene* s, double* boxes, int64_t* meta, int64_t* order) {
+    if (!s || !boxes || !meta || !order) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    std::vector<int32_t> st{0};
+    int64_t k = 0;
+    while (!st.empty()) {
+        const rt::RNode& n = s->tree.nodes[st.back()];
+        st.pop_back();
+        for (int a = 0; a < 3; a++) { boxes[k * 6 + a] = n.mn[a]; boxes[k * 6 + 3 + a] = n.mx[a]; }
+        meta[k * 3] = n.begin;
+        meta[k * 3 + 1] = n.end;
+        meta[k * 3 + 2] = (int64_t)n.kids.size();
+        k++;
+        for (int32_t c : n.kids) st.push_back(c);
+    }
+    for (size_t i = 0; i < s->tree.order.size(); i++) order[i] = s->tree.order[i];
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* s) {
+    if (!s) return;
+    for (auto& r : s->reps) free_replica(r);
+    delete s;
+}
+
+}  // extern "C"

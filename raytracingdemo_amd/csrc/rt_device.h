@@ -1,0 +1,63 @@
+// Layouts shared by the host flattener and the gfx950 kernels.
+//
+// HBM layout of one scene replica (see DESIGN.md §Data layout):
+//   wide nodes   W child slots, SoA fp32 bounds (lo_x[W] hi_x[W] lo_y[W]
+//                hi_y[W] lo_z[W] hi_z[W]) then u32 child refs[W]; one node is
+//                node_bytes(W) = roundup(28*W, 64) bytes (W=8: 256 B, four
+//                64-B lines).  Bounds are the reference's fp64 boxes rounded
+//                outward to fp32 and padded (conservative superset).
+//   tri32        BVH order, fp32 v0,e1,e2 + pad (48 B)   — fp32 pre-filter
+//   tri64        BVH order, fp64 v0,e1,e2 (72 B)         — exact reference MT
+//   tri_id/rank/leaf  BVH order u32: loader index, reference visit rank,
+//                real leaf node (for the ancestor re-verification)
+//   rbox/rparent real reference nodes: fp64 box (48 B) + parent
+//   normal       loader order fp64 normal (24 B), read once per hit pixel
+#pragma once
+#include <stdint.h>
+
+#define RT_LEAF_BIT 0x80000000u
+#define RT_INVALID_REF 0xFFFFFFFFu
+#define RT_LEAF_FIRST_MASK 0x07FFFFFFu
+#define RT_LEAF_MAX_FIRST 0x07FFFFFFu
+
+#ifdef __cplusplus
+static inline constexpr uint32_t rt_node_bytes(int W) { return (uint32_t)((28 * W + 63) / 64 * 64); }
+static inline constexpr uint32_t rt_make_leaf(uint32_t first, uint32_t count) {
+    return RT_LEAF_BIT | ((count - 1u) << 27) | first;
+}
+#endif
+
+struct RtDevScene {
+    const uint8_t* nodes;
+    const float* tri32;      // 12 floats per triangle
+    const double* tri64;     // 9 doubles per triangle
+    const uint32_t* tri_id;
+    const uint32_t* tri_rank;
+    const uint32_t* tri_leaf;
+    const double* rbox;      // 6 per real node
+    const int32_t* rparent;
+    const double* normal;    // loader order, 3 per triangle
+    const uint32_t* rkid_off;// real tree CSR (literal reference-order mode)
+    const uint32_t* rkid;
+    const uint32_t* rrange;  // real node primitive range [begin, end)
+    uint32_t root_ref;
+    float root_box[6];
+    uint32_t n_tris;
+    uint32_t node_bytes;
+    int32_t width;
+    uint32_t stack_bound;
+};
+
+struct RtFrameParams {
+    double pos[3], dir[3], right[3], up[3];
+    const double* px;  // W pixel-plane x coefficients (camera.hpp:35)
+    const double* py;  // H pixel-plane y coefficients (camera.hpp:37)
+    int32_t W, H;
+    int32_t row0, row_stride, nrows;
+    uint32_t* hit_id;
+    double* dist;
+    double* hit_pos;
+    uint8_t* rgb;
+    unsigned long long* hit_count;
+    unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits] or NULL
+};

@@ -1,0 +1,75 @@
+// Host-side internals of librtmi355x.so (not part of the ABI).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rt_device.h"
+#include "../../include/rt.h"
+
+namespace rt {
+
+// Status + message, thrown inside the library and converted at the ABI.
+struct Error {
+    int status;
+    std::string msg;
+};
+
+// Triangle soup in loader order with the per-triangle values the reference
+// precomputes (triangle.hpp:14-19, getMin/getMax :27-38), stored SoA.
+struct Soup {
+    uint64_t n = 0;
+    std::vector<double> v;           // n*9: v0, v1, v2
+    std::vector<double> c[3];        // centre per axis
+    std::vector<double> lo[3], hi[3];// per-triangle box
+    std::vector<double> normal;      // n*3
+};
+Soup make_soup(const double* tri_v, uint64_t n);
+
+// One node of the reference tree (stack_bvh.hpp:13-18): a contiguous range of
+// the owned primitive vector and its children.
+struct RNode {
+    double mn[3], mx[3];
+    int64_t begin, end;
+    std::vector<int32_t> kids;
+    int32_t parent = -1;
+};
+
+struct Tree {
+    std::vector<RNode> nodes;     // nodes[0] = root
+    std::vector<uint32_t> order;  // owned primitive vector (loader indices)
+};
+
+// StackBVH::build + partition fn + collapse (stack_bvh.hpp:26-608).
+Tree build_tree(const Soup& s, int algo, int k, int collapse);
+
+// Device-format scene (wide fp32 nodes + fp64 leaf data), built from Tree.
+struct Flat {
+    int width = 8;                        // W
+    uint32_t root_ref = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
+    double pad = 0, coord_max = 0;        // outward padding of fp32 boxes
+    std::vector<uint8_t> wide;            // wide nodes, node_bytes(W) each
+    uint64_t n_wide = 0;
+    std::vector<double> tri64;            // BVH order: v0, e1, e2 (9 doubles)
+    std::vector<float> tri32;             // BVH order: v0, e1, e2 (fp32, 12 floats padded)
+    std::vector<uint32_t> tri_id, tri_rank, tri_leaf;
+    std::vector<double> rbox;             // real nodes: 6 doubles
+    std::vector<int32_t> rparent;         // real nodes: parent
+    std::vector<uint32_t> rkid_off, rkid, rrange;  // real tree in CSR form
+    uint32_t stack_bound = 0;
+    uint32_t depth = 0, max_children = 0, max_leaf = 0;
+    uint64_t real_inner = 0, real_leaves = 0;
+};
+Flat flatten(const Soup& s, const Tree& t, int width_hint);
+
+// Camera helpers (camera.hpp:20-38, main.cpp:325-329, camera_path.hpp:18-26)
+void pixel_caches(int W, int H, std::vector<double>& px, std::vector<double>& py);
+void camera_basis(const double dir[3], double right[3], double up[3]);
+void camera_path(const double center[3], int res, int step, double pos[3], double dir[3]);
+void scene_center(const double* tri_v, uint64_t n, double out[3]);
+
+// OBJ ingestion with objl semantics (lib/OBJ_Loader.h:431-1003).
+std::vector<double> load_obj(const std::string& path, double scale);
+
+}  // namespace rt

@@ -1,0 +1,224 @@
+"""GPU parity: the gfx950 kernels through the C ABI vs the reference's goldens
+and the oracle.  Bit-exact hit-IDs, hit positions (fp64), distances and PPM
+bytes; both traversal modes (exact-fast and literal fp64)."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import golden_scene, normals_of, pixel_fixture, pixel_fixture_names
+
+pytestmark = pytest.mark.gpu
+
+rt = pytest.importorskip("raytracingdemo_amd")
+MODELS = ["teapot.obj", "suzanne.obj", "stanford-bunny.obj"]
+_SCENES: dict = {}
+
+
+def scene(model, algo="bsah", k=2, scale=None, tris=None):
+    key = (model, algo, k, scale)
+    if key not in _SCENES:
+        t = golden_scene(model, scale) if tris is None else tris
+        _SCENES[key] = rt.Scene(t, algo, k).upload([0])
+    return _SCENES[key]
+
+
+def compare_with_oracle(oracle, s, tris, pos, d, W, H, algo, k, mode="exact"):
+    g = s.calculate_screen(pos, d, W, H, mode=mode)
+    o = oracle.bvh(tris, algo, k).render(pos, d, W, H)
+    oid = o["id"].astype(np.int64)
+    gid = np.where(g["hit_id"] == rt.RT_MISS, -1, g["hit_id"].astype(np.int64))
+    assert np.array_equal(gid, oid), f"hit-id mismatch at {np.flatnonzero(gid != oid)[:10]}"
+    m = oid >= 0
+    assert np.array_equal(g["pos"][m], o["pos"][m])
+    assert np.array_equal(g["dist"][m], o["dist"][m])
+    assert np.all(g["dist"][~m] == -1.0)
+    assert np.array_equal(g["rgb"], o["rgb"])
+    assert g["hits"] == o["hits"]
+    return g
+
+
+@pytest.mark.parametrize("mode", ["exact", "fp64"])
+@pytest.mark.parametrize("model", MODELS)
+def test_reference_frames_bit_exact(frames_golden, model, mode):
+    """500x500 frames 0,9,17,27 == testruns_final PPM bytes and hit counts."""
+    g = frames_golden[model]
+    tris = golden_scene(model)
+    s = scene(model, "bsah", 2)
+    c = rt.scene_center(tris)
+    for step in (0, 9, 17, 27):
+        pos, d = rt.CameraPath(c, 36).circular_path(step)
+        out = s.calculate_screen(pos, d, 500, 500, mode=mode, want=("rgb",))
+        assert hashlib.sha256(rt.ppm_bytes(out["rgb"], 500, 500)).hexdigest() == g["frames"][step]["sha256"], step
+        assert out["hits"] == g["frames"][step]["hits"]
+
+
+@pytest.mark.parametrize("algo,k", [("bsah", 4), ("bsah", 8), ("bsah", 16), ("sah", 4), ("median", 16),
+                                    ("bsah-c", 8), ("sah-c", 16), ("median-c", 4)])
+def test_every_tree_variant_gives_reference_frame(frames_golden, algo, k):
+    """The reference's validate_data invariant: identical bytes for every BVH."""
+    for model in MODELS:
+        tris = golden_scene(model)
+        s = scene(model, algo, k)
+        c = rt.scene_center(tris)
+        step = 17
+        pos, d = rt.CameraPath(c, 36).circular_path(step)
+        out = s.calculate_screen(pos, d, 500, 500, want=("rgb",))
+        assert hashlib.sha256(rt.ppm_bytes(out["rgb"], 500, 500)).hexdigest() == \
+            frames_golden[model]["frames"][step]["sha256"], (model, algo, k)
+
+
+@pytest.mark.parametrize("name", pixel_fixture_names())
+def test_pixels_vs_reference_fixture(name):
+    """Per-pixel fixtures produced by the compiled reference (oracle/_ref)."""
+    z = pixel_fixture(name)
+    model = str(z["model"])
+    tris = golden_scene(model, float(z["scale"]))
+    s = scene(model, str(z["algo"]), int(z["k"]), float(z["scale"]), tris)
+    W, H = int(z["W"]), int(z["H"])
+    g = s.calculate_screen(z["cam_pos"], z["cam_dir"], W, H)
+    hit = np.unpackbits(z["hit"])[: W * H].astype(bool)
+    assert np.array_equal(g["hit_id"] != rt.RT_MISS, hit)
+    assert np.array_equal(g["rgb"], z["rgb"])
+    assert g["hits"] == int(z["hits"])
+    sel = z["sel"]
+    hs = hit[sel]
+    assert np.array_equal(g["pos"][sel][hs], z["pos"][hs])
+    nrm = normals_of(tris)[g["hit_id"][sel][hs].astype(np.int64)]
+    assert np.array_equal(nrm, z["nrm"][hs])
+
+
+@pytest.mark.parametrize("mode", ["exact", "fp64"])
+def test_vs_oracle_random_cameras(oracle, mode):
+    rng = np.random.default_rng(1234)
+    for model, algo, k in [("teapot.obj", "bsah", 8), ("suzanne.obj", "sah-c", 8), ("stanford-bunny.obj", "median", 2)]:
+        tris = golden_scene(model)
+        s = scene(model, algo, k)
+        c = rt.scene_center(tris)
+        lo, hi = tris.reshape(-1, 3).min(0), tris.reshape(-1, 3).max(0)
+        for _ in range(3):
+            pos = c + rng.uniform(-1.0, 1.0, 3) * (hi - lo) * 1.2
+            d = c + rng.uniform(-0.3, 0.3, 3) * (hi - lo) - pos
+            d = d / np.sqrt((d * d).sum())
+            W, H = int(rng.integers(16, 160)), int(rng.integers(16, 120))
+            compare_with_oracle(oracle, s, tris, pos, d, W, H, algo, k, mode)
+
+
+def test_non_square_and_odd_sizes(oracle):
+    tris = golden_scene("stanford-bunny.obj")
+    s = scene("stanford-bunny.obj", "bsah", 4)
+    c = rt.scene_center(tris)
+    pos, d = rt.CameraPath(c, 36).circular_path(4)
+    for W, H in [(1, 1), (7, 3), (640, 360), (123, 457), (1920, 1080)]:
+        compare_with_oracle(oracle, s, tris, pos, d, W, H, "bsah", 4)
+
+
+def test_sponza_proxy_bands_vs_oracle(oracle):
+    """Headline scene (262,267-triangle proxy), 1920x1080 BVH8: row bands vs oracle."""
+    from raytracingdemo_amd.scenes import sponza_proxy_triangles
+    tris = sponza_proxy_triangles()
+    s = rt.Scene(tris, "bsah", 8).upload([0])
+    c = rt.scene_center(tris)
+    b = oracle.bvh(tris, "bsah", 8)
+    for step in (0, 13, 29):
+        pos, d = rt.CameraPath(c, 36).circular_path(step)
+        g = s.calculate_screen(pos, d, 1920, 1080)
+        for row0 in (0, 389, 777, 1064):
+            o = b.render(pos, d, 1920, 1080, row0=row0, nrows=16)
+            sl = slice(row0 * 1920, (row0 + 16) * 1920)
+            gid = np.where(g["hit_id"][sl] == rt.RT_MISS, -1, g["hit_id"][sl].astype(np.int64))
+            assert np.array_equal(gid, o["id"]), (step, row0)
+            m = o["id"] >= 0
+            assert np.array_equal(g["pos"][sl][m], o["pos"][m])
+            assert np.array_equal(g["rgb"][sl], o["rgb"])
+
+
+def test_exact_and_literal_modes_agree_on_sponza_proxy():
+    from raytracingdemo_amd.scenes import sponza_proxy_triangles
+    tris = sponza_proxy_triangles(60000)
+    s = rt.Scene(tris, "bsah", 8).upload([0])
+    c = rt.scene_center(tris)
+    pos, d = rt.CameraPath(c, 36).circular_path(7)
+    a = s.calculate_screen(pos, d, 320, 180, mode="exact")
+    b = s.calculate_screen(pos, d, 320, 180, mode="fp64")
+    for key in ("hit_id", "dist", "pos", "rgb"):
+        assert np.array_equal(a[key], b[key]), key
+
+
+def test_distance_ties_resolve_in_reference_visit_order(oracle):
+    """Coincident duplicate triangles tie exactly; the reference keeps the first
+    one it visits (strict '<', stack_bvh.hpp:631)."""
+    base = golden_scene("suzanne.obj")
+    tris = np.concatenate([base, base[::7]])  # duplicates of every 7th triangle
+    for algo, k in [("sah", 2), ("median", 8), ("sah-c", 16)]:
+        s = rt.Scene(tris, algo, k).upload([0])
+        c = rt.scene_center(tris)
+        pos, d = rt.CameraPath(c, 36).circular_path(3)
+        compare_with_oracle(oracle, s, tris, pos, d, 160, 120, algo, k)
+        compare_with_oracle(oracle, s, tris, pos, d, 160, 120, algo, k, mode="fp64")
+
+
+def test_edge_scenes(oracle):
+    # empty scene: every ray misses
+    s = rt.Scene(np.zeros((0, 9)), "bsah", 8).upload([0])
+    out = s.calculate_screen([0, 0, 5], [0, 0, -1], 32, 16)
+    assert out["hits"] == 0 and np.all(out["hit_id"] == rt.RT_MISS) and not out["rgb"].any()
+    # one triangle, leaf root
+    tri = np.array([[-1.0, -1.0, 0.0, 1.0, -1.0, 0.0, 0.0, 1.0, 0.0]])
+    s = rt.Scene(tri, "bsah", 2).upload([0])
+    compare_with_oracle(oracle, s, tri, [0.0, 0.0, 3.0], [0.0, 0.0, -1.0], 64, 48, "bsah", 2)
+    # camera looking away from the scene: all miss (boxes behind the camera are
+    # still "hit" by the reference's unclipped slab test, but no triangle is)
+    tris = golden_scene("teapot.obj")
+    s = scene("teapot.obj", "bsah", 8)
+    c = rt.scene_center(tris)
+    out = s.calculate_screen(c + np.array([0.0, 0.0, 8.0]), [0.0, 0.0, 1.0], 64, 64)
+    assert out["hits"] == 0
+    # degenerate (zero-area) triangles never hit (|a| < EPS, triangle.hpp:46)
+    deg = np.concatenate([tris[:100], np.tile(tris[:1, 0:3], (1, 3))])
+    s = rt.Scene(deg, "sah", 4).upload([0])
+    compare_with_oracle(oracle, s, deg, c + np.array([0.0, 0.0, 5.0]), [0.0, 0.0, -1.0], 80, 60, "sah", 4)
+
+
+def test_row_shards_reassemble_to_full_frame():
+    """Row-interleaved shards (multi-GPU partition) rebuild the full frame bit for bit."""
+    torch = pytest.importorskip("torch")
+    tris = golden_scene("stanford-bunny.obj")
+    s = scene("stanford-bunny.obj", "bsah", 4)
+    c = rt.scene_center(tris)
+    pos, d = rt.CameraPath(c, 36).circular_path(11)
+    W, H = 320, 240
+    full = s.calculate_screen(pos, d, W, H)
+    for G in (2, 3, 8):
+        rgb = np.zeros((H, W, 3), np.uint8)
+        ids = np.zeros((H, W), np.uint32)
+        hits = 0
+        for r in range(G):
+            nrows = len(range(r, H, G))
+            t_id = torch.empty(nrows * W, dtype=torch.int32, device="cuda:0")
+            t_rgb = torch.empty(nrows * W * 3, dtype=torch.uint8, device="cuda:0")
+            t_cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+            st = torch.cuda.current_stream()
+            s.render_rows_device(0, pos, d, W, H, r, G, nrows, hit_id=t_id.data_ptr(), rgb=t_rgb.data_ptr(),
+                                 hit_count=t_cnt.data_ptr(), stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            ids[r::G] = t_id.cpu().numpy().view(np.uint32).reshape(nrows, W)
+            rgb[r::G] = t_rgb.cpu().numpy().reshape(nrows, W, 3)
+            hits += int(t_cnt.item())
+        assert np.array_equal(ids.reshape(-1), full["hit_id"])
+        assert np.array_equal(rgb.reshape(-1, 3), full["rgb"])
+        assert hits == full["hits"]
+
+
+def test_errors_fail_loudly():
+    with pytest.raises(rt.RTError, match="Unknown algorithm"):
+        rt.Scene(golden_scene("teapot.obj"), "quick", 2)
+    with pytest.raises(rt.RTError, match="Unsupported bvh degree"):
+        rt.Scene(golden_scene("teapot.obj"), "bsah", 3)
+    with pytest.raises(rt.RTError, match="invalid split position"):
+        rt.Scene(np.tile(golden_scene("teapot.obj")[:1], (3, 1)), "bsah", 2)
+    s = rt.Scene(golden_scene("teapot.obj"), "bsah", 2)
+    with pytest.raises(rt.RTError, match="not uploaded"):
+        s.calculate_screen([0, 0, 5], [0, 0, -1], 8, 8)

@@ -1,0 +1,38 @@
+#!/usr/bin/env bash
+# One GPU-box session: smoke -> parity tests -> bench -> rocprofv3 kernel trace.
+# Each GPU step has its own time limit; the session stops at the first fault,
+# abort, segfault or timeout (exit >= 2 other than pytest's "tests failed" = 1).
+# Usage: tools/gpu_session.sh [steps...]   (default: smoke tests bench prof)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${*:-smoke tests bench prof}
+
+run() {  # name limit cmd...
+    local name=$1 lim=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name exit=$rc"
+    tail -n 25 "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name exit $rc"; exit $rc; fi
+    if [ $rc -eq 1 ] && [ "$name" != "tests" ]; then echo "STOP: $name failed"; exit 1; fi
+    return 0
+}
+
+for s in $STEPS; do
+    case $s in
+        smoke) run smoke 300 python __graft_entry__.py smoke ;;
+        tests) run tests 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+        bench) run bench 600 python bench.py ;;
+        prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
+                   -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+        pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o fetch \
+                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \
+               run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
+                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "=== session done"

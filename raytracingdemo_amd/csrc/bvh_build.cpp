@@ -329,11 +329,12 @@ struct Flattener {
 
     Flattener(const Soup& s_, const Tree& t_, Flat& f_) : s(s_), t(t_), f(f_), W(f_.width), nb(rt_node_bytes(f_.width)) {}
 
-    // fp32 conservative box of a real node, padded by f.pad in world units
+    // fp32 conservative (outward-rounded) box of a real node; the kernel adds a
+    // per-frame margin to the planes (render.hip, "pad")
     void box32(const double mn[3], const double mx[3], float out[6]) const {
         for (int a = 0; a < 3; a++) {
-            out[2 * a] = round_down(mn[a] - f.pad);
-            out[2 * a + 1] = round_up(mx[a] + f.pad);
+            out[2 * a] = round_down(mn[a]);
+            out[2 * a + 1] = round_up(mx[a]);
         }
     }
 
@@ -457,12 +458,12 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     f.width = W;
     (void)stack_bound;  // real-tree bound: used by the literal kernel (rt_api.cpp)
 
-    // --- padding of the fp32 boxes: 2^-18 * max |coordinate| (DESIGN.md
-    // "exactness").  Valid for camera origins within 3x that magnitude.
+    // --- scene coordinate magnitude: sizes the per-frame plane margin of the
+    // fp32 traversal (rt_api.cpp frame_params, DESIGN.md "exactness")
     double cm = 0;
     for (double x : s.v) cm = std::max(cm, std::fabs(x));
     f.coord_max = cm;
-    f.pad = std::ldexp(cm > 0 ? cm : 1.0, -18);
+    f.pad = 0;
 
     // --- per-triangle data in BVH order
     const uint64_t n = s.n;

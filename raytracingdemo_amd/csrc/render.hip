@@ -244,7 +244,13 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
         return f;
     };
     const float ix = inv32(ray.ix), iy = inv32(ray.iy), iz = inv32(ray.iz);
-    const float oix = ox * ix, oiy = oy * iy, oiz = oz * iz;
+    // Slab planes widened by fp.pad (world units): t = (plane -/+ pad - o)*inv.
+    // Near planes use o + pad*sgn(inv), far planes o - pad*sgn(inv); pad bounds
+    // every fp32 rounding of o, inv and the fma (DESIGN.md "exactness").
+    const float px_ = ix >= 0.f ? fp.pad : -fp.pad, py_ = iy >= 0.f ? fp.pad : -fp.pad,
+                pz_ = iz >= 0.f ? fp.pad : -fp.pad;
+    const float onx = (ox + px_) * ix, ony = (oy + py_) * iy, onz = (oz + pz_) * iz;  // near offsets
+    const float ofx = (ox - px_) * ix, ofy = (oy - py_) * iy, ofz = (oz - pz_) * iz;  // far offsets
     // near/far plane selection by direction sign (ray-constant)
     const int nxo = ix >= 0.f ? 0 : W, fxo = ix >= 0.f ? W : 0;
     const int nyo = iy >= 0.f ? 2 * W : 3 * W, fyo = iy >= 0.f ? 3 * W : 2 * W;
@@ -267,12 +273,12 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
     uint32_t cur = sc.root_ref;
     {
         const float* b = sc.root_box;
-        const float tx0 = __builtin_fmaf(ix >= 0.f ? b[0] : b[1], ix, -oix);
-        const float tx1 = __builtin_fmaf(ix >= 0.f ? b[1] : b[0], ix, -oix);
-        const float ty0 = __builtin_fmaf(iy >= 0.f ? b[2] : b[3], iy, -oiy);
-        const float ty1 = __builtin_fmaf(iy >= 0.f ? b[3] : b[2], iy, -oiy);
-        const float tz0 = __builtin_fmaf(iz >= 0.f ? b[4] : b[5], iz, -oiz);
-        const float tz1 = __builtin_fmaf(iz >= 0.f ? b[5] : b[4], iz, -oiz);
+        const float tx0 = __builtin_fmaf(ix >= 0.f ? b[0] : b[1], ix, -onx);
+        const float tx1 = __builtin_fmaf(ix >= 0.f ? b[1] : b[0], ix, -ofx);
+        const float ty0 = __builtin_fmaf(iy >= 0.f ? b[2] : b[3], iy, -ony);
+        const float ty1 = __builtin_fmaf(iy >= 0.f ? b[3] : b[2], iy, -ofy);
+        const float tz0 = __builtin_fmaf(iz >= 0.f ? b[4] : b[5], iz, -onz);
+        const float tz1 = __builtin_fmaf(iz >= 0.f ? b[5] : b[4], iz, -ofz);
         const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, 0.f));
         const float tf = fminf(fminf(tx1, ty1), tz1);
         if (!(tn <= tf) || cur == RT_INVALID_REF) cur = RT_INVALID_REF;
@@ -295,12 +301,12 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
             uint32_t mask = 0;
 #pragma unroll
             for (int c = 0; c < W; c++) {
-                const float a0 = __builtin_fmaf(nx[c], ix, -oix);
-                const float a1 = __builtin_fmaf(fx[c], ix, -oix);
-                const float b0 = __builtin_fmaf(ny[c], iy, -oiy);
-                const float b1 = __builtin_fmaf(fy[c], iy, -oiy);
-                const float c0 = __builtin_fmaf(nz[c], iz, -oiz);
-                const float c1 = __builtin_fmaf(fz[c], iz, -oiz);
+                const float a0 = __builtin_fmaf(nx[c], ix, -onx);
+                const float a1 = __builtin_fmaf(fx[c], ix, -ofx);
+                const float b0 = __builtin_fmaf(ny[c], iy, -ony);
+                const float b1 = __builtin_fmaf(fy[c], iy, -ofy);
+                const float c0 = __builtin_fmaf(nz[c], iz, -onz);
+                const float c1 = __builtin_fmaf(fz[c], iz, -ofz);
                 const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
                 const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
                 tn[c] = t0;

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -184,15 +185,26 @@ void check_camera(const rt_scene* s, const rt_camera* c) {
     if (!c) throw rt::Error{RT_ERR_INVALID_ARGUMENT, "camera is NULL"};
     if (c->width <= 0 || c->height <= 0 || c->width > 65536 || c->height > 65536)
         throw rt::Error{RT_ERR_INVALID_ARGUMENT, "bad image size"};
-    // the fp32 box padding covers camera origins up to 3x the scene's
-    // coordinate magnitude (exactness argument)
-    const double lim = 3.0 * std::max(s->flat.coord_max, 1.0);
     for (int a = 0; a < 3; a++)
-        if (!(std::fabs(c->pos[a]) <= lim)) throw rt::Error{RT_ERR_OUT_OF_RANGE, "camera outside the exact-traversal envelope"};
+        if (!std::isfinite(c->pos[a]) || !std::isfinite(c->dir[a]))
+            throw rt::Error{RT_ERR_INVALID_ARGUMENT, "camera position/direction must be finite"};
+    (void)s;
 }
 
-RtFrameParams frame_params(Replica& r, const rt_camera* c, int row0, int row_stride, int nrows) {
+// World-space margin added to every fp32 slab plane: 2^-19 * (|o|_max +
+// |coordinate|_max) dominates the fp32 rounding of the origin, the reciprocal
+// and the fma (each <= 2^-24 relative) by >= 8x (DESIGN.md "exactness").
+float frame_pad(const rt_scene* s, const rt_camera* c) {
+    double om = std::max({std::fabs(c->pos[0]), std::fabs(c->pos[1]), std::fabs(c->pos[2])});
+    double p = std::ldexp(om + s->flat.coord_max + 1e-30, -19);
+    float f = (float)p;
+    if ((double)f < p) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+}
+
+RtFrameParams frame_params(const rt_scene* s, Replica& r, const rt_camera* c, int row0, int row_stride, int nrows) {
     RtFrameParams fp{};
+    fp.pad = frame_pad(s, c);
     for (int a = 0; a < 3; a++) {
         fp.pos[a] = c->pos[a];
         fp.dir[a] = c->dir[a];
@@ -320,7 +332,7 @@ int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mod
         DevGuard g(device);
         hipStream_t st = (hipStream_t)stream;
         ensure_camera(*r, cam->width, cam->height, st);
-        RtFrameParams fp = frame_params(*r, cam, row0, row_stride, nrows);
+        RtFrameParams fp = frame_params(s, *r, cam, row0, row_stride, nrows);
         fp.hit_id = out->hit_id;
         fp.dist = out->dist;
         fp.hit_pos = out->pos;
@@ -361,7 +373,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         d.hit_count = reinterpret_cast<unsigned long long*>(base + o_cnt);
         ensure_camera(r, cam->width, cam->height, r.stream);
         HIP_TRY(hipMemsetAsync(d.hit_count, 0, 8, r.stream));
-        RtFrameParams fp = frame_params(r, cam, 0, 1, cam->height);
+        RtFrameParams fp = frame_params(s, r, cam, 0, 1, cam->height);
         fp.hit_id = d.hit_id;
         fp.dist = d.dist;
         fp.hit_pos = d.pos;

@@ -5,7 +5,8 @@
 //                hi_y[W] lo_z[W] hi_z[W]) then u32 child refs[W]; one node is
 //                node_bytes(W) = roundup(28*W, 64) bytes (W=8: 256 B, four
 //                64-B lines).  Bounds are the reference's fp64 boxes rounded
-//                outward to fp32 and padded (conservative superset).
+//                outward to fp32 (a conservative superset); the kernel widens
+//                every slab by a per-frame margin (RtFrameParams.pad).
 //   tri32        BVH order, fp32 v0,e1,e2 + pad (48 B)   — fp32 pre-filter
 //   tri64        BVH order, fp64 v0,e1,e2 (72 B)         — exact reference MT
 //   tri_id/rank/leaf  BVH order u32: loader index, reference visit rank,
@@ -59,5 +60,6 @@ struct RtFrameParams {
     double* hit_pos;
     uint8_t* rgb;
     unsigned long long* hit_count;
-    unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits] or NULL
+    unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits, chain_nodes] or NULL
+    float pad;                     // world-space slab margin of the fp32 traversal
 };

@@ -48,7 +48,7 @@ struct Flat {
     int width = 8;                        // W
     uint32_t root_ref = 0;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
-    double pad = 0, coord_max = 0;        // outward padding of fp32 boxes
+    double pad = 0, coord_max = 0;        // max |coordinate| (sizes the per-frame margin)
     std::vector<uint8_t> wide;            // wide nodes, node_bytes(W) each
     uint64_t n_wide = 0;
     std::vector<double> tri64;            // BVH order: v0, e1, e2 (9 doubles)

@@ -73,6 +73,26 @@ class rt_frame_stats_t(C.Structure):
 _lib = None
 
 
+def _share_hip_runtime_with_torch() -> None:
+    """One HIP runtime per process.
+
+    PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7, loaded by
+    torch as "libamdhip64.so" from torch/lib).  If librtmi355x.so were loaded
+    first it would pull /opt/rocm's copy and torch would then map a second
+    runtime that finds no GPU.  Pre-loading torch's file (RTLD_GLOBAL) makes
+    our NEEDED libamdhip64.so.7 bind to it, and torch later reuses the same
+    mapped file.  Without torch installed, /opt/rocm's runtime is used.
+    """
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        C.CDLL(cand, mode=C.RTLD_GLOBAL)
+
+
 def lib() -> C.CDLL:
     """Load librtmi355x.so once (raises if it was not built)."""
     global _lib
@@ -80,6 +100,7 @@ def lib() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RTError(RT_ERR_NO_DEVICE, f"{LIB_PATH} is not built (run __graft_entry__.build())")
+    _share_hip_runtime_with_torch()
     L = C.CDLL(LIB_PATH)
     dp, u64p = C.POINTER(C.c_double), C.POINTER(C.c_uint64)
     L.rt_last_error.restype = C.c_char_p

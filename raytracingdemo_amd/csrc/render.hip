@@ -13,12 +13,15 @@
 //                   src/utils/benchmark.hpp:105-114
 //
 // Two traversal kernels, both exact:
-//   k_trace_exact   fp32 conservative traversal of W-wide nodes (outward-
-//                   rounded, padded boxes; ordered, distance-culled), exact
-//                   fp64 Moller-Trumbore on leaf triangles, and an fp64
+//   k_trace_exact   persistent waves pull 8x8 pixel tiles from an atomic
+//                   queue; fp32 conservative traversal of W-wide nodes
+//                   (outward-rounded boxes, per-frame widened slabs, ordered,
+//                   distance-culled) with the traversal stack in LDS (ring of
+//                   S entries per lane, global spill beyond); exact fp64
+//                   Moller-Trumbore on leaf triangles and an fp64
 //                   re-verification of the reference ancestor chain before a
 //                   candidate may win (the reference only sees a triangle if
-//                   every ancestor's fp64 slab test passes).  Ties in distance
+//                   every ancestor's fp64 slab test passes).  Distance ties
 //                   resolve by the reference visit rank.  See DESIGN.md.
 //   k_trace_literal the reference's own traversal (LIFO, no culling, no
 //                   ordering) in fp64 on the real tree — a cross-check.
@@ -166,19 +169,6 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDev
     if (b.tri >= 0 && fp.hit_count) atomicAdd(fp.hit_count, 1ull);
 }
 
-// Pixel of this lane: each wave64 owns an 8x8 tile; a 256-thread block owns
-// four consecutive tiles along the row.
-__device__ __forceinline__ bool lane_pixel(const RtFrameParams& fp, int& i, int& r) {
-    const int lane = threadIdx.x & 63;
-    const int tiles_x = (fp.W + 7) >> 3;
-    const int tiles_y = (fp.nrows + 7) >> 3;
-    const int tile = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (tile >= tiles_x * tiles_y) return false;
-    i = (tile % tiles_x) * 8 + (lane & 7);
-    r = (tile / tiles_x) * 8 + (lane >> 3);
-    return i < fp.W && r < fp.nrows;
-}
-
 template <int W>
 __device__ __forceinline__ void load_w(float (&d)[W], const float* __restrict__ p) {
     if constexpr (W % 4 == 0) {
@@ -225,13 +215,36 @@ __device__ __forceinline__ bool chain_ok(const RtDevScene& sc, uint32_t leaf, co
     return true;
 }
 
+// Per-lane traversal stack: the top S entries live in LDS (one column per
+// lane: entry e of lane t at lds[e % S][t], conflict-free for ds_read_b64),
+// older entries spill to the lane's slice of a global buffer.
+template <int S>
+struct LaneStack {
+    uint2 (*lds)[256];
+    uint2* spill;
+    int tid;
+    int top;
+    __device__ __forceinline__ void push(uint32_t ref, float t) {
+        const int slot = top & (S - 1);
+        if (top >= S) spill[top - S] = lds[slot][tid];
+        lds[slot][tid] = make_uint2(ref, __float_as_uint(t));
+        top++;
+    }
+    __device__ __forceinline__ uint2 pop() {
+        top--;
+        const int slot = top & (S - 1);
+        const uint2 e = lds[slot][tid];
+        if (top >= S) lds[slot][tid] = spill[top - S];
+        return e;
+    }
+};
+
 // --------------------------------------------------------------------------
-// Fast exact kernel.
+// Fast exact kernel (persistent).
 // --------------------------------------------------------------------------
-template <int W, int SMAX, bool COUNT>
-__global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParams fp) {
-    int i, r;
-    if (!lane_pixel(fp, i, r)) return;
+template <int W, int S, bool COUNT>
+__device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int i, int r,
+                                            LaneStack<S>& st) {
     const int j = fp.row0 + r * fp.row_stride;
     const Ray64 ray = gen_ray(fp, i, j);
 
@@ -265,10 +278,7 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
     uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
     uint32_t chain_leaf = 0xFFFFFFFFu;
     bool chain_res = false;
-
-    uint32_t sref[SMAX];
-    float stm[SMAX];
-    int sp = 0;
+    st.top = 0;
 
     uint32_t cur = sc.root_ref;
     {
@@ -281,7 +291,7 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
         const float tz1 = __builtin_fmaf(iz >= 0.f ? b[5] : b[4], iz, -ofz);
         const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, 0.f));
         const float tf = fminf(fminf(tx1, ty1), tz1);
-        if (!(tn <= tf) || cur == RT_INVALID_REF) cur = RT_INVALID_REF;
+        if (!(tn <= tf)) cur = RT_INVALID_REF;
     }
 
     while (cur != RT_INVALID_REF) {
@@ -324,11 +334,7 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
 #pragma unroll
                     for (int c = 1; c < W; c++)
                         if (c == far_c) far_ref = ref[c];
-                    if (sp < SMAX) {
-                        sref[sp] = far_ref;
-                        stm[sp] = far_t;
-                        sp++;
-                    }
+                    st.push(far_ref, far_t);
                     mask &= ~(1u << far_c);
                 }
                 const int c0 = __builtin_ctz(mask);
@@ -368,10 +374,10 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
         }
         // pop the next subtree still in front of the current best
         cur = RT_INVALID_REF;
-        while (sp > 0) {
-            sp--;
-            if (stm[sp] <= tcull) {
-                cur = sref[sp];
+        while (st.top > 0) {
+            const uint2 e = st.pop();
+            if (__uint_as_float(e.y) <= tcull) {
+                cur = e.x;
                 break;
             }
         }
@@ -389,9 +395,45 @@ __global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParam
     }
 }
 
+// Persistent waves: each wave pulls 8x8 pixel tiles from `tile_ctr` until the
+// shard is exhausted (every wave reaches the exit test each iteration).
+template <int W, int S, bool COUNT>
+__global__ void __launch_bounds__(256) k_trace_exact(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
+    __shared__ uint2 lds[S][256];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int tiles_x = (fp.W + 7) >> 3;
+    const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
+    LaneStack<S> st;
+    st.lds = lds;
+    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
+    st.tid = tid;
+    st.top = 0;
+    for (;;) {
+        int tile = 0;
+        if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);
+        tile = __shfl(tile, 0);
+        if (tile >= tiles) break;
+        const int i = (tile % tiles_x) * 8 + (lane & 7);
+        const int r = (tile / tiles_x) * 8 + (lane >> 3);
+        if (i < fp.W && r < fp.nrows) trace_exact<W, S, COUNT>(sc, fp, i, r, st);
+    }
+}
+
 // --------------------------------------------------------------------------
 // Literal reference traversal (stack_bvh.hpp:611-644) on the real tree.
 // --------------------------------------------------------------------------
+__device__ __forceinline__ bool lane_pixel(const RtFrameParams& fp, int& i, int& r) {
+    const int lane = threadIdx.x & 63;
+    const int tiles_x = (fp.W + 7) >> 3;
+    const int tiles_y = (fp.nrows + 7) >> 3;
+    const int tile = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (tile >= tiles_x * tiles_y) return false;
+    i = (tile % tiles_x) * 8 + (lane & 7);
+    r = (tile / tiles_x) * 8 + (lane >> 3);
+    return i < fp.W && r < fp.nrows;
+}
+
 template <int SMAX, bool COUNT>
 __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFrameParams fp) {
     int i, r;
@@ -442,21 +484,15 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
     }
 }
 
-template <int W, int SMAX>
-hipError_t launch_exact_w(const RtDevScene& sc, const RtFrameParams& fp, bool count, dim3 grid, hipStream_t s) {
-    if (count) hipLaunchKernelGGL((k_trace_exact<W, SMAX, true>), grid, dim3(256), 0, s, sc, fp);
-    else hipLaunchKernelGGL((k_trace_exact<W, SMAX, false>), grid, dim3(256), 0, s, sc, fp);
-    return hipGetLastError();
-}
+constexpr int kLdsStack = 16;  // LDS ring entries per lane (8 B each)
 
 template <int W>
-hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, bool count, dim3 grid, hipStream_t s) {
-    const uint32_t need = sc.stack_bound;
-    if (need <= 32) return launch_exact_w<W, 32>(sc, fp, count, grid, s);
-    if (need <= 64) return launch_exact_w<W, 64>(sc, fp, count, grid, s);
-    if (need <= 128) return launch_exact_w<W, 128>(sc, fp, count, grid, s);
-    if (need <= 256) return launch_exact_w<W, 256>(sc, fp, count, grid, s);
-    return hipErrorInvalidValue;
+hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
+                        hipStream_t s) {
+    const dim3 grid((unsigned)aux.grid);
+    if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true>), grid, dim3(256), 0, s, sc, fp, aux);
+    else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false>), grid, dim3(256), 0, s, sc, fp, aux);
+    return hipGetLastError();
 }
 
 template <int SMAX>
@@ -470,24 +506,44 @@ hipError_t launch_literal_s(const RtDevScene& sc, const RtFrameParams& fp, bool 
 
 namespace rt {
 
+// Blocks per CU the persistent exact kernel is launched with.
+int exact_blocks_per_cu(int width) {
+    int n = 0;
+    hipError_t e = hipSuccess;
+    switch (width) {
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<2, kLdsStack, false>, 256, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<4, kLdsStack, false>, 256, 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<8, kLdsStack, false>, 256, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<16, kLdsStack, false>, 256, 0); break;
+    }
+    if (e != hipSuccess || n < 1) n = 1;
+    return n < 8 ? n : 8;
+}
+
+int exact_lds_stack() { return kLdsStack; }
+
 // Host entry: validates the launch geometry against what the kernels assume
-// and dispatches on node width / stack bound.  mode 0 = exact fast, 1 = literal.
-hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count, hipStream_t s,
-                        uint32_t literal_stack) {
+// and dispatches on node width.  mode 0 = exact fast, 1 = literal.
+hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
+                        hipStream_t s, uint32_t literal_stack) {
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
-    const long tiles = (long)((fp.W + 7) / 8) * (long)((fp.nrows + 7) / 8);
-    const dim3 grid((unsigned)((tiles + 3) / 4));
     if (mode == 1) {
+        const long tiles = (long)((fp.W + 7) / 8) * (long)((fp.nrows + 7) / 8);
+        const dim3 grid((unsigned)((tiles + 3) / 4));
         if (literal_stack <= 64) return launch_literal_s<64>(sc, fp, count, grid, s);
         if (literal_stack <= 256) return launch_literal_s<256>(sc, fp, count, grid, s);
         if (literal_stack <= 1024) return launch_literal_s<1024>(sc, fp, count, grid, s);
         return hipErrorInvalidValue;
     }
+    if (aux.spill_cap + kLdsStack < sc.stack_bound || !aux.tile_ctr || !aux.spill || aux.grid <= 0)
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
     switch (sc.width) {
-        case 2: return launch_exact<2>(sc, fp, count, grid, s);
-        case 4: return launch_exact<4>(sc, fp, count, grid, s);
-        case 8: return launch_exact<8>(sc, fp, count, grid, s);
-        case 16: return launch_exact<16>(sc, fp, count, grid, s);
+        case 2: return launch_exact<2>(sc, fp, aux, count, s);
+        case 4: return launch_exact<4>(sc, fp, aux, count, s);
+        case 8: return launch_exact<8>(sc, fp, aux, count, s);
+        case 16: return launch_exact<16>(sc, fp, aux, count, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -16,8 +16,10 @@
 #include "rt_internal.h"
 
 namespace rt {
-hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count, hipStream_t s,
-                        uint32_t literal_stack);
+hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
+                        hipStream_t s, uint32_t literal_stack);
+int exact_blocks_per_cu(int width);
+int exact_lds_stack();
 }
 
 namespace {
@@ -66,6 +68,13 @@ struct Replica {
     size_t frame_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // persistent-kernel resources; every launch on this replica is serialised
+    // through `stream` (the work-queue head and the stack spill are shared)
+    uint32_t* d_tiles = nullptr;
+    uint64_t* d_spill = nullptr;
+    uint32_t spill_cap = 0;
+    int grid = 0;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
 };
 
 }  // namespace
@@ -89,6 +98,10 @@ void free_replica(Replica& r) {
     if (r.d_cam) hipFree(r.d_cam);
     if (r.d_counters) hipFree(r.d_counters);
     if (r.frame) hipFree(r.frame);
+    if (r.d_tiles) hipFree(r.d_tiles);
+    if (r.d_spill) hipFree(r.d_spill);
+    if (r.ev_in) hipEventDestroy(r.ev_in);
+    if (r.ev_out) hipEventDestroy(r.ev_out);
     if (r.ev0) hipEventDestroy(r.ev0);
     if (r.ev1) hipEventDestroy(r.ev1);
     if (r.stream) hipStreamDestroy(r.stream);
@@ -163,6 +176,13 @@ void upload_one(rt_scene* s, int device) {
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
+    HIP_TRY(hipEventCreateWithFlags(&r.ev_in, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&r.ev_out, hipEventDisableTiming));
+    r.grid = prop.multiProcessorCount * rt::exact_blocks_per_cu(f.width);
+    const int S = rt::exact_lds_stack();
+    r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
+    HIP_TRY(hipMalloc(&r.d_tiles, 256));
+    HIP_TRY(hipMalloc(&r.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
     s->reps.push_back(r);
 }
 
@@ -218,6 +238,15 @@ RtFrameParams frame_params(const rt_scene* s, Replica& r, const rt_camera* c, in
     fp.row_stride = row_stride;
     fp.nrows = nrows;
     return fp;
+}
+
+RtLaunchAux aux_of(Replica& r) {
+    RtLaunchAux a{};
+    a.tile_ctr = r.d_tiles;
+    a.spill = r.d_spill;
+    a.spill_cap = r.spill_cap;
+    a.grid = r.grid;
+    return a;
 }
 
 uint32_t literal_stack_bound(const rt_scene* s) {
@@ -339,7 +368,14 @@ int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mod
         fp.rgb = out->rgb;
         fp.hit_count = out->hit_count;
         fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
-        HIP_TRY(rt::launch_trace(r->dev, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, literal_stack_bound(s)));
+        // serialise on the replica's stream: the caller's stream waits for it
+        std::lock_guard<std::mutex> lk(s->mu);
+        HIP_TRY(hipEventRecord(r->ev_in, st));
+        HIP_TRY(hipStreamWaitEvent(r->stream, r->ev_in, 0));
+        HIP_TRY(rt::launch_trace(r->dev, fp, aux_of(*r), mode, (flags & RT_FLAG_COUNT) != 0, r->stream,
+                                 literal_stack_bound(s)));
+        HIP_TRY(hipEventRecord(r->ev_out, r->stream));
+        HIP_TRY(hipStreamWaitEvent(st, r->ev_out, 0));
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
@@ -380,7 +416,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         fp.rgb = d.rgb;
         fp.hit_count = d.hit_count;
         HIP_TRY(hipEventRecord(r.ev0, r.stream));
-        HIP_TRY(rt::launch_trace(r.dev, fp, mode, false, r.stream, literal_stack_bound(s)));
+        HIP_TRY(rt::launch_trace(r.dev, fp, aux_of(r), mode, false, r.stream, literal_stack_bound(s)));
         HIP_TRY(hipEventRecord(r.ev1, r.stream));
         if (out->hit_id) HIP_TRY(hipMemcpyAsync(out->hit_id, d.hit_id, npx * 4, hipMemcpyDeviceToHost, r.stream));
         if (out->dist) HIP_TRY(hipMemcpyAsync(out->dist, d.dist, npx * 8, hipMemcpyDeviceToHost, r.stream));

@@ -49,6 +49,14 @@ struct RtDevScene {
     uint32_t stack_bound;
 };
 
+// Per-launch resources of the persistent exact kernel.
+struct RtLaunchAux {
+    uint32_t* tile_ctr;   // work-queue head, zeroed before every launch
+    uint64_t* spill;      // traversal-stack spill: spill_cap entries per lane
+    uint32_t spill_cap;
+    int32_t grid;         // persistent blocks (CUs x resident blocks per CU)
+};
+
 struct RtFrameParams {
     double pos[3], dir[3], right[3], up[3];
     const double* px;  // W pixel-plane x coefficients (camera.hpp:35)

@@ -32,6 +32,15 @@ for s in $STEPS; do
                    -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
                    -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu ;;
+        list)  run list 120 rocprofv3 -L ;;
+        sq)    run sq1 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+                   SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --output-format csv -d gpurun_out/sq -o sq1 \
+                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \
+               run sq2 900 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM \
+                   SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS --output-format csv \
+                   -d gpurun_out/sq -o sq2 -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \
+               run sq3 900 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum \
+                   --output-format csv -d gpurun_out/sq -o sq3 -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -467,7 +467,7 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
 
     // --- per-triangle data in BVH order
     const uint64_t n = s.n;
-    f.tri64.resize(n * 9);
+    f.tri64.resize(n * RT_TRI64_DOUBLES);
     f.tri32.resize(n * 12, 0.0f);
     f.tri_id.resize(n);
     f.tri_rank.resize(n);
@@ -475,7 +475,7 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     for (uint64_t i = 0; i < n; i++) {
         uint32_t id = t.order[i];
         const double* p = s.v.data() + (size_t)id * 9;
-        double* q = f.tri64.data() + i * 9;
+        double* q = f.tri64.data() + i * RT_TRI64_DOUBLES;
         q[0] = p[0]; q[1] = p[1]; q[2] = p[2];
         q[3] = p[3] - p[0]; q[4] = p[4] - p[1]; q[5] = p[5] - p[2];  // edge1 = v1 - v0 (triangle.hpp:42)
         q[6] = p[6] - p[0]; q[7] = p[7] - p[1]; q[8] = p[8] - p[2];  // edge2 = v2 - v0
@@ -513,6 +513,12 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
                 for (int64_t i = nd.begin; i < nd.end; i++) { f.tri_rank[i] = rank++; f.tri_leaf[i] = (uint32_t)ni; }
             for (int32_t c : nd.kids) st.push_back(c);
         }
+    }
+    // rank and leaf ride in the fp64 record's 10th slot (one 80-B load burst)
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(f.tri64.data() + i * RT_TRI64_DOUBLES + 9);
+        w[0] = f.tri_rank[i];
+        w[1] = f.tri_leaf[i];
     }
     // --- wide nodes
     Flattener F(s, t, f);

@@ -215,6 +215,27 @@ __device__ __forceinline__ bool chain_ok(const RtDevScene& sc, uint32_t leaf, co
     return true;
 }
 
+// Sufficient condition for chain_ok without walking the chain: if the hit
+// point p = fl(o + d t) lies inside the (real) leaf box with a margin
+// m_a = 2^-48 (|mn_a| + |mx_a| + |o_a| + |p_a|) on every axis and no direction
+// component is zero, every fp64 slab test on the root path passes.  Proof
+// sketch (DESIGN.md "exactness"): |p_a - (o_a + d_a t)| <= 2^-52(|o_a|+|d_a t|)
+// and each computed slab bound is within 2^-51 |mn_a - o_a| / |d_a| of its
+// real value, so every computed near bound is < t < every computed far bound;
+// ancestor boxes contain the leaf box, so their margins are no smaller.
+__device__ __forceinline__ bool chain_fast_ok(const double* __restrict__ b, const Ray64& r, double px, double py,
+                                              double pz) {
+    if (r.dx == 0.0 || r.dy == 0.0 || r.dz == 0.0) return false;
+    const double o[3] = {r.ox, r.oy, r.oz}, p[3] = {px, py, pz};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double m = 0x1p-48 * (__builtin_fabs(b[a]) + __builtin_fabs(b[3 + a]) + __builtin_fabs(o[a]) +
+                                    __builtin_fabs(p[a]));
+        if (!(p[a] - b[a] >= m && b[3 + a] - p[a] >= m)) return false;
+    }
+    return true;
+}
+
 // Per-lane traversal stack: the top S entries live in LDS (one column per
 // lane: entry e of lane t at lds[e % S][t], conflict-free for ds_read_b64),
 // older entries spill to the lane's slice of a global buffer.
@@ -270,117 +291,131 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
     const int nzo = iz >= 0.f ? 4 * W : 5 * W, fzo = iz >= 0.f ? 5 * W : 4 * W;
 
     Best best;
-    best.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
-    best.rank = 0xFFFFFFFFu;
-    best.tri = -1;
-    best.px = best.py = best.pz = 0.0;
-    float tcull = __builtin_huge_valf();
     uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
-    uint32_t chain_leaf = 0xFFFFFFFFu;
-    bool chain_res = false;
-    st.top = 0;
+    // pass 0: traverse with the ancestor re-verification deferred to the
+    //         winner (one check per ray, usually the margin test alone);
+    // pass 1: only if that winner is invisible to the reference — traverse
+    //         again verifying every would-be winner inline.
+    for (int pass = 0; pass < 2; pass++) {
+        best.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
+        best.rank = 0xFFFFFFFFu;
+        best.tri = -1;
+        best.px = best.py = best.pz = 0.0;
+        float tcull = __builtin_huge_valf();
+        uint32_t chain_leaf = 0xFFFFFFFFu;
+        bool chain_res = false;
+        st.top = 0;
 
-    uint32_t cur = sc.root_ref;
-    {
-        const float* b = sc.root_box;
-        const float tx0 = __builtin_fmaf(ix >= 0.f ? b[0] : b[1], ix, -onx);
-        const float tx1 = __builtin_fmaf(ix >= 0.f ? b[1] : b[0], ix, -ofx);
-        const float ty0 = __builtin_fmaf(iy >= 0.f ? b[2] : b[3], iy, -ony);
-        const float ty1 = __builtin_fmaf(iy >= 0.f ? b[3] : b[2], iy, -ofy);
-        const float tz0 = __builtin_fmaf(iz >= 0.f ? b[4] : b[5], iz, -onz);
-        const float tz1 = __builtin_fmaf(iz >= 0.f ? b[5] : b[4], iz, -ofz);
-        const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, 0.f));
-        const float tf = fminf(fminf(tx1, ty1), tz1);
-        if (!(tn <= tf)) cur = RT_INVALID_REF;
-    }
+        uint32_t cur = sc.root_ref;
+        {
+            const float* b = sc.root_box;
+            const float tx0 = __builtin_fmaf(ix >= 0.f ? b[0] : b[1], ix, -onx);
+            const float tx1 = __builtin_fmaf(ix >= 0.f ? b[1] : b[0], ix, -ofx);
+            const float ty0 = __builtin_fmaf(iy >= 0.f ? b[2] : b[3], iy, -ony);
+            const float ty1 = __builtin_fmaf(iy >= 0.f ? b[3] : b[2], iy, -ofy);
+            const float tz0 = __builtin_fmaf(iz >= 0.f ? b[4] : b[5], iz, -onz);
+            const float tz1 = __builtin_fmaf(iz >= 0.f ? b[5] : b[4], iz, -ofz);
+            const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, 0.f));
+            const float tf = fminf(fminf(tx1, ty1), tz1);
+            if (!(tn <= tf)) cur = RT_INVALID_REF;
+        }
 
-    while (cur != RT_INVALID_REF) {
-        if (!(cur & RT_LEAF_BIT)) {
-            if (COUNT) n_nodes++;
-            const float* nb = reinterpret_cast<const float*>(sc.nodes + (size_t)cur * sc.node_bytes);
-            float nx[W], fx[W], ny[W], fy[W], nz[W], fz[W];
-            uint32_t ref[W];
-            load_w<W>(nx, nb + nxo);
-            load_w<W>(fx, nb + fxo);
-            load_w<W>(ny, nb + nyo);
-            load_w<W>(fy, nb + fyo);
-            load_w<W>(nz, nb + nzo);
-            load_w<W>(fz, nb + fzo);
-            load_refs<W>(ref, reinterpret_cast<const uint32_t*>(nb + 6 * W));
-            float tn[W];
-            uint32_t mask = 0;
+        while (cur != RT_INVALID_REF) {
+            if (!(cur & RT_LEAF_BIT)) {
+                if (COUNT) n_nodes++;
+                const float* nb = reinterpret_cast<const float*>(sc.nodes + (size_t)cur * sc.node_bytes);
+                float nx[W], fx[W], ny[W], fy[W], nz[W], fz[W];
+                uint32_t ref[W];
+                load_w<W>(nx, nb + nxo);
+                load_w<W>(fx, nb + fxo);
+                load_w<W>(ny, nb + nyo);
+                load_w<W>(fy, nb + fyo);
+                load_w<W>(nz, nb + nzo);
+                load_w<W>(fz, nb + fzo);
+                load_refs<W>(ref, reinterpret_cast<const uint32_t*>(nb + 6 * W));
+                float tn[W];
+                uint32_t mask = 0;
 #pragma unroll
-            for (int c = 0; c < W; c++) {
-                const float a0 = __builtin_fmaf(nx[c], ix, -onx);
-                const float a1 = __builtin_fmaf(fx[c], ix, -ofx);
-                const float b0 = __builtin_fmaf(ny[c], iy, -ony);
-                const float b1 = __builtin_fmaf(fy[c], iy, -ofy);
-                const float c0 = __builtin_fmaf(nz[c], iz, -onz);
-                const float c1 = __builtin_fmaf(fz[c], iz, -ofz);
-                const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
-                const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
-                tn[c] = t0;
-                if (t0 <= t1 && ref[c] != RT_INVALID_REF) mask |= 1u << c;
-            }
-            if (mask) {
-                // push all but the nearest, farthest first
-                while (__builtin_popcount(mask) > 1) {
-                    float far_t = -1.f;
-                    int far_c = 0;
+                for (int c = 0; c < W; c++) {
+                    const float a0 = __builtin_fmaf(nx[c], ix, -onx);
+                    const float a1 = __builtin_fmaf(fx[c], ix, -ofx);
+                    const float b0 = __builtin_fmaf(ny[c], iy, -ony);
+                    const float b1 = __builtin_fmaf(fy[c], iy, -ofy);
+                    const float c0 = __builtin_fmaf(nz[c], iz, -onz);
+                    const float c1 = __builtin_fmaf(fz[c], iz, -ofz);
+                    const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
+                    const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
+                    tn[c] = t0;
+                    if (t0 <= t1 && ref[c] != RT_INVALID_REF) mask |= 1u << c;
+                }
+                if (mask) {
+                    // push all but the nearest, farthest first
+                    while (__builtin_popcount(mask) > 1) {
+                        float far_t = -1.f;
+                        int far_c = 0;
 #pragma unroll
-                    for (int c = 0; c < W; c++)
-                        if (((mask >> c) & 1u) && tn[c] > far_t) { far_t = tn[c]; far_c = c; }
-                    uint32_t far_ref = ref[0];
+                        for (int c = 0; c < W; c++)
+                            if (((mask >> c) & 1u) && tn[c] > far_t) { far_t = tn[c]; far_c = c; }
+                        uint32_t far_ref = ref[0];
+#pragma unroll
+                        for (int c = 1; c < W; c++)
+                            if (c == far_c) far_ref = ref[c];
+                        st.push(far_ref, far_t);
+                        mask &= ~(1u << far_c);
+                    }
+                    const int c0 = __builtin_ctz(mask);
+                    uint32_t nxt = ref[0];
 #pragma unroll
                     for (int c = 1; c < W; c++)
-                        if (c == far_c) far_ref = ref[c];
-                    st.push(far_ref, far_t);
-                    mask &= ~(1u << far_c);
+                        if (c == c0) nxt = ref[c];
+                    cur = nxt;
+                    continue;
                 }
-                const int c0 = __builtin_ctz(mask);
-                uint32_t nxt = ref[0];
-#pragma unroll
-                for (int c = 1; c < W; c++)
-                    if (c == c0) nxt = ref[c];
-                cur = nxt;
-                continue;
+            } else {
+                const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+                const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+                for (uint32_t q = first; q < first + cnt; q++) {
+                    if (COUNT) n_tris++;
+                    const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)q;
+                    double t;
+                    if (!mt64(T, ray, t)) continue;
+                    double hx, hy, hz;
+                    const double d = hit_dist(ray, t, hx, hy, hz);
+                    const uint2 rl = *reinterpret_cast<const uint2*>(T + 9);  // {rank, leaf}
+                    if (!(d < best.dist || (d == best.dist && rl.x < best.rank))) continue;
+                    if (pass == 1) {
+                        if (rl.y != chain_leaf) {
+                            if (COUNT) n_chain++;
+                            chain_leaf = rl.y;
+                            chain_res = chain_ok(sc, rl.y, ray, n_chain_nodes);
+                        }
+                        if (!chain_res) continue;
+                    }
+                    best.dist = d;
+                    best.rank = rl.x;
+                    best.tri = (int32_t)q;
+                    best.px = hx;
+                    best.py = hy;
+                    best.pz = hz;
+                    tcull = round_up_f(d * (1.0 + 0x1p-20));
+                }
             }
-        } else {
-            const uint32_t first = cur & RT_LEAF_FIRST_MASK;
-            const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
-            for (uint32_t q = first; q < first + cnt; q++) {
-                if (COUNT) n_tris++;
-                double t;
-                if (!mt64(sc.tri64 + 9 * (size_t)q, ray, t)) continue;
-                double hx, hy, hz;
-                const double d = hit_dist(ray, t, hx, hy, hz);
-                const uint32_t rk = sc.tri_rank[q];
-                if (!(d < best.dist || (d == best.dist && rk < best.rank))) continue;
-                const uint32_t leaf = sc.tri_leaf[q];
-                if (leaf != chain_leaf) {
-                    if (COUNT) n_chain++;
-                    chain_leaf = leaf;
-                    chain_res = chain_ok(sc, leaf, ray, n_chain_nodes);
+            // pop the next subtree still in front of the current best
+            cur = RT_INVALID_REF;
+            while (st.top > 0) {
+                const uint2 e = st.pop();
+                if (__uint_as_float(e.y) <= tcull) {
+                    cur = e.x;
+                    break;
                 }
-                if (!chain_res) continue;
-                best.dist = d;
-                best.rank = rk;
-                best.tri = (int32_t)q;
-                best.px = hx;
-                best.py = hy;
-                best.pz = hz;
-                tcull = round_up_f(d * (1.0 + 0x1p-20));
             }
         }
-        // pop the next subtree still in front of the current best
-        cur = RT_INVALID_REF;
-        while (st.top > 0) {
-            const uint2 e = st.pop();
-            if (__uint_as_float(e.y) <= tcull) {
-                cur = e.x;
-                break;
-            }
-        }
+        if (pass == 1 || best.tri < 0) break;
+        // deferred re-verification of the winner's reference ancestor chain
+        const uint32_t leaf = reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + 9)->y;
+        if (COUNT) n_chain++;
+        if (chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, best.px, best.py, best.pz)) break;
+        if (chain_ok(sc, leaf, ray, n_chain_nodes)) break;
     }
 
     const size_t o = (size_t)r * fp.W + i;
@@ -459,7 +494,7 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
             for (uint32_t q = b; q < e; q++) {
                 if (COUNT) n_tris++;
                 double t;
-                if (!mt64(sc.tri64 + 9 * (size_t)q, ray, t)) continue;
+                if (!mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)q, ray, t)) continue;
                 double hx, hy, hz;
                 const double d = hit_dist(ray, t, hx, hy, hz);
                 if (d < best.dist) {

@@ -8,7 +8,8 @@
 //                outward to fp32 (a conservative superset); the kernel widens
 //                every slab by a per-frame margin (RtFrameParams.pad).
 //   tri32        BVH order, fp32 v0,e1,e2 + pad (48 B)   — fp32 pre-filter
-//   tri64        BVH order, fp64 v0,e1,e2 (72 B)         — exact reference MT
+//   tri64        BVH order, fp64 v0,e1,e2 + u32 visit rank + u32 real leaf
+//                (80 B)                                  — exact reference MT
 //   tri_id/rank/leaf  BVH order u32: loader index, reference visit rank,
 //                real leaf node (for the ancestor re-verification)
 //   rbox/rparent real reference nodes: fp64 box (48 B) + parent
@@ -20,6 +21,7 @@
 #define RT_INVALID_REF 0xFFFFFFFFu
 #define RT_LEAF_FIRST_MASK 0x07FFFFFFu
 #define RT_LEAF_MAX_FIRST 0x07FFFFFFu
+#define RT_TRI64_DOUBLES 10  // v0, e1, e2 (9 doubles) + {u32 rank, u32 leaf}: 80 B
 
 #ifdef __cplusplus
 static inline constexpr uint32_t rt_node_bytes(int W) { return (uint32_t)((28 * W + 63) / 64 * 64); }
@@ -31,7 +33,7 @@ static inline constexpr uint32_t rt_make_leaf(uint32_t first, uint32_t count) {
 struct RtDevScene {
     const uint8_t* nodes;
     const float* tri32;      // 12 floats per triangle
-    const double* tri64;     // 9 doubles per triangle
+    const double* tri64;     // RT_TRI64_DOUBLES per triangle: v0,e1,e2,{rank,leaf}
     const uint32_t* tri_id;
     const uint32_t* tri_rank;
     const uint32_t* tri_leaf;

@@ -31,7 +31,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec (primary, 1spp) on Sponza 1920×1080; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-TRI_BYTES = 72         # fp64 v0, e1, e2 read per Moller-Trumbore test
+TRI32_BYTES = 48       # fp32 pre-filter record (v0, e1, e2 + 3 bounds) per pre-test
+TRI64_BYTES = 80       # fp64 record (v0, e1, e2, rank, leaf) per exact Moller-Trumbore test
 CHAIN_BYTES = 52       # fp64 box (48 B) + parent (4 B) per re-verified ancestor
 OUT_BYTES = 7          # u32 hit-id + 3 B rgb written per ray
 CAM_BYTES = 16         # px[i] + py[j] per ray
@@ -150,7 +151,7 @@ def main():
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
     launches = F
-    alg_bytes_per_launch = (cs["node_fetches"] * st["node_bytes"] + cs["tri_tests"] * TRI_BYTES +
+    alg_bytes_per_launch = (cs["node_fetches"] * st["node_bytes"] + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
                             cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * (OUT_BYTES + CAM_BYTES)) / launches
 
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
@@ -203,10 +204,12 @@ def main():
                          "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(alg_bytes_per_launch),
                          "per_ray": {"node_fetches": round(cs["node_fetches"] / max(cs["rays"], 1), 3),
-                                     "tri_tests": round(cs["tri_tests"] / max(cs["rays"], 1), 3),
+                                     "tri_prefilter": round(cs["tri_prefilter"] / max(cs["rays"], 1), 3),
+                                     "tri_tests_fp64": round(cs["tri_tests"] / max(cs["rays"], 1), 3),
                                      "chain_checks": round(cs["chain_checks"] / max(cs["rays"], 1), 4),
                                      "chain_nodes": round(cs["chain_nodes"] / max(cs["rays"], 1), 4),
-                                     "node_bytes": st["node_bytes"], "tri_bytes": TRI_BYTES}},
+                                     "node_bytes": st["node_bytes"], "tri32_bytes": TRI32_BYTES,
+                                     "tri64_bytes": TRI64_BYTES}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

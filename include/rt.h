@@ -107,6 +107,7 @@ typedef struct {
     uint64_t chain_checks;  /* fp64 ancestor-chain re-verifications  */
     uint64_t hits;
     uint64_t chain_nodes;   /* fp64 ancestor boxes loaded by those checks */
+    uint64_t tri_prefilter; /* fp32 conservative triangle pre-tests     */
 } rt_frame_stats_t;
 
 /* objl::Loader + ObjectLoader::loadFromFile (object_loader.hpp:14-70,

@@ -479,8 +479,19 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
         q[0] = p[0]; q[1] = p[1]; q[2] = p[2];
         q[3] = p[3] - p[0]; q[4] = p[4] - p[1]; q[5] = p[5] - p[2];  // edge1 = v1 - v0 (triangle.hpp:42)
         q[6] = p[6] - p[0]; q[7] = p[7] - p[1]; q[8] = p[8] - p[2];  // edge2 = v2 - v0
+        // fp32 pre-filter record: v0, e1, e2 rounded to nearest, then the
+        // magnitudes its error bounds need, rounded up: max|e1_i|, max|e2_i|,
+        // max|v0_i| (render.hip tri_prefilter)
         float* r = f.tri32.data() + i * 12;
         for (int k = 0; k < 9; k++) r[k] = (float)q[k];
+        auto up = [](double x) {
+            float v = (float)x;
+            if ((double)v < x) v = std::nextafter(v, std::numeric_limits<float>::infinity());
+            return v;
+        };
+        r[9] = up(std::max({std::fabs(q[3]), std::fabs(q[4]), std::fabs(q[5])}));
+        r[10] = up(std::max({std::fabs(q[6]), std::fabs(q[7]), std::fabs(q[8])}));
+        r[11] = up(std::max({std::fabs(q[0]), std::fabs(q[1]), std::fabs(q[2])}));
         f.tri_id[i] = id;
     }
     // --- real nodes (fp64 box + parent) and reference visit ranks

@@ -89,6 +89,49 @@ __device__ __forceinline__ bool mt64(const double* __restrict__ T, const Ray64& 
     return true;
 }
 
+// Conservative fp32 pre-filter of Triangle::intersect.  Returns false only
+// when the exact fp64 test must reject (u < 0, v < 0, u+v > 1 or t < 0), or
+// the hit lies beyond `tcull`.  Record: v0, e1, e2 (fp32, nearest) and, rounded
+// up, M1 = max|e1_i|, M2 = max|e2_i|, Cv = max|v0_i|; `co` = max|o_i| rounded up.
+// Every computed MT quantity X (a, U = s.h, V = d.q, T = e2.q) is within a
+// quarter of its budget errX of the exact real value, with
+//   G = 256 Ms + 64 (co + Cv)     (Ms = max|s_i|, s = o - v0 in fp32)
+//   errA = 256 u M1 M2, errU = u M2 G, errV = u M1 G, errT = u M1 M2 G
+// (u = 2^-24; |d_i| <= 1; each quantity is a 3-term dot of products of inputs
+// carrying <= 2u relative rounding, plus the absolute rounding of s).  A
+// rejection therefore leaves >= 3/4 of a budget between the real value and the
+// decision boundary — far beyond the fp64 test's own rounding (2^-50 scale) —
+// so the fp64 test would reject too.  DESIGN.md "exactness" has the details.
+__device__ __forceinline__ bool tri_prefilter(const float4 A, const float4 B, const float4 C, float ox, float oy,
+                                              float oz, float dx, float dy, float dz, float co, float tcull) {
+    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = C.x;
+    const float M1 = C.y, M2 = C.z, Cv = C.w;
+    const float sx = ox - A.x, sy = oy - A.y, sz = oz - A.z;
+    const float hx = __builtin_fmaf(dy, e2z, -dz * e2y);
+    const float hy = __builtin_fmaf(dz, e2x, -dx * e2z);
+    const float hz = __builtin_fmaf(dx, e2y, -dy * e2x);
+    const float a = __builtin_fmaf(e1x, hx, __builtin_fmaf(e1y, hy, e1z * hz));
+    const float U = __builtin_fmaf(sx, hx, __builtin_fmaf(sy, hy, sz * hz));
+    const float qx = __builtin_fmaf(sy, e1z, -sz * e1y);
+    const float qy = __builtin_fmaf(sz, e1x, -sx * e1z);
+    const float qz = __builtin_fmaf(sx, e1y, -sy * e1x);
+    const float V = __builtin_fmaf(dx, qx, __builtin_fmaf(dy, qy, dz * qz));
+    const float T = __builtin_fmaf(e2x, qx, __builtin_fmaf(e2y, qy, e2z * qz));
+    const float Ms = fmaxf(fmaxf(__builtin_fabsf(sx), __builtin_fabsf(sy)), __builtin_fabsf(sz));
+    const float u = 0x1p-24f;
+    const float G = __builtin_fmaf(256.f, Ms, 64.f * (co + Cv));
+    const float errA = 256.f * u * M1 * M2;
+    const float errU = u * M2 * G, errV = u * M1 * G, errT = u * M1 * M2 * G;
+    const float aa = __builtin_fabsf(a);
+    if (!(aa > errA)) return true;  // sign of the determinant uncertain: let fp64 decide
+    const float sg = a > 0.f ? 1.f : -1.f;
+    const float Us = sg * U, Vs = sg * V, Ts = sg * T;
+    if (Us < -errU || Vs < -errV || Ts < -errT) return false;
+    if (Us + Vs > aa + errU + errV + errA) return false;
+    if (Ts - errT > tcull * (aa + errA)) return false;  // t > tcull: cannot improve
+    return true;
+}
+
 // main.cpp:332-337: d = dir + up*py + right*px; d *= 1/|d|; Ray{pos, d}
 __device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) {
     const double px = fp.px[i], py = fp.py[j];
@@ -289,9 +332,17 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
     const int nxo = ix >= 0.f ? 0 : W, fxo = ix >= 0.f ? W : 0;
     const int nyo = iy >= 0.f ? 2 * W : 3 * W, fyo = iy >= 0.f ? 3 * W : 2 * W;
     const int nzo = iz >= 0.f ? 4 * W : 5 * W, fzo = iz >= 0.f ? 5 * W : 4 * W;
+    // fp32 direction and origin magnitude for the triangle pre-filter
+    const float dx32 = (float)ray.dx, dy32 = (float)ray.dy, dz32 = (float)ray.dz;
+    const double omax = __builtin_fmax(__builtin_fmax(__builtin_fabs(ray.ox), __builtin_fabs(ray.oy)),
+                                       __builtin_fabs(ray.oz));
+    const float co32 = round_up_f(omax + 1e-30);
+    // distance -> ray-parameter slack for culling: dist = |fl(o + d t) - o|
+    // differs from t by <= 2^-52 |o| + 2^-50 t, covered by tslack + 2^-20 t
+    const double tslack = 0x1p-40 * (omax + 1.0);
 
     Best best;
-    uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
+    uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_pre = 0;
     // pass 0: traverse with the ancestor re-verification deferred to the
     //         winner (one check per ray, usually the margin test alone);
     // pass 1: only if that winner is invisible to the reference — traverse
@@ -375,6 +426,9 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
                 const uint32_t first = cur & RT_LEAF_FIRST_MASK;
                 const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
                 for (uint32_t q = first; q < first + cnt; q++) {
+                    const float4* R = reinterpret_cast<const float4*>(sc.tri32 + 12 * (size_t)q);
+                    if (COUNT) n_pre++;
+                    if (!tri_prefilter(R[0], R[1], R[2], ox, oy, oz, dx32, dy32, dz32, co32, tcull)) continue;
                     if (COUNT) n_tris++;
                     const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)q;
                     double t;
@@ -397,7 +451,7 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
                     best.px = hx;
                     best.py = hy;
                     best.pz = hz;
-                    tcull = round_up_f(d * (1.0 + 0x1p-20));
+                    tcull = round_up_f((d + tslack) * (1.0 + 0x1p-20));
                 }
             }
             // pop the next subtree still in front of the current best
@@ -427,6 +481,7 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
         atomicAdd(&fp.counters[3], (unsigned long long)n_chain);
         if (best.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
         atomicAdd(&fp.counters[5], (unsigned long long)n_chain_nodes);
+        atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
     }
 }
 

@@ -449,6 +449,7 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->chain_checks = c[3];
         out->hits = c[4];
         out->chain_nodes = c[5];
+        out->tri_prefilter = c[6];
         if (reset) HIP_TRY(hipMemset(r.d_counters, 0, sizeof c));
         return RT_OK;
     } catch (const rt::Error& e) {

@@ -32,7 +32,7 @@ static inline constexpr uint32_t rt_make_leaf(uint32_t first, uint32_t count) {
 
 struct RtDevScene {
     const uint8_t* nodes;
-    const float* tri32;      // 12 floats per triangle
+    const float* tri32;      // 12 floats per triangle: v0,e1,e2, max|e1|,max|e2|,max|v0|
     const double* tri64;     // RT_TRI64_DOUBLES per triangle: v0,e1,e2,{rank,leaf}
     const uint32_t* tri_id;
     const uint32_t* tri_rank;

@@ -1,0 +1,282 @@
+// Device helpers shared by the gfx950 kernels (render.hip): the reference's
+// fp64 arithmetic (slab test, Moller-Trumbore, ray generation, shading) in
+// exact operation order, the conservative fp32 pre-filter, the ancestor-
+// chain re-verification and the LDS traversal stack.  Included by one TU
+// compiled with -ffp-contract=off.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_device.h"
+
+namespace rtk {
+
+
+struct Ray64 {
+    double ox, oy, oz;
+    double dx, dy, dz;
+    double ix, iy, iz;
+};
+
+__device__ __forceinline__ double smin(double a, double b) { return (b < a) ? b : a; }  // std::min
+__device__ __forceinline__ double smax(double a, double b) { return (a < b) ? b : a; }  // std::max
+__device__ __forceinline__ double sclamp(double v, double lo, double hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
+
+// AABB::hit (aabb.hpp:32-49); b = {mn.x, mn.y, mn.z, mx.x, mx.y, mx.z}
+__device__ __forceinline__ bool box_hit64(const double* __restrict__ b, const Ray64& r) {
+    double tx1 = (b[0] - r.ox) * r.ix;
+    double tx2 = (b[3] - r.ox) * r.ix;
+    double tmin = smin(tx1, tx2);
+    double tmax = smax(tx1, tx2);
+    double ty1 = (b[1] - r.oy) * r.iy;
+    double ty2 = (b[4] - r.oy) * r.iy;
+    tmin = smax(tmin, smin(ty1, ty2));
+    tmax = smin(tmax, smax(ty1, ty2));
+    double tz1 = (b[2] - r.oz) * r.iz;
+    double tz2 = (b[5] - r.oz) * r.iz;
+    tmin = smax(tmin, smin(tz1, tz2));
+    tmax = smin(tmax, smax(tz1, tz2));
+    return tmax >= tmin;
+}
+
+// Triangle::intersect (triangle.hpp:40-62).  T = v0, edge1, edge2 (the
+// edges are precomputed with the same subtraction the reference performs).
+__device__ __forceinline__ bool mt64(const double* __restrict__ T, const Ray64& r, double& t_out) {
+    const double EPS = 1e-8;
+    const double e1x = T[3], e1y = T[4], e1z = T[5];
+    const double e2x = T[6], e2y = T[7], e2z = T[8];
+    const double hx = r.dy * e2z - r.dz * e2y;
+    const double hy = r.dz * e2x - r.dx * e2z;
+    const double hz = r.dx * e2y - r.dy * e2x;
+    const double a = e1x * hx + e1y * hy + e1z * hz;
+    if (a > -EPS && a < EPS) return false;
+    const double f = 1.0 / a;
+    const double sx = r.ox - T[0], sy = r.oy - T[1], sz = r.oz - T[2];
+    const double u = f * (sx * hx + sy * hy + sz * hz);
+    if (u < 0.0 || u > 1.0) return false;
+    const double qx = sy * e1z - sz * e1y;
+    const double qy = sz * e1x - sx * e1z;
+    const double qz = sx * e1y - sy * e1x;
+    const double v = f * (r.dx * qx + r.dy * qy + r.dz * qz);
+    if (v < 0.0 || u + v > 1.0) return false;
+    const double t = f * (e2x * qx + e2y * qy + e2z * qz);
+    if (!(t > EPS)) return false;
+    t_out = t;
+    return true;
+}
+
+// Conservative fp32 pre-filter of Triangle::intersect.  Returns false only
+// when the exact fp64 test must reject (u < 0, v < 0, u+v > 1 or t < 0), or
+// the hit lies beyond `tcull`.  Record: v0, e1, e2 (fp32, nearest) and, rounded
+// up, M1 = max|e1_i|, M2 = max|e2_i|, Cv = max|v0_i|; `co` = max|o_i| rounded up.
+// Every computed MT quantity X (a, U = s.h, V = d.q, T = e2.q) is within a
+// quarter of its budget errX of the exact real value, with
+//   G = 256 Ms + 64 (co + Cv)     (Ms = max|s_i|, s = o - v0 in fp32)
+//   errA = 256 u M1 M2, errU = u M2 G, errV = u M1 G, errT = u M1 M2 G
+// (u = 2^-24; |d_i| <= 1; each quantity is a 3-term dot of products of inputs
+// carrying <= 2u relative rounding, plus the absolute rounding of s).  A
+// rejection therefore leaves >= 3/4 of a budget between the real value and the
+// decision boundary — far beyond the fp64 test's own rounding (2^-50 scale) —
+// so the fp64 test would reject too.  DESIGN.md "exactness" has the details.
+__device__ __forceinline__ bool tri_prefilter(const float4 A, const float4 B, const float4 C, float ox, float oy,
+                                              float oz, float dx, float dy, float dz, float co, float tcull) {
+    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = C.x;
+    const float M1 = C.y, M2 = C.z, Cv = C.w;
+    const float sx = ox - A.x, sy = oy - A.y, sz = oz - A.z;
+    const float hx = __builtin_fmaf(dy, e2z, -dz * e2y);
+    const float hy = __builtin_fmaf(dz, e2x, -dx * e2z);
+    const float hz = __builtin_fmaf(dx, e2y, -dy * e2x);
+    const float a = __builtin_fmaf(e1x, hx, __builtin_fmaf(e1y, hy, e1z * hz));
+    const float U = __builtin_fmaf(sx, hx, __builtin_fmaf(sy, hy, sz * hz));
+    const float qx = __builtin_fmaf(sy, e1z, -sz * e1y);
+    const float qy = __builtin_fmaf(sz, e1x, -sx * e1z);
+    const float qz = __builtin_fmaf(sx, e1y, -sy * e1x);
+    const float V = __builtin_fmaf(dx, qx, __builtin_fmaf(dy, qy, dz * qz));
+    const float T = __builtin_fmaf(e2x, qx, __builtin_fmaf(e2y, qy, e2z * qz));
+    const float Ms = fmaxf(fmaxf(__builtin_fabsf(sx), __builtin_fabsf(sy)), __builtin_fabsf(sz));
+    const float u = 0x1p-24f;
+    const float G = __builtin_fmaf(256.f, Ms, 64.f * (co + Cv));
+    const float errA = 256.f * u * M1 * M2;
+    const float errU = u * M2 * G, errV = u * M1 * G, errT = u * M1 * M2 * G;
+    const float aa = __builtin_fabsf(a);
+    if (!(aa > errA)) return true;  // sign of the determinant uncertain: let fp64 decide
+    const float sg = a > 0.f ? 1.f : -1.f;
+    const float Us = sg * U, Vs = sg * V, Ts = sg * T;
+    if (Us < -errU || Vs < -errV || Ts < -errT) return false;
+    if (Us + Vs > aa + errU + errV + errA) return false;
+    if (Ts - errT > tcull * (aa + errA)) return false;  // t > tcull: cannot improve
+    return true;
+}
+
+// main.cpp:332-337: d = dir + up*py + right*px; d *= 1/|d|; Ray{pos, d}
+__device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) {
+    const double px = fp.px[i], py = fp.py[j];
+    double dx = (fp.dir[0] + fp.up[0] * py) + fp.right[0] * px;
+    double dy = (fp.dir[1] + fp.up[1] * py) + fp.right[1] * px;
+    double dz = (fp.dir[2] + fp.up[2] * py) + fp.right[2] * px;
+    const double s = 1.0 / __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+    dx = dx * s;
+    dy = dy * s;
+    dz = dz * s;
+    Ray64 r;
+    r.ox = fp.pos[0];
+    r.oy = fp.pos[1];
+    r.oz = fp.pos[2];
+    r.dx = dx;
+    r.dy = dy;
+    r.dz = dz;
+    const double inf = __builtin_huge_val();
+    r.ix = dx != 0.0 ? 1.0 / dx : inf;
+    r.iy = dy != 0.0 ? 1.0 / dy : inf;
+    r.iz = dz != 0.0 ? 1.0 / dz : inf;
+    return r;
+}
+
+// Candidate bookkeeping shared by both kernels.
+struct Best {
+    double dist;
+    uint32_t rank;
+    int32_t tri;  // BVH-order index, -1 = none
+    double px, py, pz;
+};
+
+// Distance of a detected hit exactly as stack_bvh.hpp:630-631 computes it.
+__device__ __forceinline__ double hit_dist(const Ray64& r, double t, double& px, double& py, double& pz) {
+    px = r.ox + r.dx * t;
+    py = r.oy + r.dy * t;
+    pz = r.oz + r.dz * t;
+    const double ex = px - r.ox, ey = py - r.oy, ez = pz - r.oz;
+    return __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+}
+
+// shadeScreen body (main.cpp:356-377) + PPM byte cast (benchmark.hpp:105-114)
+__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDevScene& sc, size_t o, const Best& b) {
+    uint8_t c0 = 0, c1 = 0, c2 = 0;
+    if (b.tri >= 0 && fp.rgb) {
+        const uint32_t id = sc.tri_id[b.tri];
+        double nx = sc.normal[3 * (size_t)id], ny = sc.normal[3 * (size_t)id + 1], nz = sc.normal[3 * (size_t)id + 2];
+        const double nl = __builtin_sqrt(nx * nx + ny * ny + nz * nz);
+        if (nl > 0.0) {
+            const double s = 1.0 / nl;
+            nx = nx * s; ny = ny * s; nz = nz * s;
+        }
+        double lx = fp.pos[0] - b.px, ly = fp.pos[1] - b.py, lz = fp.pos[2] - b.pz;
+        const double dist = __builtin_sqrt(lx * lx + ly * ly + lz * lz);
+        if (dist > 0.0) {
+            const double s = 1.0 / dist;
+            lx = lx * s; ly = ly * s; lz = lz * s;
+        }
+        const double diffuse = smax(0.0, nx * lx + ny * ly + nz * lz) * 1.35;
+        const double att = 1.0 / (1.0 + 0.05 * dist * dist);
+        const double I = sclamp((0.45 + diffuse * att) * 1.25, 0.0, 1.0);
+        c0 = (uint8_t)sclamp((0.5 * (nx + 1.0)) * I * 255.0, 0.0, 255.0);
+        c1 = (uint8_t)sclamp((0.5 * (ny + 1.0)) * I * 255.0, 0.0, 255.0);
+        c2 = (uint8_t)sclamp((0.5 * (nz + 1.0)) * I * 255.0, 0.0, 255.0);
+    }
+    if (fp.rgb) {
+        fp.rgb[3 * o] = c0;
+        fp.rgb[3 * o + 1] = c1;
+        fp.rgb[3 * o + 2] = c2;
+    }
+    if (fp.hit_id) fp.hit_id[o] = b.tri >= 0 ? sc.tri_id[b.tri] : RT_INVALID_REF;
+    if (fp.dist) fp.dist[o] = b.tri >= 0 ? b.dist : -1.0;
+    if (fp.hit_pos) {
+        fp.hit_pos[3 * o] = b.tri >= 0 ? b.px : 0.0;
+        fp.hit_pos[3 * o + 1] = b.tri >= 0 ? b.py : 0.0;
+        fp.hit_pos[3 * o + 2] = b.tri >= 0 ? b.pz : 0.0;
+    }
+    if (b.tri >= 0 && fp.hit_count) atomicAdd(fp.hit_count, 1ull);
+}
+
+template <int W>
+__device__ __forceinline__ void load_w(float (&d)[W], const float* __restrict__ p) {
+    if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < W; c += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(p + c);
+            d[c] = v.x; d[c + 1] = v.y; d[c + 2] = v.z; d[c + 3] = v.w;
+        }
+    } else {
+        const float2 v = *reinterpret_cast<const float2*>(p);
+        d[0] = v.x; d[1] = v.y;
+    }
+}
+template <int W>
+__device__ __forceinline__ void load_refs(uint32_t (&d)[W], const uint32_t* __restrict__ p) {
+    if constexpr (W % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < W; c += 4) {
+            const uint4 v = *reinterpret_cast<const uint4*>(p + c);
+            d[c] = v.x; d[c + 1] = v.y; d[c + 2] = v.z; d[c + 3] = v.w;
+        }
+    } else {
+        const uint2 v = *reinterpret_cast<const uint2*>(p);
+        d[0] = v.x; d[1] = v.y;
+    }
+}
+
+// fp32 upper bound of a positive double
+__device__ __forceinline__ float round_up_f(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return f;
+}
+
+// The reference sees a triangle only when every box on its root path passes
+// the fp64 slab test; re-check that chain for a would-be winner.
+__device__ __forceinline__ bool chain_ok(const RtDevScene& sc, uint32_t leaf, const Ray64& r, uint32_t& loads) {
+    int32_t n = (int32_t)leaf;
+    while (n >= 0) {
+        loads++;
+        if (!box_hit64(sc.rbox + 6 * (size_t)n, r)) return false;
+        n = sc.rparent[n];
+    }
+    return true;
+}
+
+// Sufficient condition for chain_ok without walking the chain: if the hit
+// point p = fl(o + d t) lies inside the (real) leaf box with a margin
+// m_a = 2^-48 (|mn_a| + |mx_a| + |o_a| + |p_a|) on every axis and no direction
+// component is zero, every fp64 slab test on the root path passes.  Proof
+// sketch (DESIGN.md "exactness"): |p_a - (o_a + d_a t)| <= 2^-52(|o_a|+|d_a t|)
+// and each computed slab bound is within 2^-51 |mn_a - o_a| / |d_a| of its
+// real value, so every computed near bound is < t < every computed far bound;
+// ancestor boxes contain the leaf box, so their margins are no smaller.
+__device__ __forceinline__ bool chain_fast_ok(const double* __restrict__ b, const Ray64& r, double px, double py,
+                                              double pz) {
+    if (r.dx == 0.0 || r.dy == 0.0 || r.dz == 0.0) return false;
+    const double o[3] = {r.ox, r.oy, r.oz}, p[3] = {px, py, pz};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double m = 0x1p-48 * (__builtin_fabs(b[a]) + __builtin_fabs(b[3 + a]) + __builtin_fabs(o[a]) +
+                                    __builtin_fabs(p[a]));
+        if (!(p[a] - b[a] >= m && b[3 + a] - p[a] >= m)) return false;
+    }
+    return true;
+}
+
+// Per-lane traversal stack: the top S entries live in LDS (one column per
+// lane: entry e of lane t at lds[e % S][t], conflict-free for ds_read_b64),
+// older entries spill to the lane's slice of a global buffer.
+template <int S>
+struct LaneStack {
+    uint2 (*lds)[256];
+    uint2* spill;
+    int tid;
+    int top;
+    __device__ __forceinline__ void push(uint32_t ref, float t) {
+        const int slot = top & (S - 1);
+        if (top >= S) spill[top - S] = lds[slot][tid];
+        lds[slot][tid] = make_uint2(ref, __float_as_uint(t));
+        top++;
+    }
+    __device__ __forceinline__ uint2 pop() {
+        top--;
+        const int slot = top & (S - 1);
+        const uint2 e = lds[slot][tid];
+        if (top >= S) lds[slot][tid] = spill[top - S];
+        return e;
+    }
+};
+
+}  // namespace rtk

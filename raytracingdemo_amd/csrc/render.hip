@@ -268,6 +268,240 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
     }
 }
 
+// --------------------------------------------------------------------------
+// Wave-cooperative ("packet") exact kernel: the 64 rays of one 8x8 tile walk
+// the tree together.  The current node is wave-uniform, so its bounds and
+// child refs come in through the scalar data path (s_load into SGPRs, once per
+// wave) instead of 64 per-lane copies through the vector memory pipe; each
+// lane slab-tests its own ray against the W children; `ballot` turns the
+// per-lane results into one 64-bit lane mask per child; the wave continues
+// into the child nearest to its first active lane and pushes the others
+// (ref + lane mask) on a wave-uniform stack in LDS.  Leaves are tested the
+// same way: uniform triangle records, per-lane pre-filter, fp64 only for the
+// lanes the pre-filter cannot reject.  Exactness machinery as trace_exact.
+// --------------------------------------------------------------------------
+typedef const __attribute__((address_space(4))) float* cfloat_p;
+typedef const __attribute__((address_space(4))) uint32_t* cuint_p;
+typedef const __attribute__((address_space(4))) double* cdouble_p;
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+
+template <int W, int SP, bool COUNT>
+__device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrameParams& fp, int i, int r, bool valid,
+                                             uint4* __restrict__ wstack) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t me = 1ull << lane;
+    if (!valid) { i = 0; r = 0; }
+    const int j = fp.row0 + r * fp.row_stride;
+    Ray32 q;
+    double tslack;
+    {
+        const Ray64 ray = gen_ray(fp, i, j);
+        q = make_ray32(ray, fp.pad);
+        tslack = 0x1p-40 * ((double)q.co + 1.0);
+    }
+    // slab offsets for the lo / hi planes (pad moves lo down and hi up)
+    const float pd = fp.pad;
+    const float olx = (q.ox + pd) * q.ix, ohx = (q.ox - pd) * q.ix;
+    const float oly = (q.oy + pd) * q.iy, ohy = (q.oy - pd) * q.iy;
+    const float olz = (q.oz + pd) * q.iz, ohz = (q.oz - pd) * q.iz;
+
+    Win best;
+    best.dist = 1.7976931348623157e308;
+    best.t = 0.0;
+    best.rank = 0xFFFFFFFFu;
+    best.tri = -1;
+    uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_pre = 0;
+    uint64_t need = uni64(__ballot(valid));
+    for (int pass = 0; pass < 2 && need; pass++) {
+        const bool mine = (need & me) != 0;
+        if (mine) {
+            best.dist = 1.7976931348623157e308;
+            best.t = 0.0;
+            best.rank = 0xFFFFFFFFu;
+            best.tri = -1;
+        }
+        float tcull = __builtin_huge_valf();
+        uint32_t chain_leaf = 0xFFFFFFFFu;
+        bool chain_res = false;
+        bool root_hit = false;
+        {
+            const float* b = sc.root_box;
+            const float t0 = fmaxf(fmaxf(fminf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
+                                         fminf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
+                                   fmaxf(fminf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), 0.f));
+            const float t1 = fminf(fminf(fmaxf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
+                                         fmaxf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
+                                   fmaxf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)));
+            root_hit = mine && t0 <= t1;
+        }
+        uint64_t active = uni64(__ballot(root_hit));
+        uint32_t cur = sc.root_ref;
+        int sp = 0;
+        for (;;) {
+            if (active != 0 && cur != RT_INVALID_REF) {
+                const bool act = (active & me) != 0;
+                if (!(cur & RT_LEAF_BIT)) {
+                    if (COUNT && act) n_nodes++;
+                    const cfloat_p nb = (cfloat_p)(sc.nodes + (size_t)cur * sc.node_bytes);
+                    const cuint_p rb = (cuint_p)(nb + 6 * W);
+                    float key[W];
+                    uint64_t m[W];
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        const float tlx = __builtin_fmaf(nb[0 * W + c], q.ix, -olx);
+                        const float thx = __builtin_fmaf(nb[1 * W + c], q.ix, -ohx);
+                        const float tly = __builtin_fmaf(nb[2 * W + c], q.iy, -oly);
+                        const float thy = __builtin_fmaf(nb[3 * W + c], q.iy, -ohy);
+                        const float tlz = __builtin_fmaf(nb[4 * W + c], q.iz, -olz);
+                        const float thz = __builtin_fmaf(nb[5 * W + c], q.iz, -ohz);
+                        const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
+                        const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
+                        const bool h = act && t0 <= t1;
+                        m[c] = rb[c] == RT_INVALID_REF ? 0ull : uni64(__ballot(h));
+                        // ordering key: the entry distance seen by the child's first lane
+                        key[c] = m[c] ? __uint_as_float((uint32_t)__builtin_amdgcn_readlane(
+                                            (int)__float_as_uint(t0), (int)__builtin_ctzll(m[c])))
+                                      : __builtin_huge_valf();
+                    }
+                    // nearest child continues; the others go on the stack, farthest first
+                    int nearest = -1;
+                    float kn = __builtin_huge_valf();
+#pragma unroll
+                    for (int c = 0; c < W; c++)
+                        if (m[c] && (nearest < 0 || key[c] < kn)) { kn = key[c]; nearest = c; }
+                    if (nearest >= 0) {
+                        uint32_t left = 0;
+#pragma unroll
+                        for (int c = 0; c < W; c++)
+                            if (m[c] && c != nearest) left |= 1u << c;
+                        while (left) {
+                            int far_c = 0;
+                            float kf = -1.f;
+#pragma unroll
+                            for (int c = 0; c < W; c++)
+                                if (((left >> c) & 1u) && key[c] >= kf) { kf = key[c]; far_c = c; }
+                            uint64_t fm = 0;
+#pragma unroll
+                            for (int c = 0; c < W; c++)
+                                if (c == far_c) fm = m[c];
+                            if (sp < SP) {
+                                if (lane == 0) wstack[sp] = make_uint4(rb[far_c], (uint32_t)fm, (uint32_t)(fm >> 32), 0u);
+                                sp++;
+                            }
+                            left &= ~(1u << far_c);
+                        }
+                        uint64_t nm = 0;
+#pragma unroll
+                        for (int c = 0; c < W; c++)
+                            if (c == nearest) nm = m[c];
+                        cur = rb[nearest];
+                        active = nm;
+                        continue;
+                    }
+                } else {
+                    const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+                    const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+                    for (uint32_t k = first; k < first + cnt; k++) {
+                        const cfloat_p R = (cfloat_p)(sc.tri32 + 12 * (size_t)k);
+                        const float4 A = make_float4(R[0], R[1], R[2], R[3]);
+                        const float4 B = make_float4(R[4], R[5], R[6], R[7]);
+                        const float4 Cc = make_float4(R[8], R[9], R[10], R[11]);
+                        if (COUNT && act) n_pre++;
+                        const bool pre =
+                            act && tri_prefilter(A, B, Cc, q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull);
+                        if (__ballot(pre) == 0) continue;
+                        if (!pre) continue;
+                        if (COUNT) n_tris++;
+                        const Ray64 ray = gen_ray(fp, opaque(i), j);
+                        const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)k;
+                        double t;
+                        if (!mt64(T, ray, t)) continue;
+                        double hx, hy, hz;
+                        const double d = hit_dist(ray, t, hx, hy, hz);
+                        const uint2 rl = *reinterpret_cast<const uint2*>(T + 9);  // {rank, leaf}
+                        if (!(d < best.dist || (d == best.dist && rl.x < best.rank))) continue;
+                        if (pass == 1) {
+                            if (rl.y != chain_leaf) {
+                                if (COUNT) n_chain++;
+                                chain_leaf = rl.y;
+                                chain_res = chain_ok(sc, rl.y, ray, n_chain_nodes);
+                            }
+                            if (!chain_res) continue;
+                        }
+                        best.dist = d;
+                        best.t = t;
+                        best.rank = rl.x;
+                        best.tri = (int32_t)k;
+                        tcull = round_up_f((d + tslack) * (1.0 + 0x1p-20));
+                    }
+                }
+            }
+            if (sp == 0) break;
+            sp--;
+            const uint4 e = wstack[sp];
+            cur = uni(e.x);
+            active = ((uint64_t)uni(e.z) << 32) | uni(e.y);
+        }
+        if (pass == 1) break;
+        // deferred re-verification of each lane's winner
+        bool redo = false;
+        if (mine && best.tri >= 0) {
+            const Ray64 ray = gen_ray(fp, opaque(i), j);
+            double hx, hy, hz;
+            (void)hit_dist(ray, best.t, hx, hy, hz);
+            const uint32_t leaf =
+                reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + 9)->y;
+            if (COUNT) n_chain++;
+            redo = !chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz) &&
+                   !chain_ok(sc, leaf, ray, n_chain_nodes);
+        }
+        need = uni64(__ballot(redo));
+    }
+    if (!valid) return;
+    Best out;
+    out.dist = best.dist;
+    out.rank = best.rank;
+    out.tri = best.tri;
+    out.px = out.py = out.pz = 0.0;
+    if (best.tri >= 0) {
+        const Ray64 ray = gen_ray(fp, opaque(i), j);
+        (void)hit_dist(ray, best.t, out.px, out.py, out.pz);
+    }
+    const size_t o = (size_t)r * fp.W + i;
+    shade_store(fp, sc, o, out);
+    if (COUNT && fp.counters) {
+        atomicAdd(&fp.counters[0], 1ull);
+        atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
+        atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
+        atomicAdd(&fp.counters[3], (unsigned long long)n_chain);
+        if (best.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
+        atomicAdd(&fp.counters[5], (unsigned long long)n_chain_nodes);
+        atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
+    }
+}
+
+template <int W, int SP, bool COUNT>
+__global__ void __launch_bounds__(256) k_trace_packet(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
+    __shared__ uint4 stacks[4][SP];
+    const int lane = threadIdx.x & 63;
+    uint4* wstack = stacks[threadIdx.x >> 6];
+    const int tiles_x = (fp.W + 7) >> 3;
+    const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
+    for (;;) {
+        int tile = 0;
+        if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);
+        tile = __shfl(tile, 0);
+        if (tile >= tiles) break;
+        const int i = (tile % tiles_x) * 8 + (lane & 7);
+        const int r = (tile / tiles_x) * 8 + (lane >> 3);
+        trace_packet<W, SP, COUNT>(sc, fp, i, r, i < fp.W && r < fp.nrows, wstack);
+    }
+}
+
 // Persistent waves: each wave pulls 8x8 pixel tiles from `tile_ctr` until the
 // shard is exhausted (every wave reaches the exit test each iteration).
 template <int W, int S, bool COUNT, int MINW>
@@ -357,53 +591,40 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
     }
 }
 
-constexpr int kLdsStack = 16;  // LDS ring entries per lane (8 B each)
+constexpr int kLdsStack = 16;      // per-lane kernel: LDS ring entries per lane (8 B each)
+constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (16 B each)
 
-template <int W, int MINW>
-hipError_t launch_exact_m(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
-                          hipStream_t s) {
-    const dim3 grid((unsigned)aux.grid);
-    if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true, MINW>), grid, dim3(256), 0, s, sc, fp, aux);
-    else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false, MINW>), grid, dim3(256), 0, s, sc, fp, aux);
-    return hipGetLastError();
-}
-
-// Occupancy target of the exact kernel (waves per SIMD the register
-// allocation is bounded for): 4 by default, RT_WAVES=3/5 for experiments.
-int waves_target() {
-    static const int w = [] {
-        const char* e = getenv("RT_WAVES");
-        const int v = e ? atoi(e) : 4;
-        return (v == 3 || v == 5) ? v : 4;
+// Kernel choice: the packet kernel unless its stack cannot hold the tree's
+// bound or RT_KERNEL=lane asks for the per-lane kernel.
+bool use_packet(uint32_t stack_bound) {
+    static const bool lane_forced = [] {
+        const char* e = getenv("RT_KERNEL");
+        return e && e[0] == 'l';
     }();
-    return w;
+    return !lane_forced && stack_bound <= (uint32_t)kPacketStack;
 }
 
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
                         hipStream_t s) {
-    switch (waves_target()) {
-        case 3: return launch_exact_m<W, 3>(sc, fp, aux, count, s);
-        case 5: return launch_exact_m<W, 5>(sc, fp, aux, count, s);
-        default: return launch_exact_m<W, 4>(sc, fp, aux, count, s);
+    const dim3 grid((unsigned)aux.grid);
+    if (use_packet(sc.stack_bound)) {
+        if (count) hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, true>), grid, dim3(256), 0, s, sc, fp, aux);
+        else hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, false>), grid, dim3(256), 0, s, sc, fp, aux);
+    } else {
+        if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true, 3>), grid, dim3(256), 0, s, sc, fp, aux);
+        else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false, 3>), grid, dim3(256), 0, s, sc, fp, aux);
     }
+    return hipGetLastError();
 }
 
-template <int W, int MINW>
-int blocks_per_cu_m() {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<W, kLdsStack, false, MINW>, 256, 0) !=
-        hipSuccess)
-        n = 1;
-    return n;
-}
 template <int W>
-int blocks_per_cu_w() {
-    switch (waves_target()) {
-        case 3: return blocks_per_cu_m<W, 3>();
-        case 5: return blocks_per_cu_m<W, 5>();
-        default: return blocks_per_cu_m<W, 4>();
-    }
+int blocks_per_cu_w(uint32_t stack_bound) {
+    int n = 0;
+    hipError_t e = use_packet(stack_bound)
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_packet<W, kPacketStack, false>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<W, kLdsStack, false, 3>, 256, 0);
+    return e == hipSuccess ? n : 1;
 }
 
 template <int SMAX>
@@ -418,9 +639,11 @@ hipError_t launch_literal_s(const RtDevScene& sc, const RtFrameParams& fp, bool 
 namespace rt {
 
 // Blocks per CU the persistent exact kernel is launched with.
-int exact_blocks_per_cu(int width) {
-    int n = width == 2 ? blocks_per_cu_w<2>() : width == 4 ? blocks_per_cu_w<4>() : width == 8 ? blocks_per_cu_w<8>()
-                                                                                          : blocks_per_cu_w<16>();
+int exact_blocks_per_cu(int width, uint32_t stack_bound) {
+    int n = width == 2   ? blocks_per_cu_w<2>(stack_bound)
+            : width == 4 ? blocks_per_cu_w<4>(stack_bound)
+            : width == 8 ? blocks_per_cu_w<8>(stack_bound)
+                         : blocks_per_cu_w<16>(stack_bound);
     if (n < 1) n = 1;
     return n < 8 ? n : 8;
 }

@@ -18,7 +18,7 @@
 namespace rt {
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
                         hipStream_t s, uint32_t literal_stack);
-int exact_blocks_per_cu(int width);
+int exact_blocks_per_cu(int width, uint32_t stack_bound);
 int exact_lds_stack();
 }
 
@@ -178,7 +178,7 @@ void upload_one(rt_scene* s, int device) {
     HIP_TRY(hipEventCreate(&r.ev1));
     HIP_TRY(hipEventCreateWithFlags(&r.ev_in, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&r.ev_out, hipEventDisableTiming));
-    r.grid = prop.multiProcessorCount * rt::exact_blocks_per_cu(f.width);
+    r.grid = prop.multiProcessorCount * rt::exact_blocks_per_cu(f.width, f.stack_bound);
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
     HIP_TRY(hipMalloc(&r.d_tiles, 256));

@@ -35,6 +35,8 @@ for s in $STEPS; do
         list)  run list 120 rocprofv3 -L ;;
         waves) for w in 3 4 5; do RT_WAVES=$w run bench_w$w 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
         quick) run bench_quick 300 python bench.py --no-cpu --steps 5 ;;
+        lane)  RT_KERNEL=lane run bench_lane 300 python bench.py --no-cpu --steps 5 ;;
+        lanetests) RT_KERNEL=lane run tests_lane 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
         sq)    run sq1 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
                    SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --output-format csv -d gpurun_out/sq -o sq1 \
                    -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \

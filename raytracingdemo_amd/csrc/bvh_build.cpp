@@ -341,30 +341,17 @@ struct Flattener {
     uint32_t alloc_node() {
         uint32_t id = (uint32_t)f.n_wide++;
         f.wide.resize(f.n_wide * nb, 0);
-        uint8_t* p = f.wide.data() + (size_t)id * nb;
-        float* b = reinterpret_cast<float*>(p);
-        for (int c = 0; c < W; c++) {  // empty slot: inverted box, never hit
-            b[0 * W + c] = std::numeric_limits<float>::infinity();
-            b[1 * W + c] = -std::numeric_limits<float>::infinity();
-            b[2 * W + c] = std::numeric_limits<float>::infinity();
-            b[3 * W + c] = -std::numeric_limits<float>::infinity();
-            b[4 * W + c] = std::numeric_limits<float>::infinity();
-            b[5 * W + c] = -std::numeric_limits<float>::infinity();
-        }
-        uint32_t* r = reinterpret_cast<uint32_t*>(p + 24 * W);
-        for (int c = 0; c < W; c++) r[c] = RT_INVALID_REF;
+        // empty slot: zero box, ref RT_INVALID_REF (the kernels mask it out)
+        uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + (size_t)id * nb);
+        for (int c = 0; c < W; c++) p[8 * c + RT_CHILD_REF] = RT_INVALID_REF;
         return id;
     }
+    // one 32-B child record: lo.x hi.x lo.y hi.y lo.z hi.z ref pad
     void set_slot(uint32_t node, int c, const float b6[6], uint32_t ref) {
-        uint8_t* p = f.wide.data() + (size_t)node * nb;
-        float* b = reinterpret_cast<float*>(p);
-        b[0 * W + c] = b6[0];
-        b[1 * W + c] = b6[1];
-        b[2 * W + c] = b6[2];
-        b[3 * W + c] = b6[3];
-        b[4 * W + c] = b6[4];
-        b[5 * W + c] = b6[5];
-        reinterpret_cast<uint32_t*>(p + 24 * W)[c] = ref;
+        float* b = reinterpret_cast<float*>(f.wide.data() + (size_t)node * nb) + 8 * c;
+        for (int k = 0; k < 6; k++) b[k] = b6[k];
+        reinterpret_cast<uint32_t*>(b)[RT_CHILD_REF] = ref;
+        reinterpret_cast<uint32_t*>(b)[7] = 0;
     }
 
     // reference of a real node as a child slot value

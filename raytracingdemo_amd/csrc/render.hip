@@ -113,10 +113,9 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
         // covered by tslack + the 2^-20 relative margin of tcull
         tslack = 0x1p-40 * ((double)q.co + 1.0);
     }
-    // near/far plane selection by direction sign (ray-constant)
-    const int nxo = q.ix >= 0.f ? 0 : W, fxo = q.ix >= 0.f ? W : 0;
-    const int nyo = q.iy >= 0.f ? 2 * W : 3 * W, fyo = q.iy >= 0.f ? 3 * W : 2 * W;
-    const int nzo = q.iz >= 0.f ? 4 * W : 5 * W, fzo = q.iz >= 0.f ? 5 * W : 4 * W;
+    // near/far plane selection by direction sign (ray-constant): a negative
+    // reciprocal swaps lo and hi
+    const bool sx = q.ix < 0.f, sy = q.iy < 0.f, sz = q.iz < 0.f;
 
     Win best;
     uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_pre = 0;
@@ -151,33 +150,32 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
         while (cur != RT_INVALID_REF) {
             if (!(cur & RT_LEAF_BIT)) {
                 if (COUNT) n_nodes++;
-                const float* nb = reinterpret_cast<const float*>(sc.nodes + (size_t)cur * sc.node_bytes);
-                const uint32_t* rb = reinterpret_cast<const uint32_t*>(nb + 6 * W);
+                const float4* nb = reinterpret_cast<const float4*>(sc.nodes + (size_t)cur * sc.node_bytes);
                 float tn[W];
+                uint32_t rb[W];
                 uint32_t mask = 0;
 #pragma unroll
                 for (int g = 0; g < W; g += G) {
-                    float nx[G], fx[G], ny[G], fy[G], nz[G], fz[G];
-                    uint32_t ref[G];
-                    load_w<G>(nx, nb + nxo + g);
-                    load_w<G>(fx, nb + fxo + g);
-                    load_w<G>(ny, nb + nyo + g);
-                    load_w<G>(fy, nb + fyo + g);
-                    load_w<G>(nz, nb + nzo + g);
-                    load_w<G>(fz, nb + fzo + g);
-                    load_refs<G>(ref, rb + g);
+                    float4 lo[G], hi[G];  // {lx,hx,ly,hy}, {lz,hz,ref,pad}
 #pragma unroll
                     for (int c = 0; c < G; c++) {
-                        const float a0 = __builtin_fmaf(nx[c], q.ix, -q.onx);
-                        const float a1 = __builtin_fmaf(fx[c], q.ix, -q.ofx);
-                        const float b0 = __builtin_fmaf(ny[c], q.iy, -q.ony);
-                        const float b1 = __builtin_fmaf(fy[c], q.iy, -q.ofy);
-                        const float c0 = __builtin_fmaf(nz[c], q.iz, -q.onz);
-                        const float c1 = __builtin_fmaf(fz[c], q.iz, -q.ofz);
+                        lo[c] = nb[2 * (g + c)];
+                        hi[c] = nb[2 * (g + c) + 1];
+                    }
+#pragma unroll
+                    for (int c = 0; c < G; c++) {
+                        const float a0 = __builtin_fmaf(sx ? lo[c].y : lo[c].x, q.ix, -q.onx);
+                        const float a1 = __builtin_fmaf(sx ? lo[c].x : lo[c].y, q.ix, -q.ofx);
+                        const float b0 = __builtin_fmaf(sy ? lo[c].w : lo[c].z, q.iy, -q.ony);
+                        const float b1 = __builtin_fmaf(sy ? lo[c].z : lo[c].w, q.iy, -q.ofy);
+                        const float c0 = __builtin_fmaf(sz ? hi[c].y : hi[c].x, q.iz, -q.onz);
+                        const float c1 = __builtin_fmaf(sz ? hi[c].x : hi[c].y, q.iz, -q.ofz);
                         const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
                         const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
+                        const uint32_t ref = __float_as_uint(hi[c].z);
                         tn[g + c] = t0;
-                        if (t0 <= t1 && ref[c] != RT_INVALID_REF) mask |= 1u << (g + c);
+                        rb[g + c] = ref;
+                        if (t0 <= t1 && ref != RT_INVALID_REF) mask |= 1u << (g + c);
                     }
                 }
                 if (mask) {
@@ -280,9 +278,28 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
 // same way: uniform triangle records, per-lane pre-filter, fp64 only for the
 // lanes the pre-filter cannot reject.  Exactness machinery as trace_exact.
 // --------------------------------------------------------------------------
+struct __attribute__((aligned(32))) ChildRec {  // 32-B child record (rt_device.h)
+    float lx, hx, ly, hy, lz, hz;
+    uint32_t ref, pad;
+};
 typedef const __attribute__((address_space(4))) float* cfloat_p;
-typedef const __attribute__((address_space(4))) uint32_t* cuint_p;
-typedef const __attribute__((address_space(4))) double* cdouble_p;
+typedef const __attribute__((address_space(4))) ChildRec* cchild_p;
+
+// Field-wise reads through the constant address space: adjacent uniform loads
+// merge into one s_load_dwordx8 (child) / dwordx4 runs (triangle record).
+__device__ __forceinline__ ChildRec load_child(cchild_p p) {
+    ChildRec r;
+    r.lx = p->lx;
+    r.hx = p->hx;
+    r.ly = p->ly;
+    r.hy = p->hy;
+    r.lz = p->lz;
+    r.hz = p->hz;
+    r.ref = p->ref;
+    r.pad = p->pad;
+    return r;
+}
+__device__ __forceinline__ float4 load_f4(cfloat_p p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
@@ -346,22 +363,24 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
                 const bool act = (active & me) != 0;
                 if (!(cur & RT_LEAF_BIT)) {
                     if (COUNT && act) n_nodes++;
-                    const cfloat_p nb = (cfloat_p)(sc.nodes + (size_t)cur * sc.node_bytes);
-                    const cuint_p rb = (cuint_p)(nb + 6 * W);
+                    const cchild_p nb = (cchild_p)(sc.nodes + (size_t)cur * sc.node_bytes);
                     float key[W];
                     uint64_t m[W];
+                    uint32_t rb[W];
 #pragma unroll
                     for (int c = 0; c < W; c++) {
-                        const float tlx = __builtin_fmaf(nb[0 * W + c], q.ix, -olx);
-                        const float thx = __builtin_fmaf(nb[1 * W + c], q.ix, -ohx);
-                        const float tly = __builtin_fmaf(nb[2 * W + c], q.iy, -oly);
-                        const float thy = __builtin_fmaf(nb[3 * W + c], q.iy, -ohy);
-                        const float tlz = __builtin_fmaf(nb[4 * W + c], q.iz, -olz);
-                        const float thz = __builtin_fmaf(nb[5 * W + c], q.iz, -ohz);
+                        const ChildRec ch = load_child(nb + c);  // s_load_dwordx8
+                        rb[c] = ch.ref;
+                        const float tlx = __builtin_fmaf(ch.lx, q.ix, -olx);
+                        const float thx = __builtin_fmaf(ch.hx, q.ix, -ohx);
+                        const float tly = __builtin_fmaf(ch.ly, q.iy, -oly);
+                        const float thy = __builtin_fmaf(ch.hy, q.iy, -ohy);
+                        const float tlz = __builtin_fmaf(ch.lz, q.iz, -olz);
+                        const float thz = __builtin_fmaf(ch.hz, q.iz, -ohz);
                         const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
                         const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
                         const bool h = act && t0 <= t1;
-                        m[c] = rb[c] == RT_INVALID_REF ? 0ull : uni64(__ballot(h));
+                        m[c] = ch.ref == RT_INVALID_REF ? 0ull : uni64(__ballot(h));
                         // ordering key: the entry distance seen by the child's first lane
                         key[c] = m[c] ? __uint_as_float((uint32_t)__builtin_amdgcn_readlane(
                                             (int)__float_as_uint(t0), (int)__builtin_ctzll(m[c])))
@@ -406,10 +425,8 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
                     const uint32_t first = cur & RT_LEAF_FIRST_MASK;
                     const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
                     for (uint32_t k = first; k < first + cnt; k++) {
-                        const cfloat_p R = (cfloat_p)(sc.tri32 + 12 * (size_t)k);
-                        const float4 A = make_float4(R[0], R[1], R[2], R[3]);
-                        const float4 B = make_float4(R[4], R[5], R[6], R[7]);
-                        const float4 Cc = make_float4(R[8], R[9], R[10], R[11]);
+                        const cfloat_p R = (cfloat_p)(sc.tri32 + 12 * (size_t)k);  // scalar loads
+                        const float4 A = load_f4(R), B = load_f4(R + 4), Cc = load_f4(R + 8);
                         if (COUNT && act) n_pre++;
                         const bool pre =
                             act && tri_prefilter(A, B, Cc, q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull);

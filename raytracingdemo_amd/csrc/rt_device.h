@@ -1,12 +1,13 @@
 // Layouts shared by the host flattener and the gfx950 kernels.
 //
 // HBM layout of one scene replica (see DESIGN.md §Data layout):
-//   wide nodes   W child slots, SoA fp32 bounds (lo_x[W] hi_x[W] lo_y[W]
-//                hi_y[W] lo_z[W] hi_z[W]) then u32 child refs[W]; one node is
-//                node_bytes(W) = roundup(28*W, 64) bytes (W=8: 256 B, four
-//                64-B lines).  Bounds are the reference's fp64 boxes rounded
-//                outward to fp32 (a conservative superset); the kernel widens
-//                every slab by a per-frame margin (RtFrameParams.pad).
+//   wide nodes   W child records of 32 B: fp32 lo.x hi.x lo.y hi.y lo.z hi.z,
+//                u32 ref, pad — one s_load_dwordx8 per child in the packet
+//                kernel, two dwordx4 in the per-lane kernel; node_bytes(W) =
+//                32*W (W=8: 256 B, four 64-B lines).  Bounds are the
+//                reference's fp64 boxes rounded outward to fp32 (a
+//                conservative superset); the kernels widen every slab by a
+//                per-frame margin (RtFrameParams.pad).
 //   tri32        BVH order, fp32 v0,e1,e2 + pad (48 B)   — fp32 pre-filter
 //   tri64        BVH order, fp64 v0,e1,e2 + u32 visit rank + u32 real leaf
 //                (80 B)                                  — exact reference MT
@@ -21,10 +22,11 @@
 #define RT_INVALID_REF 0xFFFFFFFFu
 #define RT_LEAF_FIRST_MASK 0x07FFFFFFu
 #define RT_LEAF_MAX_FIRST 0x07FFFFFFu
+#define RT_CHILD_REF 6       // u32 slot of the child ref in a 32-B child record
 #define RT_TRI64_DOUBLES 10  // v0, e1, e2 (9 doubles) + {u32 rank, u32 leaf}: 80 B
 
 #ifdef __cplusplus
-static inline constexpr uint32_t rt_node_bytes(int W) { return (uint32_t)((28 * W + 63) / 64 * 64); }
+static inline constexpr uint32_t rt_node_bytes(int W) { return (uint32_t)(32 * W); }
 static inline constexpr uint32_t rt_make_leaf(uint32_t first, uint32_t count) {
     return RT_LEAF_BIT | ((count - 1u) << 27) | first;
 }

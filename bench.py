@@ -208,6 +208,8 @@ def main():
                                      "tri_tests_fp64": round(cs["tri_tests"] / max(cs["rays"], 1), 3),
                                      "chain_checks": round(cs["chain_checks"] / max(cs["rays"], 1), 4),
                                      "chain_nodes": round(cs["chain_nodes"] / max(cs["rays"], 1), 4),
+                                     "wave_nodes_per_tile": round(cs["wave_nodes"] / max(cs["wave_tiles"], 1), 2),
+                                     "wave_leaves_per_tile": round(cs["wave_leaves"] / max(cs["wave_tiles"], 1), 2),
                                      "node_bytes": st["node_bytes"], "tri32_bytes": TRI32_BYTES,
                                      "tri64_bytes": TRI64_BYTES}},
             "cpu_baseline": cpu,

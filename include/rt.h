@@ -108,6 +108,9 @@ typedef struct {
     uint64_t hits;
     uint64_t chain_nodes;   /* fp64 ancestor boxes loaded by those checks */
     uint64_t tri_prefilter; /* fp32 conservative triangle pre-tests     */
+    uint64_t wave_nodes;    /* packet kernel: inner-node visits per wave */
+    uint64_t wave_leaves;   /* packet kernel: leaf visits per wave       */
+    uint64_t wave_tiles;    /* packet kernel: 8x8 tiles traced           */
 } rt_frame_stats_t;
 
 /* objl::Loader + ObjectLoader::loadFromFile (object_loader.hpp:14-70,

@@ -68,7 +68,8 @@ class rt_scene_stats_t(C.Structure):
 class rt_frame_stats_t(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("node_fetches", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("chain_checks", C.c_uint64), ("hits", C.c_uint64), ("chain_nodes", C.c_uint64),
-                ("tri_prefilter", C.c_uint64)]
+                ("tri_prefilter", C.c_uint64), ("wave_nodes", C.c_uint64), ("wave_leaves", C.c_uint64),
+                ("wave_tiles", C.c_uint64)]
 
 
 _lib = None

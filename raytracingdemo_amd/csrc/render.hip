@@ -266,258 +266,7 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
     }
 }
 
-// --------------------------------------------------------------------------
-// Wave-cooperative ("packet") exact kernel: the 64 rays of one 8x8 tile walk
-// the tree together.  The current node is wave-uniform, so its bounds and
-// child refs come in through the scalar data path (s_load into SGPRs, once per
-// wave) instead of 64 per-lane copies through the vector memory pipe; each
-// lane slab-tests its own ray against the W children; `ballot` turns the
-// per-lane results into one 64-bit lane mask per child; the wave continues
-// into the child nearest to its first active lane and pushes the others
-// (ref + lane mask) on a wave-uniform stack in LDS.  Leaves are tested the
-// same way: uniform triangle records, per-lane pre-filter, fp64 only for the
-// lanes the pre-filter cannot reject.  Exactness machinery as trace_exact.
-// --------------------------------------------------------------------------
-struct __attribute__((aligned(32))) ChildRec {  // 32-B child record (rt_device.h)
-    float lx, hx, ly, hy, lz, hz;
-    uint32_t ref, pad;
-};
-typedef const __attribute__((address_space(4))) float* cfloat_p;
-typedef const __attribute__((address_space(4))) ChildRec* cchild_p;
-
-// Field-wise reads through the constant address space: adjacent uniform loads
-// merge into one s_load_dwordx8 (child) / dwordx4 runs (triangle record).
-__device__ __forceinline__ ChildRec load_child(cchild_p p) {
-    ChildRec r;
-    r.lx = p->lx;
-    r.hx = p->hx;
-    r.ly = p->ly;
-    r.hy = p->hy;
-    r.lz = p->lz;
-    r.hz = p->hz;
-    r.ref = p->ref;
-    r.pad = p->pad;
-    return r;
-}
-__device__ __forceinline__ float4 load_f4(cfloat_p p) { return make_float4(p[0], p[1], p[2], p[3]); }
-
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-__device__ __forceinline__ uint64_t uni64(uint64_t x) {
-    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
-}
-
-template <int W, int SP, bool COUNT>
-__device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrameParams& fp, int i, int r, bool valid,
-                                             uint4* __restrict__ wstack) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t me = 1ull << lane;
-    if (!valid) { i = 0; r = 0; }
-    const int j = fp.row0 + r * fp.row_stride;
-    Ray32 q;
-    double tslack;
-    {
-        const Ray64 ray = gen_ray(fp, i, j);
-        q = make_ray32(ray, fp.pad);
-        tslack = 0x1p-40 * ((double)q.co + 1.0);
-    }
-    // slab offsets for the lo / hi planes (pad moves lo down and hi up)
-    const float pd = fp.pad;
-    const float olx = (q.ox + pd) * q.ix, ohx = (q.ox - pd) * q.ix;
-    const float oly = (q.oy + pd) * q.iy, ohy = (q.oy - pd) * q.iy;
-    const float olz = (q.oz + pd) * q.iz, ohz = (q.oz - pd) * q.iz;
-
-    Win best;
-    best.dist = 1.7976931348623157e308;
-    best.t = 0.0;
-    best.rank = 0xFFFFFFFFu;
-    best.tri = -1;
-    uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_pre = 0;
-    uint64_t need = uni64(__ballot(valid));
-    for (int pass = 0; pass < 2 && need; pass++) {
-        const bool mine = (need & me) != 0;
-        if (mine) {
-            best.dist = 1.7976931348623157e308;
-            best.t = 0.0;
-            best.rank = 0xFFFFFFFFu;
-            best.tri = -1;
-        }
-        float tcull = __builtin_huge_valf();
-        uint32_t chain_leaf = 0xFFFFFFFFu;
-        bool chain_res = false;
-        bool root_hit = false;
-        {
-            const float* b = sc.root_box;
-            const float t0 = fmaxf(fmaxf(fminf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
-                                         fminf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
-                                   fmaxf(fminf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), 0.f));
-            const float t1 = fminf(fminf(fmaxf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
-                                         fmaxf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
-                                   fmaxf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)));
-            root_hit = mine && t0 <= t1;
-        }
-        uint64_t active = uni64(__ballot(root_hit));
-        uint32_t cur = sc.root_ref;
-        int sp = 0;
-        for (;;) {
-            if (active != 0 && cur != RT_INVALID_REF) {
-                const bool act = (active & me) != 0;
-                if (!(cur & RT_LEAF_BIT)) {
-                    if (COUNT && act) n_nodes++;
-                    const cchild_p nb = (cchild_p)(sc.nodes + (size_t)cur * sc.node_bytes);
-                    float key[W];
-                    uint64_t m[W];
-                    uint32_t rb[W];
-#pragma unroll
-                    for (int c = 0; c < W; c++) {
-                        const ChildRec ch = load_child(nb + c);  // s_load_dwordx8
-                        rb[c] = ch.ref;
-                        const float tlx = __builtin_fmaf(ch.lx, q.ix, -olx);
-                        const float thx = __builtin_fmaf(ch.hx, q.ix, -ohx);
-                        const float tly = __builtin_fmaf(ch.ly, q.iy, -oly);
-                        const float thy = __builtin_fmaf(ch.hy, q.iy, -ohy);
-                        const float tlz = __builtin_fmaf(ch.lz, q.iz, -olz);
-                        const float thz = __builtin_fmaf(ch.hz, q.iz, -ohz);
-                        const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
-                        const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
-                        const bool h = act && t0 <= t1;
-                        m[c] = ch.ref == RT_INVALID_REF ? 0ull : uni64(__ballot(h));
-                        // ordering key: the entry distance seen by the child's first lane
-                        key[c] = m[c] ? __uint_as_float((uint32_t)__builtin_amdgcn_readlane(
-                                            (int)__float_as_uint(t0), (int)__builtin_ctzll(m[c])))
-                                      : __builtin_huge_valf();
-                    }
-                    // nearest child continues; the others go on the stack, farthest first
-                    int nearest = -1;
-                    float kn = __builtin_huge_valf();
-#pragma unroll
-                    for (int c = 0; c < W; c++)
-                        if (m[c] && (nearest < 0 || key[c] < kn)) { kn = key[c]; nearest = c; }
-                    if (nearest >= 0) {
-                        uint32_t left = 0;
-#pragma unroll
-                        for (int c = 0; c < W; c++)
-                            if (m[c] && c != nearest) left |= 1u << c;
-                        while (left) {
-                            int far_c = 0;
-                            float kf = -1.f;
-#pragma unroll
-                            for (int c = 0; c < W; c++)
-                                if (((left >> c) & 1u) && key[c] >= kf) { kf = key[c]; far_c = c; }
-                            uint64_t fm = 0;
-#pragma unroll
-                            for (int c = 0; c < W; c++)
-                                if (c == far_c) fm = m[c];
-                            if (sp < SP) {
-                                if (lane == 0) wstack[sp] = make_uint4(rb[far_c], (uint32_t)fm, (uint32_t)(fm >> 32), 0u);
-                                sp++;
-                            }
-                            left &= ~(1u << far_c);
-                        }
-                        uint64_t nm = 0;
-#pragma unroll
-                        for (int c = 0; c < W; c++)
-                            if (c == nearest) nm = m[c];
-                        cur = rb[nearest];
-                        active = nm;
-                        continue;
-                    }
-                } else {
-                    const uint32_t first = cur & RT_LEAF_FIRST_MASK;
-                    const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
-                    for (uint32_t k = first; k < first + cnt; k++) {
-                        const cfloat_p R = (cfloat_p)(sc.tri32 + 12 * (size_t)k);  // scalar loads
-                        const float4 A = load_f4(R), B = load_f4(R + 4), Cc = load_f4(R + 8);
-                        if (COUNT && act) n_pre++;
-                        const bool pre =
-                            act && tri_prefilter(A, B, Cc, q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull);
-                        if (__ballot(pre) == 0) continue;
-                        if (!pre) continue;
-                        if (COUNT) n_tris++;
-                        const Ray64 ray = gen_ray(fp, opaque(i), j);
-                        const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)k;
-                        double t;
-                        if (!mt64(T, ray, t)) continue;
-                        double hx, hy, hz;
-                        const double d = hit_dist(ray, t, hx, hy, hz);
-                        const uint2 rl = *reinterpret_cast<const uint2*>(T + 9);  // {rank, leaf}
-                        if (!(d < best.dist || (d == best.dist && rl.x < best.rank))) continue;
-                        if (pass == 1) {
-                            if (rl.y != chain_leaf) {
-                                if (COUNT) n_chain++;
-                                chain_leaf = rl.y;
-                                chain_res = chain_ok(sc, rl.y, ray, n_chain_nodes);
-                            }
-                            if (!chain_res) continue;
-                        }
-                        best.dist = d;
-                        best.t = t;
-                        best.rank = rl.x;
-                        best.tri = (int32_t)k;
-                        tcull = round_up_f((d + tslack) * (1.0 + 0x1p-20));
-                    }
-                }
-            }
-            if (sp == 0) break;
-            sp--;
-            const uint4 e = wstack[sp];
-            cur = uni(e.x);
-            active = ((uint64_t)uni(e.z) << 32) | uni(e.y);
-        }
-        if (pass == 1) break;
-        // deferred re-verification of each lane's winner
-        bool redo = false;
-        if (mine && best.tri >= 0) {
-            const Ray64 ray = gen_ray(fp, opaque(i), j);
-            double hx, hy, hz;
-            (void)hit_dist(ray, best.t, hx, hy, hz);
-            const uint32_t leaf =
-                reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + 9)->y;
-            if (COUNT) n_chain++;
-            redo = !chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz) &&
-                   !chain_ok(sc, leaf, ray, n_chain_nodes);
-        }
-        need = uni64(__ballot(redo));
-    }
-    if (!valid) return;
-    Best out;
-    out.dist = best.dist;
-    out.rank = best.rank;
-    out.tri = best.tri;
-    out.px = out.py = out.pz = 0.0;
-    if (best.tri >= 0) {
-        const Ray64 ray = gen_ray(fp, opaque(i), j);
-        (void)hit_dist(ray, best.t, out.px, out.py, out.pz);
-    }
-    const size_t o = (size_t)r * fp.W + i;
-    shade_store(fp, sc, o, out);
-    if (COUNT && fp.counters) {
-        atomicAdd(&fp.counters[0], 1ull);
-        atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
-        atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
-        atomicAdd(&fp.counters[3], (unsigned long long)n_chain);
-        if (best.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
-        atomicAdd(&fp.counters[5], (unsigned long long)n_chain_nodes);
-        atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
-    }
-}
-
-template <int W, int SP, bool COUNT>
-__global__ void __launch_bounds__(256) k_trace_packet(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
-    __shared__ uint4 stacks[4][SP];
-    const int lane = threadIdx.x & 63;
-    uint4* wstack = stacks[threadIdx.x >> 6];
-    const int tiles_x = (fp.W + 7) >> 3;
-    const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
-    for (;;) {
-        int tile = 0;
-        if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);
-        tile = __shfl(tile, 0);
-        if (tile >= tiles) break;
-        const int i = (tile % tiles_x) * 8 + (lane & 7);
-        const int r = (tile / tiles_x) * 8 + (lane >> 3);
-        trace_packet<W, SP, COUNT>(sc, fp, i, r, i < fp.W && r < fp.nrows, wstack);
-    }
-}
+#include "packet_kernel.h"
 
 // Persistent waves: each wave pulls 8x8 pixel tiles from `tile_ctr` until the
 // shard is exhausted (every wave reaches the exit test each iteration).

@@ -171,8 +171,8 @@ void upload_one(rt_scene* s, int device) {
     d.node_bytes = rt_node_bytes(f.width);
     d.width = f.width;
     d.stack_bound = f.stack_bound;
-    HIP_TRY(hipMalloc(&r.d_counters, 8 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(r.d_counters, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&r.d_counters, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(r.d_counters, 0, 16 * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
@@ -441,7 +441,7 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         Replica& r = replica_for(s, device);
         DevGuard g(device);
         HIP_TRY(hipDeviceSynchronize());
-        unsigned long long c[8];
+        unsigned long long c[16];
         HIP_TRY(hipMemcpy(c, r.d_counters, sizeof c, hipMemcpyDeviceToHost));
         out->rays = c[0];
         out->node_fetches = c[1];
@@ -450,6 +450,9 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->hits = c[4];
         out->chain_nodes = c[5];
         out->tri_prefilter = c[6];
+        out->wave_nodes = c[7];
+        out->wave_leaves = c[8];
+        out->wave_tiles = c[9];
         if (reset) HIP_TRY(hipMemset(r.d_counters, 0, sizeof c));
         return RT_OK;
     } catch (const rt::Error& e) {

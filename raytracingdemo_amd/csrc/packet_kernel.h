@@ -1,20 +1,24 @@
 // Wave-cooperative ("packet") exact traversal kernel for gfx950.
 // Included by render.hip inside its anonymous namespace (uses Ray32, Win,
-// make_ray32, opaque and the rtk helpers).
+// make_ray32 and the rtk helpers).
 //
 // The 64 rays of one 8x8 pixel tile walk the tree together.  The current
 // node is wave-uniform, so its child records come in through the scalar data
 // path (s_load_dwordx8 per 32-B child, once per wave) instead of 64 per-lane
-// copies through the vector memory pipe; each lane slab-tests its own ray;
-// `ballot` turns the per-lane results into a 64-bit lane mask per child; the
-// wave continues into the child nearest to its first active lane and pushes
-// the others (ref + lane mask) on a wave-uniform stack in LDS.  Leaves are
-// tested the same way: uniform triangle records, a conservative per-lane fp32
-// pre-filter, fp64 Moller-Trumbore only for the lanes it cannot reject.
+// copies through the vector memory pipe; every lane slab-tests its own ray
+// against each child and `ballot` says whether any lane needs the child.  The
+// wave continues into the hit child nearest to the first lane that hit it and
+// pushes the others on a wave-uniform stack of node refs in LDS.
 //
-// Register budget: each lane's fp64 ray (o, d, 1/d) lives in LDS, not in
-// VGPRs/SGPRs, and children are loaded four at a time, so the 106-SGPR budget
-// holds the loop without spilling.  Exactness machinery as trace_exact.
+// No per-child lane masks are kept: all lanes of a wave execute every child
+// test anyway, and a lane that missed a parent box misses its children too
+// (real child boxes lie inside the parent box and outward rounding to fp32 is
+// monotone), so re-testing with every lane returns the same answers.  Lanes
+// that take no part in a pass carry tcull = -1, which fails every test.
+//
+// Leaves: uniform triangle records, a conservative per-lane fp32 pre-filter,
+// the exact fp64 Moller-Trumbore only for lanes it cannot reject.  Each lane's
+// fp64 ray (o, d, 1/d) lives in LDS.  Exactness machinery as trace_exact.
 #pragma once
 
 struct __attribute__((aligned(32))) ChildRec {  // 32-B child record (rt_device.h)
@@ -41,9 +45,6 @@ __device__ __forceinline__ ChildRec load_child(cchild_p p) {
 __device__ __forceinline__ float4 load_f4(cfloat_p p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-__device__ __forceinline__ uint64_t uni64(uint64_t x) {
-    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
-}
 
 // Per-lane fp64 ray in LDS: component k of lane l at ray[k * 64 + l]
 // (consecutive lanes -> consecutive 8-B words, conflict-free ds_read_b64).
@@ -59,6 +60,7 @@ __device__ __forceinline__ void store_ray(double* __restrict__ ray_lds, int lane
     ray_lds[8 * 64 + lane] = r.iz;
 }
 __device__ __forceinline__ Ray64 load_ray(const double* __restrict__ ray_lds, int lane) {
+    lane = opaque(lane);  // no store-to-load forwarding: the ray must stay in LDS, not VGPRs
     Ray64 r;
     r.ox = ray_lds[0 * 64 + lane];
     r.oy = ray_lds[1 * 64 + lane];
@@ -74,10 +76,9 @@ __device__ __forceinline__ Ray64 load_ray(const double* __restrict__ ray_lds, in
 
 template <int W, int SP, bool COUNT>
 __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrameParams& fp, int i, int r, bool valid,
-                                             uint4* __restrict__ wstack, double* __restrict__ ray_lds) {
+                                             uint32_t* __restrict__ wstack, double* __restrict__ ray_lds) {
     constexpr int G = W < 4 ? W : 4;  // children per scalar load group
     const int lane = threadIdx.x & 63;
-    const uint64_t me = 1ull << lane;
     if (!valid) { i = 0; r = 0; }
     const int j = fp.row0 + r * fp.row_stride;
     Ray32 q;
@@ -101,19 +102,19 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
     best.tri = -1;
     uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_pre = 0;
     uint32_t w_nodes = 0, w_leaves = 0;  // wave-level visits (COUNT only)
-    uint64_t need = uni64(__ballot(valid));
-    for (int pass = 0; pass < 2 && need; pass++) {
-        const bool mine = (need & me) != 0;
+    bool mine = valid;                   // this lane takes part in the pass
+    for (int pass = 0; pass < 2; pass++) {
+        if (__ballot(mine) == 0) break;
         if (mine) {
             best.dist = 1.7976931348623157e308;
             best.t = 0.0;
             best.rank = 0xFFFFFFFFu;
             best.tri = -1;
         }
-        float tcull = __builtin_huge_valf();
+        float tcull = mine ? __builtin_huge_valf() : -1.f;
         uint32_t chain_leaf = 0xFFFFFFFFu;
         bool chain_res = false;
-        bool root_hit = false;
+        uint32_t cur = sc.root_ref;
         {
             const float* b = sc.root_box;
             const float t0 = fmaxf(fmaxf(fminf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
@@ -121,29 +122,25 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
                                    fmaxf(fminf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), 0.f));
             const float t1 = fminf(fminf(fmaxf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
                                          fmaxf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
-                                   fmaxf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)));
-            root_hit = mine && t0 <= t1;
+                                   fminf(fmaxf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), tcull));
+            if (__ballot(t0 <= t1) == 0) cur = RT_INVALID_REF;
         }
-        uint64_t active = uni64(__ballot(root_hit));
-        uint32_t cur = sc.root_ref;
         int sp = 0;
         for (;;) {
-            if (active != 0 && cur != RT_INVALID_REF) {
-                const bool act = (active & me) != 0;
+            if (cur != RT_INVALID_REF) {
                 if (!(cur & RT_LEAF_BIT)) {
-                    if (COUNT && act) n_nodes++;
-                    if (COUNT) w_nodes++;
+                    if (COUNT) {
+                        w_nodes++;
+                        n_nodes += mine;
+                    }
                     const cchild_p nb = (cchild_p)(sc.nodes + (size_t)cur * (32 * W));
-                    float key[W];
-                    uint64_t m[W];
-                    uint32_t rb[W];
+                    uint32_t near_ref = RT_INVALID_REF, near_key = 0xFFFFFFFFu;
 #pragma unroll
                     for (int g = 0; g < W; g += G) {
                         __builtin_amdgcn_sched_barrier(0);  // bound the SGPRs of in-flight child records
 #pragma unroll
                         for (int c = g; c < g + G; c++) {
                             const ChildRec ch = load_child(nb + c);
-                            rb[c] = ch.ref;
                             const float tlx = __builtin_fmaf(ch.lx, q.ix, -olx);
                             const float thx = __builtin_fmaf(ch.hx, q.ix, -ohx);
                             const float tly = __builtin_fmaf(ch.ly, q.iy, -oly);
@@ -154,47 +151,27 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
                                 fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
                             const float t1 =
                                 fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
-                            const bool h = act && t0 <= t1;
-                            m[c] = ch.ref == RT_INVALID_REF ? 0ull : uni64(__ballot(h));
-                            // ordering key: the entry distance seen by the child's first lane
-                            key[c] = m[c] ? __uint_as_float((uint32_t)__builtin_amdgcn_readlane(
-                                                (int)__float_as_uint(t0), (int)__builtin_ctzll(m[c])))
-                                          : __builtin_huge_valf();
+                            const uint64_t hm = __ballot(t0 <= t1);
+                            if (hm != 0 && ch.ref != RT_INVALID_REF) {
+                                // entry distance (>= 0, so its bits order like the
+                                // value) of the first lane that hit the child
+                                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane(
+                                    (int)__float_as_uint(t0), (int)__builtin_ctzll(hm));
+                                uint32_t push = ch.ref;
+                                if (key < near_key) {
+                                    push = near_ref;
+                                    near_ref = ch.ref;
+                                    near_key = key;
+                                }
+                                if (push != RT_INVALID_REF) {
+                                    if (lane == 0) wstack[sp] = push;
+                                    sp++;
+                                }
+                            }
                         }
                     }
-                    // nearest child continues; the others go on the stack, farthest first
-                    int nearest = -1;
-                    float kn = __builtin_huge_valf();
-#pragma unroll
-                    for (int c = 0; c < W; c++)
-                        if (m[c] && (nearest < 0 || key[c] < kn)) { kn = key[c]; nearest = c; }
-                    if (nearest >= 0) {
-                        uint32_t left = 0;
-#pragma unroll
-                        for (int c = 0; c < W; c++)
-                            if (m[c] && c != nearest) left |= 1u << c;
-                        while (left) {
-                            int far_c = 0;
-                            float kf = -1.f;
-#pragma unroll
-                            for (int c = 0; c < W; c++)
-                                if (((left >> c) & 1u) && key[c] >= kf) { kf = key[c]; far_c = c; }
-                            uint64_t fm = 0;
-                            uint32_t fr = 0;
-#pragma unroll
-                            for (int c = 0; c < W; c++)
-                                if (c == far_c) { fm = m[c]; fr = rb[c]; }
-                            if (lane == 0) wstack[sp] = make_uint4(fr, (uint32_t)fm, (uint32_t)(fm >> 32), 0u);
-                            sp++;
-                            left &= ~(1u << far_c);
-                        }
-                        uint64_t nm = 0;
-                        uint32_t nr = 0;
-#pragma unroll
-                        for (int c = 0; c < W; c++)
-                            if (c == nearest) { nm = m[c]; nr = rb[c]; }
-                        cur = nr;
-                        active = nm;
+                    if (near_ref != RT_INVALID_REF) {
+                        cur = near_ref;
                         continue;
                     }
                 } else {
@@ -204,9 +181,9 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
                     for (uint32_t k = first; k < first + cnt; k++) {
                         const cfloat_p R = (cfloat_p)(sc.tri32 + 12 * (size_t)k);  // scalar loads
                         const float4 A = load_f4(R), B = load_f4(R + 4), Cc = load_f4(R + 8);
-                        if (COUNT && act) n_pre++;
+                        if (COUNT) n_pre += mine;
                         const bool pre =
-                            act && tri_prefilter(A, B, Cc, q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull);
+                            mine && tri_prefilter(A, B, Cc, q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull);
                         if (__ballot(pre) == 0) continue;
                         if (!pre) continue;
                         if (COUNT) n_tris++;
@@ -236,9 +213,7 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
             }
             if (sp == 0) break;
             sp--;
-            const uint4 e = wstack[sp];
-            cur = uni(e.x);
-            active = ((uint64_t)uni(e.z) << 32) | uni(e.y);
+            cur = uni(wstack[sp]);
         }
         if (pass == 1) break;
         // deferred re-verification of each lane's winner
@@ -253,7 +228,7 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
             redo = !chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz) &&
                    !chain_ok(sc, leaf, ray, n_chain_nodes);
         }
-        need = uni64(__ballot(redo));
+        mine = redo;
     }
     if (COUNT && fp.counters && lane == 0) {
         atomicAdd(&fp.counters[7], (unsigned long long)w_nodes);
@@ -287,7 +262,7 @@ __device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrame
 // (the host falls back to the per-lane kernel otherwise), so no push can drop.
 template <int W, int SP, bool COUNT>
 __global__ void __launch_bounds__(256) k_trace_packet(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
-    __shared__ uint4 stacks[4][SP];
+    __shared__ uint32_t stacks[4][SP];
     __shared__ double rays[4][9 * 64];
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;

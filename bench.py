@@ -168,6 +168,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # diagnostic builds: per-wave clock split of the timed launches
+    diag = scene.frame_stats(local, reset=True)["diag_cycles"]
+    tiles_timed = a.steps * F * ((W + 7) // 8) * ((my_rows + 7) // 8)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -210,6 +213,10 @@ def main():
                                      "chain_nodes": round(cs["chain_nodes"] / max(cs["rays"], 1), 4),
                                      "wave_nodes_per_tile": round(cs["wave_nodes"] / max(cs["wave_tiles"], 1), 2),
                                      "wave_leaves_per_tile": round(cs["wave_leaves"] / max(cs["wave_tiles"], 1), 2),
+                                     "redo_rays": round(cs["redo_rays"] / max(cs["rays"], 1), 7),
+                                     "redo_chain": round(cs["redo_chain"] / max(cs["rays"], 1), 7),
+                                     **({"diag_ticks_per_tile": [round(x / tiles_timed) for x in diag]}
+                                        if any(diag) else {}),
                                      "node_bytes": st["node_bytes"], "tri32_bytes": TRI32_BYTES,
                                      "tri64_bytes": TRI64_BYTES}},
             "cpu_baseline": cpu,

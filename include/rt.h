@@ -111,6 +111,11 @@ typedef struct {
     uint64_t wave_nodes;    /* packet kernel: inner-node visits per wave */
     uint64_t wave_leaves;   /* packet kernel: leaf visits per wave       */
     uint64_t wave_tiles;    /* packet kernel: 8x8 tiles traced           */
+    uint64_t redo_rays;     /* rays finished by the fix-up kernel (exact per-lane path) */
+    uint64_t redo_chain;    /*   of which: winner invisible to the reference (chain check) */
+    uint64_t diag_cycles[8]; /* diagnostic builds only (else 0): wave clock ticks in
+                                node-load wait, node work, leaves, stack pops, ray
+                                set-up, exact resolve, output, tile fetch */
 } rt_frame_stats_t;
 
 /* objl::Loader + ObjectLoader::loadFromFile (object_loader.hpp:14-70,

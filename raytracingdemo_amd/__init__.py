@@ -137,7 +137,11 @@ class Scene:
     def stats(self) -> dict:
         s = N.rt_scene_stats_t()
         N.check(N.lib().rt_scene_stats(self._h, C.byref(s)))
-        return {f: getattr(s, f) for f, _ in s._fields_}
+        out = {}
+        for f, _ in s._fields_:
+            v = getattr(s, f)
+            out[f] = list(v) if isinstance(v, C.Array) else v
+        return out
 
     def tree_dump(self) -> TreeDump:
         st = self.stats()
@@ -188,7 +192,11 @@ class Scene:
     def frame_stats(self, device: int = 0, reset: bool = True) -> dict:
         s = N.rt_frame_stats_t()
         N.check(N.lib().rt_frame_stats(self._h, int(device), int(reset), C.byref(s)))
-        return {f: getattr(s, f) for f, _ in s._fields_}
+        out = {}
+        for f, _ in s._fields_:
+            v = getattr(s, f)
+            out[f] = list(v) if isinstance(v, C.Array) else v
+        return out
 
 
 def ppm_bytes(rgb: np.ndarray, W: int, H: int) -> bytes:

@@ -372,6 +372,25 @@ struct Flattener {
     // grouped under virtual wide nodes whose slot box is the union of the
     // group's boxes (a conservative superset; the exact ancestor chain used by
     // the fp64 re-verification only contains real nodes).
+    // Slot 0's pad word carries the node's ordering hint for the packet
+    // kernel: bits 0-1 the axis its children are sorted along (the builder's
+    // partition axis: longest axis of the node box, main k-way order), bits
+    // 2-6 the number of valid slots (valid slots come first).
+    void set_meta(uint32_t node, const std::vector<int32_t>& kids, uint32_t nvalid) {
+        double mn[3], mx[3];
+        for (int a = 0; a < 3; a++) {
+            mn[a] = std::numeric_limits<double>::infinity();
+            mx[a] = -std::numeric_limits<double>::infinity();
+        }
+        for (int32_t k : kids)
+            for (int a = 0; a < 3; a++) {
+                mn[a] = std::min(mn[a], t.nodes[k].mn[a]);
+                mx[a] = std::max(mx[a], t.nodes[k].mx[a]);
+            }
+        uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + (size_t)node * nb);
+        p[7] = (uint32_t)longest_axis(mn, mx) | (nvalid << 2);
+    }
+
     uint32_t emit_inner(const std::vector<int32_t>& kids, uint32_t depth) {
         uint32_t id = alloc_node();
         wide_depth = std::max(wide_depth, depth + 1);
@@ -382,10 +401,12 @@ struct Flattener {
                 uint32_t r = ref_of(kids[c], depth + 1);
                 set_slot(id, (int)c, b6, r);
             }
+            set_meta(id, kids, (uint32_t)kids.size());
             return id;
         }
         size_t groups = std::min<size_t>((size_t)W, (kids.size() + W - 1) / W);
         size_t per = (kids.size() + groups - 1) / groups;
+        uint32_t nslots = 0;
         for (size_t g = 0; g < groups; g++) {
             size_t a = g * per, b = std::min(kids.size(), a + per);
             if (a >= b) break;
@@ -403,7 +424,9 @@ struct Flattener {
             }
             uint32_t r = sub.size() == 1 ? ref_of(sub[0], depth + 1) : emit_inner(sub, depth + 1);
             set_slot(id, (int)g, b6, r);
+            nslots++;
         }
+        set_meta(id, kids, nslots);
         return id;
     }
 };
@@ -455,7 +478,7 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     // --- per-triangle data in BVH order
     const uint64_t n = s.n;
     f.tri64.resize(n * RT_TRI64_DOUBLES);
-    f.tri32.resize(n * 12, 0.0f);
+    f.tri32.resize((n + RT_TRI32_PAD) * 12, 0.0f);  // + padding records (packet kernel leaf chunks)
     f.tri_id.resize(n);
     f.tri_rank.resize(n);
     f.tri_leaf.resize(n);

@@ -108,6 +108,53 @@ __device__ __forceinline__ bool tri_prefilter(const float4 A, const float4 B, co
     return true;
 }
 
+// Classifying variant of tri_prefilter for the deferred fp64 resolve.
+//   0  the exact fp64 test must reject (or t > tcull)
+//   1  borderline: only the fp64 test can decide
+//   2  certain: every fp64 decision passes with margin (|a| >= EPS, u, v,
+//      u+v, t > EPS all clear their bounds by a full budget, which is >= 3/4
+//      budget beyond the real value — far above fp64 rounding), so the true
+//      hit parameter is <= tu and tu may tighten the culling distance.
+// tl / tu bound the true t = T/a from below / above whenever class != 0.
+__device__ __forceinline__ int tri_classify(const float4 A, const float4 B, const float4 C, float ox, float oy,
+                                            float oz, float dx, float dy, float dz, float co, float tcull, float& tl,
+                                            float& tu) {
+    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = C.x;
+    const float M1 = C.y, M2 = C.z, Cv = C.w;
+    const float sx = ox - A.x, sy = oy - A.y, sz = oz - A.z;
+    const float hx = __builtin_fmaf(dy, e2z, -dz * e2y);
+    const float hy = __builtin_fmaf(dz, e2x, -dx * e2z);
+    const float hz = __builtin_fmaf(dx, e2y, -dy * e2x);
+    const float a = __builtin_fmaf(e1x, hx, __builtin_fmaf(e1y, hy, e1z * hz));
+    const float U = __builtin_fmaf(sx, hx, __builtin_fmaf(sy, hy, sz * hz));
+    const float qx = __builtin_fmaf(sy, e1z, -sz * e1y);
+    const float qy = __builtin_fmaf(sz, e1x, -sx * e1z);
+    const float qz = __builtin_fmaf(sx, e1y, -sy * e1x);
+    const float V = __builtin_fmaf(dx, qx, __builtin_fmaf(dy, qy, dz * qz));
+    const float T = __builtin_fmaf(e2x, qx, __builtin_fmaf(e2y, qy, e2z * qz));
+    const float Ms = fmaxf(fmaxf(__builtin_fabsf(sx), __builtin_fabsf(sy)), __builtin_fabsf(sz));
+    const float u = 0x1p-24f;
+    const float G = __builtin_fmaf(256.f, Ms, 64.f * (co + Cv));
+    const float errA = 256.f * u * M1 * M2;
+    const float errU = u * M2 * G, errV = u * M1 * G, errT = u * M1 * M2 * G;
+    const float aa = __builtin_fabsf(a);
+    tl = 0.f;
+    tu = __builtin_huge_valf();
+    if (!(aa > errA)) return 1;  // sign of the determinant uncertain: let fp64 decide
+    const float sg = a > 0.f ? 1.f : -1.f;
+    const float Us = sg * U, Vs = sg * V, Ts = sg * T;
+    if (Us < -errU || Vs < -errV || Ts < -errT) return 0;
+    if (Us + Vs > aa + errU + errV + errA) return 0;
+    if (Ts - errT > tcull * (aa + errA)) return 0;  // t > tcull: cannot improve
+    tl = fmaxf((Ts - errT) / (aa + errA), 0.f) * (1.f - 0x1p-20f);
+    const float EPS = 1e-8f;
+    const bool certain = Us >= errU && Vs >= errV && Us + Vs <= aa - errU - errV - errA && aa - errA >= 2.f * EPS &&
+                         Ts - errT >= 2.f * EPS * (aa + errA);
+    if (!certain) return 1;
+    tu = (Ts + errT) / (aa - errA) * (1.f + 0x1p-20f);
+    return 2;
+}
+
 // main.cpp:332-337: d = dir + up*py + right*px; d *= 1/|d|; Ray{pos, d}
 __device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) {
     const double px = fp.px[i], py = fp.py[j];
@@ -150,7 +197,10 @@ __device__ __forceinline__ double hit_dist(const Ray64& r, double t, double& px,
 }
 
 // shadeScreen body (main.cpp:356-377) + PPM byte cast (benchmark.hpp:105-114)
-__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDevScene& sc, size_t o, const Best& b) {
+// count_hit: add this pixel's hit to fp.hit_count here (one atomic per wave);
+// k_resolve instead reduces per block and k_fixup adds the block sums once.
+__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDevScene& sc, size_t o, const Best& b,
+                                            bool count_hit = true) {
     uint8_t c0 = 0, c1 = 0, c2 = 0;
     if (b.tri >= 0 && fp.rgb) {
         const uint32_t id = sc.tri_id[b.tri];
@@ -185,7 +235,12 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDev
         fp.hit_pos[3 * o + 1] = b.tri >= 0 ? b.py : 0.0;
         fp.hit_pos[3 * o + 2] = b.tri >= 0 ? b.pz : 0.0;
     }
-    if (b.tri >= 0 && fp.hit_count) atomicAdd(fp.hit_count, 1ull);
+    if (count_hit && fp.hit_count) {  // one atomic per wave (all active lanes reach this)
+        const uint64_t hits = __ballot(b.tri >= 0);
+        const uint64_t act = __ballot(1);
+        if (hits != 0 && (int)(threadIdx.x & 63) == __builtin_ctzll(act))
+            atomicAdd(fp.hit_count, (unsigned long long)__builtin_popcountll(hits));
+    }
 }
 
 template <int W>

@@ -1,6 +1,6 @@
 // Wave-cooperative ("packet") exact traversal kernel for gfx950.
 // Included by render.hip inside its anonymous namespace (uses Ray32, Win,
-// make_ray32 and the rtk helpers).
+// make_ray32, trace_exact and the rtk helpers).
 //
 // The 64 rays of one 8x8 pixel tile walk the tree together.  The current
 // node is wave-uniform, so its child records come in through the scalar data
@@ -14,12 +14,53 @@
 // test anyway, and a lane that missed a parent box misses its children too
 // (real child boxes lie inside the parent box and outward rounding to fp32 is
 // monotone), so re-testing with every lane returns the same answers.  Lanes
-// that take no part in a pass carry tcull = -1, which fails every test.
+// outside the image carry tcull = -1, which fails every test.
 //
-// Leaves: uniform triangle records, a conservative per-lane fp32 pre-filter,
-// the exact fp64 Moller-Trumbore only for lanes it cannot reject.  Each lane's
-// fp64 ray (o, d, 1/d) lives in LDS.  Exactness machinery as trace_exact.
+// The walk itself is fp32 only.  Leaf triangles go through tri_classify:
+// rejected, "certain" (the fp64 test provably passes and its t is bounded
+// above, so the culling distance tightens at once) or "borderline".  Both
+// kinds of survivor are appended to the lane's candidate list in LDS (index +
+// lower bound of t).  After the walk the survivors that can still win go to
+// HBM, and k_resolve (one pixel per lane, full occupancy) runs the exact fp64
+// Moller-Trumbore, picks the (distance, visit rank) minimum and re-verifies
+// the winner's reference ancestor chain.  A pixel whose list overflowed, or
+// whose winner the reference could not see, is appended to the redo list and
+// finished by k_fixup (the per-lane kernel).  Keeping fp64 out of
+// the walk keeps it at < 64 VGPRs.
 #pragma once
+
+// Tile scheduling of the packet kernel: 0 one device-wide queue, 1 one queue
+// per XCD (default), 2 static round-robin (diagnostic).
+#ifndef RT_TILE_SCHED
+#define RT_TILE_SCHED 1
+#endif
+
+// Cycle-split diagnostic (RT_DIAG_TIMING builds only): per-wave s_memtime
+// deltas accumulated over the whole persistent loop and flushed once per wave
+// into aux.diag[0..7]: node-load wait, node work, leaves, stack pops, ray
+// set-up, exact resolve, output stores, tile fetch.
+#ifdef RT_DIAG_TIMING
+#define RT_TSTAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define RT_TACC(slot, t0) (tacc[slot] += __builtin_amdgcn_s_memtime() - (t0))
+#else
+#define RT_TSTAMP(v)
+#define RT_TACC(slot, t0)
+#endif
+
+// Node record fetch: 0 scalar loads (default), 1 uniform vector loads.
+#ifndef RT_NODE_FETCH
+#define RT_NODE_FETCH 0
+#endif
+
+// Occupancy target of the packet kernel (waves per SIMD); 0 = compiler's choice.
+#ifndef RT_PACKET_WPE
+#define RT_PACKET_WPE 0
+#endif
+#if RT_PACKET_WPE > 0
+#define RT_PACKET_ATTR __attribute__((amdgpu_waves_per_eu(RT_PACKET_WPE)))
+#else
+#define RT_PACKET_ATTR
+#endif
 
 struct __attribute__((aligned(32))) ChildRec {  // 32-B child record (rt_device.h)
     float lx, hx, ly, hy, lz, hz;
@@ -46,235 +87,470 @@ __device__ __forceinline__ float4 load_f4(cfloat_p p) { return make_float4(p[0],
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
-// Per-lane fp64 ray in LDS: component k of lane l at ray[k * 64 + l]
-// (consecutive lanes -> consecutive 8-B words, conflict-free ds_read_b64).
-__device__ __forceinline__ void store_ray(double* __restrict__ ray_lds, int lane, const Ray64& r) {
-    ray_lds[0 * 64 + lane] = r.ox;
-    ray_lds[1 * 64 + lane] = r.oy;
-    ray_lds[2 * 64 + lane] = r.oz;
-    ray_lds[3 * 64 + lane] = r.dx;
-    ray_lds[4 * 64 + lane] = r.dy;
-    ray_lds[5 * 64 + lane] = r.dz;
-    ray_lds[6 * 64 + lane] = r.ix;
-    ray_lds[7 * 64 + lane] = r.iy;
-    ray_lds[8 * 64 + lane] = r.iz;
+// v_writelane_b32: lane L of `v` := uniform `x`
+template <int L>
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
+    return v;
 }
-__device__ __forceinline__ Ray64 load_ray(const double* __restrict__ ray_lds, int lane) {
-    lane = opaque(lane);  // no store-to-load forwarding: the ray must stay in LDS, not VGPRs
-    Ray64 r;
-    r.ox = ray_lds[0 * 64 + lane];
-    r.oy = ray_lds[1 * 64 + lane];
-    r.oz = ray_lds[2 * 64 + lane];
-    r.dx = ray_lds[3 * 64 + lane];
-    r.dy = ray_lds[4 * 64 + lane];
-    r.dz = ray_lds[5 * 64 + lane];
-    r.ix = ray_lds[6 * 64 + lane];
-    r.iy = ray_lds[7 * 64 + lane];
-    r.iz = ray_lds[8 * 64 + lane];
-    return r;
+// A zero the compiler must treat as per-lane (forces vector-memory loads).
+__device__ __forceinline__ int vzero() {
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
 }
 
-template <int W, int SP, bool COUNT>
-__device__ __forceinline__ void trace_packet(const RtDevScene& sc, const RtFrameParams& fp, int i, int r, bool valid,
-                                             uint32_t* __restrict__ wstack, double* __restrict__ ray_lds) {
-    constexpr int G = W < 4 ? W : 4;  // children per scalar load group
-    const int lane = threadIdx.x & 63;
-    if (!valid) { i = 0; r = 0; }
-    const int j = fp.row0 + r * fp.row_stride;
-    Ray32 q;
-    double tslack;
-    {
-        const Ray64 ray = gen_ray(fp, i, j);
-        store_ray(ray_lds, lane, ray);
-        q = make_ray32(ray, fp.pad);
-        tslack = 0x1p-40 * ((double)q.co + 1.0);
+template <int W>
+__device__ __forceinline__ uint32_t lanes_of(const ChildRec (&ch)[W]) {
+    uint32_t v = 0;
+    [&]<int... L>(std::integer_sequence<int, L...>) { ((v = writelane<L>(v, ch[L].ref)), ...); }(
+        std::make_integer_sequence<int, W>{});
+    return v;
+}
+
+constexpr uint32_t kRedoPass1 = 0x80000000u;
+constexpr int kLeafChunk = 4;  // triangle records fetched per scalar round trip
+constexpr uint32_t kCandDropped = 0x80;  // cand_cnt flag: candidates were dropped (bound in cand_drop)
+static_assert(kLeafChunk == RT_TRI32_PAD, "tri32 padding must cover a leaf chunk");
+
+// Forces uniform values to be materialised (their loads waited on) here, so
+// a chunk's loads are all in flight before the first use.
+__device__ __forceinline__ void pin_s(const float4& a, const float4& b, const float4& c) {
+    asm volatile("" ::"s"(a.x), "s"(a.y), "s"(a.z), "s"(a.w), "s"(b.x), "s"(b.y), "s"(b.z), "s"(b.w), "s"(c.x),
+                 "s"(c.y), "s"(c.z), "s"(c.w));
+}  // redo entry: start directly with the inline-verifying pass
+
+// Lane-private candidate list: entry c of lane l at cand[c * 64 + l]
+// ({triangle, bits of t lower bound}; consecutive lanes -> consecutive 8-B
+// words, conflict-free ds_read/write_b64).
+// List full after compaction: keep the K entries with the smallest t lower
+// bound among the list and the new candidate; returns the bound dropped.
+template <int K>
+__device__ __forceinline__ float keep_nearest(uint2* __restrict__ cand, int lane, uint32_t k, float tl) {
+    int far_c = 0;
+    float far_t = __uint_as_float(cand[lane].y);
+    for (int c = 1; c < K; c++) {
+        const float t = __uint_as_float(cand[c * 64 + lane].y);
+        if (t > far_t) { far_t = t; far_c = c; }
     }
+    if (tl >= far_t) return tl;
+    cand[far_c * 64 + lane] = make_uint2(k, __float_as_uint(tl));
+    return far_t;
+}
+
+template <int K>
+__device__ __forceinline__ int compact_candidates(uint2* __restrict__ cand, int lane, float tcull) {
+    int m = 0;
+    for (int c = 0; c < K; c++) {
+        const uint2 e = cand[c * 64 + lane];
+        if (__uint_as_float(e.y) <= tcull) {
+            cand[m * 64 + lane] = e;
+            m++;
+        }
+    }
+    return m;
+}
+
+// Kernel arguments.  Each workgroup copies the argument block from the
+// kernarg segment into LDS once; copies of the parameter structs are then
+// taken from a laundered LDS pointer right where they are needed (ray
+// set-up, resolve), so the compiler can neither keep ~60 SGPRs of frame and
+// scene constants alive across the walk (the walk needs the SGPRs for the
+// child records of a whole node in flight) nor re-read the kernarg segment
+// (host-coherent memory, far slower) per tile.
+struct PacketArgs {
+    RtDevScene sc;
+    RtFrameParams fp;
+    RtLaunchAux aux;
+};
+static_assert(sizeof(PacketArgs) % 4 == 0, "argument block is copied as words");
+typedef const __attribute__((address_space(3))) PacketArgs* args_p;
+
+__device__ __forceinline__ args_p launder(args_p p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// Word-wise uniform copy out of the LDS argument block (unused words fold away).
+template <class T>
+__device__ __forceinline__ T kload(const __attribute__((address_space(3))) T* p) {
+    static_assert(sizeof(T) % 4 == 0, "argument structs are word-sized");
+    T out;
+    const __attribute__((address_space(3))) uint32_t* src = (const __attribute__((address_space(3))) uint32_t*)p;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+    for (unsigned w = 0; w < sizeof(T) / 4; w++) dst[w] = uni(src[w]);
+    return out;
+}
+template <class T>
+__device__ __forceinline__ T kword(const __attribute__((address_space(3))) T* p) {
+    static_assert(sizeof(T) == 4, "one word");
+    return __builtin_bit_cast(T, uni(*(const __attribute__((address_space(3))) uint32_t*)p));
+}
+
+template <int W, int SP, int K, bool COUNT>
+__device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid, uint32_t* __restrict__ wstack,
+                                             uint2* __restrict__ cand, uint64_t* tacc) {
+    const int lane = threadIdx.x & 63;
+    RT_TSTAMP(t_setup);
+    if (!valid) { i = 0; r = 0; }
+    Ray32 q;
+    float tsl;  // distance slack (see trace_exact), fp32 rounded up
+    float pd;
+    {
+        const RtFrameParams fp = kload(&A->fp);
+        const Ray64 ray = gen_ray(fp, i, fp.row0 + r * fp.row_stride);
+        q = make_ray32(ray, fp.pad);
+        tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
+        pd = fp.pad;
+    }
+    // direction sign bits (x, y, z) of lane 0's ray: the tile's ordering key
+    const uint32_t dsg = uni((q.ix < 0.f ? 1u : 0u) | (q.iy < 0.f ? 2u : 0u) | (q.iz < 0.f ? 4u : 0u));
+    const RT_G uint8_t* const nodes = kload(&A->sc.nodes);
+    const RT_G float* const tri32 = kload(&A->sc.tri32);
     // slab offsets for the lo / hi planes (pad moves lo down and hi up)
-    const float pd = fp.pad;
     const float olx = (q.ox + pd) * q.ix, ohx = (q.ox - pd) * q.ix;
     const float oly = (q.oy + pd) * q.iy, ohy = (q.oy - pd) * q.iy;
     const float olz = (q.oz + pd) * q.iz, ohz = (q.oz - pd) * q.iz;
 
-    Win best;
-    best.dist = 1.7976931348623157e308;
-    best.t = 0.0;
-    best.rank = 0xFFFFFFFFu;
-    best.tri = -1;
-    uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_pre = 0;
-    uint32_t w_nodes = 0, w_leaves = 0;  // wave-level visits (COUNT only)
-    bool mine = valid;                   // this lane takes part in the pass
-    for (int pass = 0; pass < 2; pass++) {
-        if (__ballot(mine) == 0) break;
-        if (mine) {
-            best.dist = 1.7976931348623157e308;
-            best.t = 0.0;
-            best.rank = 0xFFFFFFFFu;
-            best.tri = -1;
-        }
-        float tcull = mine ? __builtin_huge_valf() : -1.f;
-        uint32_t chain_leaf = 0xFFFFFFFFu;
-        bool chain_res = false;
-        uint32_t cur = sc.root_ref;
-        {
-            const float* b = sc.root_box;
-            const float t0 = fmaxf(fmaxf(fminf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
-                                         fminf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
-                                   fmaxf(fminf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), 0.f));
-            const float t1 = fminf(fminf(fmaxf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
-                                         fmaxf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
-                                   fminf(fmaxf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), tcull));
-            if (__ballot(t0 <= t1) == 0) cur = RT_INVALID_REF;
-        }
-        int sp = 0;
-        for (;;) {
-            if (cur != RT_INVALID_REF) {
-                if (!(cur & RT_LEAF_BIT)) {
-                    if (COUNT) {
-                        w_nodes++;
-                        n_nodes += mine;
+    uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0;  // COUNT only
+    float tcull = valid ? __builtin_huge_valf() : -1.f;
+    int nc = 0;         // candidates in the lane's list
+    float drop = __builtin_huge_valf();  // smallest t lower bound of a dropped candidate
+    uint32_t cur = kword(&A->sc.root_ref);
+    {
+        float b[6];
+        for (int a = 0; a < 6; a++) b[a] = kword(&A->sc.root_box[a]);
+        const float t0 = fmaxf(fmaxf(fminf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
+                                     fminf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
+                               fmaxf(fminf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), 0.f));
+        const float t1 = fminf(fminf(fmaxf(__builtin_fmaf(b[0], q.ix, -olx), __builtin_fmaf(b[1], q.ix, -ohx)),
+                                     fmaxf(__builtin_fmaf(b[2], q.iy, -oly), __builtin_fmaf(b[3], q.iy, -ohy))),
+                               fminf(fmaxf(__builtin_fmaf(b[4], q.iz, -olz), __builtin_fmaf(b[5], q.iz, -ohz)), tcull));
+        if (__ballot(t0 <= t1) == 0) cur = RT_INVALID_REF;
+    }
+    int sp = 0;
+    RT_TACC(4, t_setup);
+    for (;;) {
+        if (cur != RT_INVALID_REF) {
+            if (!(cur & RT_LEAF_BIT)) {
+                RT_TSTAMP(t_n0);
+                if (COUNT) {
+                    w_nodes++;
+                    n_nodes += valid;
+                }
+                float bx[W][6];  // child boxes {lx, hx, ly, hy, lz, hz}
+                uint32_t refv;   // lane c: child c's ref
+                uint32_t meta;   // slot 0's pad: sort axis | valid slots << 2 (bvh_build.cpp set_meta)
+#if RT_NODE_FETCH == 0
+                {
+                    // scalar path: all W records are loaded before any branch
+                    // so their loads are in flight together
+                    const cchild_p nb = (cchild_p)(nodes + (size_t)cur * (32 * W));
+                    ChildRec ch[W];
+#pragma unroll
+                    for (int c = 0; c < W; c++) ch[c] = load_child(nb + c);
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;
+                        bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
                     }
-                    const cchild_p nb = (cchild_p)(sc.nodes + (size_t)cur * (32 * W));
-                    uint32_t near_ref = RT_INVALID_REF, near_key = 0xFFFFFFFFu;
+                    // built before any branch so the ref words load with the
+                    // boxes, not in a second round trip
+                    refv = lanes_of<W>(ch);
+                    meta = ch[0].pad;
+                }
+#else
+                {
+                    // vector path: every lane loads the same record words
+                    // (one request per wave-instruction through the vector
+                    // L1), lane c loads child c's ref
+                    const RT_G uint32_t* nw = (const RT_G uint32_t*)(nodes + (size_t)cur * (32 * W)) + vzero();
 #pragma unroll
-                    for (int g = 0; g < W; g += G) {
-                        __builtin_amdgcn_sched_barrier(0);  // bound the SGPRs of in-flight child records
+                    for (int c = 0; c < W; c++) {
+                        const float4 a = *(const RT_G float4*)(nw + 8 * c);
+                        const float2 b = *(const RT_G float2*)(nw + 8 * c + 4);
+                        bx[c][0] = a.x; bx[c][1] = a.y; bx[c][2] = a.z; bx[c][3] = a.w;
+                        bx[c][4] = b.x; bx[c][5] = b.y;
+                    }
+                    refv = nw[8 * (lane & (W - 1)) + RT_CHILD_REF];
+                    meta = uni(nw[7]);
+                }
+#endif
+#ifdef RT_DIAG_TIMING
+                asm volatile("" : "+v"(refv));
+#endif
+                RT_TACC(0, t_n0);
+                RT_TSTAMP(t_n1);
+                uint32_t mask = 0;
 #pragma unroll
-                        for (int c = g; c < g + G; c++) {
-                            const ChildRec ch = load_child(nb + c);
-                            const float tlx = __builtin_fmaf(ch.lx, q.ix, -olx);
-                            const float thx = __builtin_fmaf(ch.hx, q.ix, -ohx);
-                            const float tly = __builtin_fmaf(ch.ly, q.iy, -oly);
-                            const float thy = __builtin_fmaf(ch.hy, q.iy, -ohy);
-                            const float tlz = __builtin_fmaf(ch.lz, q.iz, -olz);
-                            const float thz = __builtin_fmaf(ch.hz, q.iz, -ohz);
-                            const float t0 =
-                                fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
-                            const float t1 =
-                                fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
-                            const uint64_t hm = __ballot(t0 <= t1);
-                            if (hm != 0 && ch.ref != RT_INVALID_REF) {
-                                // entry distance (>= 0, so its bits order like the
-                                // value) of the first lane that hit the child
-                                const uint32_t key = (uint32_t)__builtin_amdgcn_readlane(
-                                    (int)__float_as_uint(t0), (int)__builtin_ctzll(hm));
-                                uint32_t push = ch.ref;
-                                if (key < near_key) {
-                                    push = near_ref;
-                                    near_ref = ch.ref;
-                                    near_key = key;
-                                }
-                                if (push != RT_INVALID_REF) {
-                                    if (lane == 0) wstack[sp] = push;
-                                    sp++;
-                                }
+                for (int c = 0; c < W; c++) {
+                    const float tlx = __builtin_fmaf(bx[c][0], q.ix, -olx);
+                    const float thx = __builtin_fmaf(bx[c][1], q.ix, -ohx);
+                    const float tly = __builtin_fmaf(bx[c][2], q.iy, -oly);
+                    const float thy = __builtin_fmaf(bx[c][3], q.iy, -ohy);
+                    const float tlz = __builtin_fmaf(bx[c][4], q.iz, -olz);
+                    const float thz = __builtin_fmaf(bx[c][5], q.iz, -ohz);
+                    const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
+                    const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
+                    mask |= __ballot(t0 <= t1) != 0 ? (1u << c) : 0u;
+                }
+                mask &= (1u << (meta >> 2)) - 1u;
+                if (mask != 0) {
+                    // children are sorted along `axis`: walk them front to back
+                    // for the tile's direction (lowest index first when the
+                    // tile looks along +axis)
+                    const bool rev = (dsg >> (meta & 3u)) & 1u;
+                    const int near_c = rev ? 31 - __builtin_clz(mask) : __builtin_ctz(mask);
+                    const uint32_t pm = mask & ~(1u << near_c);
+                    if (pm != 0) {
+                        // the rest go on the stack so that they pop in order
+                        const uint32_t below = pm & ((1u << (lane & 31)) - 1u);
+                        const uint32_t above = (pm >> (lane & 31)) >> 1;
+                        const int slot = (int)__builtin_popcount(rev ? below : above);
+                        if ((pm >> (lane & 31)) & 1u & (lane < W)) wstack[sp + slot] = refv;
+                        sp += __builtin_popcount(pm);
+                    }
+                    cur = (uint32_t)__builtin_amdgcn_readlane((int)refv, near_c);
+                    RT_TACC(1, t_n1);
+                    continue;
+                }
+                RT_TACC(1, t_n1);
+            } else {
+                RT_TSTAMP(t_l0);
+                const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+                const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+                if (COUNT) w_leaves++;
+                // triangles come in chunks of kLeafChunk records: all their
+                // scalar loads are issued, then waited on once (tri32 carries
+                // kLeafChunk padding records, so reading past a leaf is safe)
+                const uint32_t end = first + cnt;
+                for (uint32_t k0 = first; k0 < end; k0 += kLeafChunk) {
+                    const cfloat_p R = (cfloat_p)(tri32 + 12 * (size_t)k0);
+                    float4 TA[kLeafChunk], TB[kLeafChunk], TC[kLeafChunk];
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        TA[t] = load_f4(R + 12 * t);
+                        TB[t] = load_f4(R + 12 * t + 4);
+                        TC[t] = load_f4(R + 12 * t + 8);
+                    }
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) pin_s(TA[t], TB[t], TC[t]);
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        const uint32_t k = k0 + t;
+                        if (k >= end) break;
+                        if (COUNT) n_pre += valid;
+                        float tl, tu;
+                        const int cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz,
+                                                             q.co, tcull, tl, tu)
+                                              : 0;
+                        if (__ballot(cls != 0) == 0) continue;
+                        if (cls != 0) {
+                            // dist of a certain hit <= (tu + slack)(1 + 2^-20)
+                            if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
+                            if (nc == K) nc = compact_candidates<K>(cand, lane, tcull);
+                            if (nc < K) {
+                                cand[nc * 64 + lane] = make_uint2(k, __float_as_uint(tl));
+                                nc++;
+                            } else {
+                                // full: keep the K smallest lower bounds, remember the
+                                // smallest bound dropped (k_resolve certifies the winner
+                                // against it, else the pixel is redone exactly)
+                                drop = fminf(drop, keep_nearest<K>(cand, lane, k, tl));
                             }
                         }
-                    }
-                    if (near_ref != RT_INVALID_REF) {
-                        cur = near_ref;
-                        continue;
-                    }
-                } else {
-                    const uint32_t first = cur & RT_LEAF_FIRST_MASK;
-                    const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
-                    if (COUNT) w_leaves++;
-                    for (uint32_t k = first; k < first + cnt; k++) {
-                        const cfloat_p R = (cfloat_p)(sc.tri32 + 12 * (size_t)k);  // scalar loads
-                        const float4 A = load_f4(R), B = load_f4(R + 4), Cc = load_f4(R + 8);
-                        if (COUNT) n_pre += mine;
-                        const bool pre =
-                            mine && tri_prefilter(A, B, Cc, q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull);
-                        if (__ballot(pre) == 0) continue;
-                        if (!pre) continue;
-                        if (COUNT) n_tris++;
-                        const Ray64 ray = load_ray(ray_lds, lane);
-                        const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)k;
-                        double t;
-                        if (!mt64(T, ray, t)) continue;
-                        double hx, hy, hz;
-                        const double d = hit_dist(ray, t, hx, hy, hz);
-                        const uint2 rl = *reinterpret_cast<const uint2*>(T + 9);  // {rank, leaf}
-                        if (!(d < best.dist || (d == best.dist && rl.x < best.rank))) continue;
-                        if (pass == 1) {
-                            if (rl.y != chain_leaf) {
-                                if (COUNT) n_chain++;
-                                chain_leaf = rl.y;
-                                chain_res = chain_ok(sc, rl.y, ray, n_chain_nodes);
-                            }
-                            if (!chain_res) continue;
-                        }
-                        best.dist = d;
-                        best.t = t;
-                        best.rank = rl.x;
-                        best.tri = (int32_t)k;
-                        tcull = round_up_f((d + tslack) * (1.0 + 0x1p-20));
                     }
                 }
+                RT_TACC(2, t_l0);
             }
-            if (sp == 0) break;
-            sp--;
-            cur = uni(wstack[sp]);
         }
-        if (pass == 1) break;
-        // deferred re-verification of each lane's winner
-        bool redo = false;
-        if (mine && best.tri >= 0) {
-            const Ray64 ray = load_ray(ray_lds, lane);
-            double hx, hy, hz;
-            (void)hit_dist(ray, best.t, hx, hy, hz);
-            const uint32_t leaf =
-                reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + 9)->y;
-            if (COUNT) n_chain++;
-            redo = !chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz) &&
-                   !chain_ok(sc, leaf, ray, n_chain_nodes);
-        }
-        mine = redo;
+        RT_TSTAMP(t_p0);
+        if (sp == 0) break;
+        sp--;
+        cur = uni(wstack[sp]);
+#ifdef RT_DIAG_TIMING
+        asm volatile("" ::"s"(cur));
+#endif
+        RT_TACC(3, t_p0);
     }
+    RT_TSTAMP(t_r0);
+    A = launder(A);
+    const RtFrameParams fp = kload(&A->fp);
     if (COUNT && fp.counters && lane == 0) {
         atomicAdd(&fp.counters[7], (unsigned long long)w_nodes);
         atomicAdd(&fp.counters[8], (unsigned long long)w_leaves);
         atomicAdd(&fp.counters[9], 1ull);
     }
     if (!valid) return;
-    Best out;
-    out.dist = best.dist;
-    out.rank = best.rank;
-    out.tri = best.tri;
-    out.px = out.py = out.pz = 0.0;
-    if (best.tri >= 0) {
-        const Ray64 ray = load_ray(ray_lds, lane);
-        (void)hit_dist(ray, best.t, out.px, out.py, out.pz);
-    }
+    // hand the lane's surviving candidates to k_resolve: count per pixel,
+    // entry c of pixel o at cand[c * npix + o] (coalesced across a row)
+    const RtLaunchAux aux = kload(&A->aux);
     const size_t o = (size_t)r * fp.W + i;
-    shade_store(fp, sc, o, out);
+    const size_t npix = (size_t)fp.W * fp.nrows;
+    uint32_t m = 0;
+    for (int c = 0; c < nc; c++) {
+        const uint2 e = cand[c * 64 + lane];
+        if (__uint_as_float(e.y) > tcull) continue;  // cannot beat a certain hit
+        reinterpret_cast<RT_G uint2*>(aux.cand)[(size_t)m * npix + o] = e;
+        m++;
+    }
+    const bool dropped = drop < __builtin_huge_valf() && drop <= tcull;  // a dropped candidate could still win
+    if (dropped) aux.cand_drop[o] = drop;
+    aux.cand_cnt[o] = (uint8_t)(m | (dropped ? kCandDropped : 0u));
+    RT_TACC(5, t_r0);
+    if (COUNT && fp.counters) {
+        atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
+        atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
+    }
+}
+
+// Exact resolve of the packet kernel's candidate lists, one pixel per lane
+// (full occupancy: the dependent fp64 loads of many pixels overlap).  For
+// each candidate the reference's fp64 Moller-Trumbore and hit distance
+// (triangle.hpp:40-88, stack_bvh.hpp:630-631); the winner is the minimum
+// (distance, reference visit rank) — the reference keeps the first strictly
+// closer hit in its LIFO order (stack_bvh.hpp:633).  The winner's ancestor
+// chain is re-verified (the reference must see the triangle); a failure or
+// a candidate-list overflow sends the pixel to k_fixup.
+template <bool COUNT>
+__global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
+    __shared__ uint32_t wave_hits[4];
+    const size_t npix = (size_t)fp.W * fp.nrows;
+    const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const bool active = o < npix;
+    const int i = (int)(o % (size_t)fp.W), r = (int)(o / (size_t)fp.W);
+    const uint32_t cnt = active ? aux.cand_cnt[o] : 0u;
+    Best out;
+    out.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
+    out.rank = 0xFFFFFFFFu;
+    out.tri = -1;
+    out.px = out.py = out.pz = 0.0;
+    uint32_t redo = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
+    const uint32_t nlist = cnt & ~kCandDropped;
+    if (cnt != 0) {
+        const Ray64 ray = gen_ray(fp, i, fp.row0 + r * fp.row_stride);
+        double best_t = 0.0;
+        for (uint32_t c = 0; c < nlist; c++) {
+            const uint2 e = reinterpret_cast<const RT_G uint2*>(aux.cand)[(size_t)c * npix + o];
+            if (COUNT) n_tris++;
+            const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)e.x;
+            double t;
+            if (!mt64(T, ray, t)) continue;
+            double hx, hy, hz;
+            const double d = hit_dist(ray, t, hx, hy, hz);
+            const uint32_t rank = reinterpret_cast<const RT_G uint2*>(T + 9)->x;
+            if (d < out.dist || (d == out.dist && rank < out.rank)) {
+                out.dist = d;
+                out.rank = rank;
+                out.tri = (int32_t)e.x;
+                best_t = t;
+            }
+        }
+        if (cnt & kCandDropped) {
+            // every dropped candidate has t >= drop, so its distance is at
+            // least drop (1 - 2^-20) - slack: the winner must be strictly
+            // nearer than that, else only the exact per-lane path can decide
+            const double omax = __builtin_fmax(__builtin_fmax(__builtin_fabs(ray.ox), __builtin_fabs(ray.oy)),
+                                               __builtin_fabs(ray.oz));
+            const double bound = (double)aux.cand_drop[o] * (1.0 - 0x1p-20) - 0x1p-40 * (omax + 1.0);
+            if (!(out.tri >= 0 && out.dist < bound)) redo = 1;
+        }
+        if (!redo && out.tri >= 0) {
+            (void)hit_dist(ray, best_t, out.px, out.py, out.pz);
+            // the reference must see the winner: re-verify its ancestor chain
+            const uint32_t leaf =
+                reinterpret_cast<const RT_G uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)out.tri + 9)->y;
+            if (COUNT) n_chain++;
+            if (!chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, out.px, out.py, out.pz) &&
+                !chain_ok(sc, leaf, ray, n_chain_nodes))
+                redo = 2;
+        }
+    }
+    if (active) {
+        if (redo) {
+            const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
+            aux.redo[slot] = (uint32_t)o | (redo == 2u ? kRedoPass1 : 0u);
+        } else {
+            shade_store(fp, sc, o, out, false);
+        }
+    }
+    // hit count: block sums spread over RT_HIT_SLOTS counters (k_fixup adds
+    // them up) instead of same-address device atomics, which serialise
+    const uint64_t hits = __ballot(active && !redo && out.tri >= 0);
+    if ((threadIdx.x & 63) == 0) wave_hits[threadIdx.x >> 6] = (uint32_t)__builtin_popcountll(hits);
+    __syncthreads();
+    if (threadIdx.x == 0 && fp.hit_count) {
+        const uint32_t sum = wave_hits[0] + wave_hits[1] + wave_hits[2] + wave_hits[3];
+        if (sum) atomicAdd(aux.tile_ctr + RT_HIT_BASE + (blockIdx.x % RT_HIT_SLOTS) * RT_QUEUE_STRIDE, sum);
+    }
+    if (!active) return;
     if (COUNT && fp.counters) {
         atomicAdd(&fp.counters[0], 1ull);
-        atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
         atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
         atomicAdd(&fp.counters[3], (unsigned long long)n_chain);
-        if (best.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
+        if (!redo && out.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
         atomicAdd(&fp.counters[5], (unsigned long long)n_chain_nodes);
-        atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
+        if (redo == 1) atomicAdd(&fp.counters[10], 1ull);
+        if (redo == 2) atomicAdd(&fp.counters[11], 1ull);
     }
 }
 
 // Persistent waves over 8x8 tiles; the stack bound of the tree must fit SP
 // (the host falls back to the per-lane kernel otherwise), so no push can drop.
-template <int W, int SP, bool COUNT>
-__global__ void __launch_bounds__(256) k_trace_packet(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
+template <int W, int SP, int K, bool COUNT>
+__global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs args) {
     __shared__ uint32_t stacks[4][SP];
-    __shared__ double rays[4][9 * 64];
+    __shared__ uint2 cands[4][K * 64];
+    __shared__ PacketArgs s_args;
+    {
+        const __attribute__((address_space(4))) uint32_t* src =
+            (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&s_args);
+        for (unsigned w = threadIdx.x; w < sizeof(PacketArgs) / 4; w += blockDim.x) dst[w] = src[w];
+        __syncthreads();
+    }
+    args_p A = (args_p)&s_args;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int tiles_x = (fp.W + 7) >> 3;
-    const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
+    uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)tacc;
+    // tile scheduling: one queue per XCD (blocks are dealt to the 8 XCDs
+    // round-robin, so block b's XCD is b % 8): queue x hands out tiles
+    // x, x + 8, x + 16, ...; every queue is drained by the blocks b = x mod 8.
+    const uint32_t xq = blockIdx.x % RT_QUEUES;
+#if RT_TILE_SCHED == 2
+    uint32_t iter = 0;  // diagnostic: static round-robin, no atomics
+#endif
     for (;;) {
+        A = launder(A);
+        const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
+        RT_G uint32_t* const qblk = kload(&A->aux.tile_ctr);
+        const int tiles_x = (W_ + 7) >> 3;
+        const int tiles = tiles_x * ((nrows + 7) >> 3);
         int tile = 0;
-        if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);
+        RT_TSTAMP(t_q0);
+#if RT_TILE_SCHED == 0
+        if (lane == 0) tile = (int)atomicAdd(qblk, 1u);
         tile = __shfl(tile, 0);
+#elif RT_TILE_SCHED == 1
+        if (lane == 0) tile = (int)(xq + RT_QUEUES * atomicAdd(qblk + xq * RT_QUEUE_STRIDE, 1u));
+        tile = __shfl(tile, 0);
+#else
+        tile = (int)((blockIdx.x * 4 + wv) + iter++ * gridDim.x * 4);
+#endif
+#ifdef RT_DIAG_TIMING
+        asm volatile("" ::"v"(tile));
+#endif
+        RT_TACC(7, t_q0);
         if (tile >= tiles) break;
         const int i = (tile % tiles_x) * 8 + (lane & 7);
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
-        trace_packet<W, SP, COUNT>(sc, fp, i, r, i < fp.W && r < fp.nrows, stacks[wv], rays[wv]);
+        trace_packet<W, SP, K, COUNT>(A, i, r, i < W_ && r < nrows, stacks[wv], cands[wv], tacc);
     }
+#ifdef RT_DIAG_TIMING
+    RT_G unsigned long long* const diag = kload(&A->aux.diag);
+    if (diag && lane == 0)
+        for (int q = 0; q < 8; q++) atomicAdd(diag + q, (unsigned long long)tacc[q]);
+#endif
 }

@@ -34,6 +34,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <utility>
+
 #include "kernels_common.h"
 #include "rt_device.h"
 
@@ -101,7 +103,7 @@ struct Win {
 // --------------------------------------------------------------------------
 template <int W, int S, bool COUNT>
 __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int i, int r,
-                                            LaneStack<S>& st) {
+                                            LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
     constexpr int G = W < 4 ? W : 4;  // children tested per load group
     const int j = fp.row0 + r * fp.row_stride;
     Ray32 q;
@@ -123,7 +125,7 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
     //         winner (one check per ray, usually the margin test alone);
     // pass 1: only if that winner is invisible to the reference — traverse
     //         again verifying every would-be winner inline.
-    for (int pass = 0; pass < 2; pass++) {
+    for (int pass = pass0; pass < 2; pass++) {
         best.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
         best.t = 0.0;
         best.rank = 0xFFFFFFFFu;
@@ -256,7 +258,7 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
     const size_t o = (size_t)r * fp.W + i;
     shade_store(fp, sc, o, out);
     if (COUNT && fp.counters) {
-        atomicAdd(&fp.counters[0], 1ull);
+        if (!fixup) atomicAdd(&fp.counters[0], 1ull);  // a fixed-up ray was counted by the packet kernel
         atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
         atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
         atomicAdd(&fp.counters[3], (unsigned long long)n_chain);
@@ -267,6 +269,41 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
 }
 
 #include "packet_kernel.h"
+
+// Finishes the pixels the packet kernel handed over (redo list, count in
+// tile_ctr[RT_REDO_COUNT]) with the per-lane exact kernel: from pass 0 after a candidate
+// list overflow, straight into the inline-verifying pass 1 when the winner's
+// ancestor chain failed.  Grid-stride; every thread reaches the exit test.
+template <int W, int S, bool COUNT>
+__global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
+    __shared__ uint2 lds[S][256];
+    __shared__ unsigned long long block_sum;
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && fp.hit_count && aux.cand) {
+        // fold k_resolve's hit-count partials into the caller's counter
+        if (tid == 0) block_sum = 0;
+        __syncthreads();
+        if (tid < RT_HIT_SLOTS) {
+            const uint32_t v = aux.tile_ctr[RT_HIT_BASE + tid * RT_QUEUE_STRIDE];
+            if (v) atomicAdd(&block_sum, (unsigned long long)v);
+        }
+        __syncthreads();
+        if (tid == 0 && block_sum) atomicAdd(fp.hit_count, block_sum);
+    }
+    const uint32_t n = *(volatile uint32_t*)(aux.tile_ctr + RT_REDO_COUNT);
+    if (n == 0) return;
+    LaneStack<S> st;
+    st.lds = lds;
+    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
+    st.tid = tid;
+    st.top = 0;
+    for (uint32_t e = blockIdx.x * 256u + (uint32_t)tid; e < n; e += gridDim.x * 256u) {
+        const uint32_t v = aux.redo[e];
+        const uint32_t o = v & ~kRedoPass1;
+        const int i = (int)(o % (uint32_t)fp.W), r = (int)(o / (uint32_t)fp.W);
+        trace_exact<W, S, COUNT>(sc, fp, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
+    }
+}
 
 // Persistent waves: each wave pulls 8x8 pixel tiles from `tile_ctr` until the
 // shard is exhausted (every wave reaches the exit test each iteration).
@@ -358,7 +395,9 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
 }
 
 constexpr int kLdsStack = 16;      // per-lane kernel: LDS ring entries per lane (8 B each)
-constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (16 B each)
+constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (4 B each)
+constexpr int kCandidates = 8;     // packet kernel: candidate list entries per lane (8 B each)
+constexpr int kFixupGrid = 256;    // k_fixup blocks (the redo list is short)
 
 // Kernel choice: the packet kernel unless its stack cannot hold the tree's
 // bound or RT_KERNEL=lane asks for the per-lane kernel.
@@ -375,8 +414,19 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
                         hipStream_t s) {
     const dim3 grid((unsigned)aux.grid);
     if (use_packet(sc.stack_bound)) {
-        if (count) hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, true>), grid, dim3(256), 0, s, sc, fp, aux);
-        else hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, false>), grid, dim3(256), 0, s, sc, fp, aux);
+        const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
+        const dim3 rgrid((unsigned)(((uint64_t)fp.W * fp.nrows + 255) / 256));
+        if (count) {
+            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true>), grid, dim3(256), 0, s,
+                               PacketArgs{sc, fp, aux});
+            hipLaunchKernelGGL((k_resolve<true>), rgrid, dim3(256), 0, s, sc, fp, aux);
+            hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, dim3(256), 0, s, sc, fp, aux);
+        } else {
+            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false>), grid, dim3(256), 0, s,
+                               PacketArgs{sc, fp, aux});
+            hipLaunchKernelGGL((k_resolve<false>), rgrid, dim3(256), 0, s, sc, fp, aux);
+            hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, dim3(256), 0, s, sc, fp, aux);
+        }
     } else {
         if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true, 3>), grid, dim3(256), 0, s, sc, fp, aux);
         else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false, 3>), grid, dim3(256), 0, s, sc, fp, aux);
@@ -388,7 +438,8 @@ template <int W>
 int blocks_per_cu_w(uint32_t stack_bound) {
     int n = 0;
     hipError_t e = use_packet(stack_bound)
-                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_packet<W, kPacketStack, false>, 256, 0)
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_packet<W, kPacketStack, kCandidates, false>,
+                                                                   256, 0)
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<W, kLdsStack, false, 3>, 256, 0);
     return e == hipSuccess ? n : 1;
 }
@@ -415,6 +466,7 @@ int exact_blocks_per_cu(int width, uint32_t stack_bound) {
 }
 
 int exact_lds_stack() { return kLdsStack; }
+int packet_candidates() { return kCandidates; }
 
 // Host entry: validates the launch geometry against what the kernels assume
 // and dispatches on node width.  mode 0 = exact fast, 1 = literal.
@@ -431,7 +483,12 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     }
     if (aux.spill_cap + kLdsStack < sc.stack_bound || !aux.tile_ctr || !aux.spill || aux.grid <= 0)
         return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, sizeof(uint32_t), s);
+    // the redo list must hold every pixel of the shard
+    if (use_packet(sc.stack_bound) &&
+        (!aux.redo || aux.redo_cap < (uint64_t)fp.W * (uint64_t)fp.nrows || !aux.cand || !aux.cand_cnt || !aux.cand_drop ||
+         aux.cand_cap < (uint64_t)fp.W * (uint64_t)fp.nrows))
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);  // queues, redo count
     if (e != hipSuccess) return e;
     switch (sc.width) {
         case 2: return launch_exact<2>(sc, fp, aux, count, s);

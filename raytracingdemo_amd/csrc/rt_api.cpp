@@ -19,6 +19,7 @@ namespace rt {
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
                         hipStream_t s, uint32_t literal_stack);
 int exact_blocks_per_cu(int width, uint32_t stack_bound);
+int packet_candidates();
 int exact_lds_stack();
 }
 
@@ -62,7 +63,7 @@ struct Replica {
     RtDevScene dev{};
     double* d_cam = nullptr;    // px[W] ++ py[H]
     int cam_w = 0, cam_h = 0;
-    unsigned long long* d_counters = nullptr;  // 5 counters
+    unsigned long long* d_counters = nullptr;  // [0..15] RT_FLAG_COUNT counters, [16..23] diagnostics
     // staging for the host-output frame call
     void* frame = nullptr;
     size_t frame_bytes = 0;
@@ -74,6 +75,10 @@ struct Replica {
     uint64_t* d_spill = nullptr;
     uint32_t spill_cap = 0;
     int grid = 0;
+    uint32_t* d_redo = nullptr;  // packet kernel -> fix-up kernel pixel list
+    uint64_t redo_cap = 0;
+    void* d_cand = nullptr;      // packet kernel -> resolve kernel candidate lists
+    uint64_t cand_cap = 0;       // pixels
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
 };
 
@@ -100,6 +105,8 @@ void free_replica(Replica& r) {
     if (r.frame) hipFree(r.frame);
     if (r.d_tiles) hipFree(r.d_tiles);
     if (r.d_spill) hipFree(r.d_spill);
+    if (r.d_redo) hipFree(r.d_redo);
+    if (r.d_cand) hipFree(r.d_cand);
     if (r.ev_in) hipEventDestroy(r.ev_in);
     if (r.ev_out) hipEventDestroy(r.ev_out);
     if (r.ev0) hipEventDestroy(r.ev0);
@@ -171,8 +178,8 @@ void upload_one(rt_scene* s, int device) {
     d.node_bytes = rt_node_bytes(f.width);
     d.width = f.width;
     d.stack_bound = f.stack_bound;
-    HIP_TRY(hipMalloc(&r.d_counters, 16 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(r.d_counters, 0, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&r.d_counters, 32 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(r.d_counters, 0, 32 * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
@@ -181,7 +188,7 @@ void upload_one(rt_scene* s, int device) {
     r.grid = prop.multiProcessorCount * rt::exact_blocks_per_cu(f.width, f.stack_bound);
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
-    HIP_TRY(hipMalloc(&r.d_tiles, 256));
+    HIP_TRY(hipMalloc(&r.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&r.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
     s->reps.push_back(r);
 }
@@ -201,9 +208,32 @@ void ensure_camera(Replica& r, int W, int H, hipStream_t stream) {
     r.cam_h = H;
 }
 
+// Redo list and candidate buffers large enough for every pixel of a launch
+// (grown, never shrunk).
+void ensure_redo(Replica& r, uint64_t pixels) {
+    if (r.cand_cap < pixels) {
+        HIP_TRY(hipStreamSynchronize(r.stream));  // earlier launches may still use it
+        if (r.d_cand) HIP_TRY(hipFree(r.d_cand));
+        r.d_cand = nullptr;
+        r.cand_cap = 0;
+        const uint64_t k = (uint64_t)rt::packet_candidates();
+        // [K][pixels] entries | [pixels] f32 drop bounds | [pixels] counts
+        HIP_TRY(hipMalloc(&r.d_cand, pixels * (8 * k + 4 + 1)));
+        r.cand_cap = pixels;
+    }
+    if (r.redo_cap >= pixels) return;
+    HIP_TRY(hipStreamSynchronize(r.stream));  // earlier launches may still use it
+    if (r.d_redo) HIP_TRY(hipFree(r.d_redo));
+    r.d_redo = nullptr;
+    r.redo_cap = 0;
+    HIP_TRY(hipMalloc(&r.d_redo, pixels * sizeof(uint32_t)));
+    r.redo_cap = pixels;
+}
+
 void check_camera(const rt_scene* s, const rt_camera* c) {
     if (!c) throw rt::Error{RT_ERR_INVALID_ARGUMENT, "camera is NULL"};
-    if (c->width <= 0 || c->height <= 0 || c->width > 65536 || c->height > 65536)
+    if (c->width <= 0 || c->height <= 0 || c->width > 65536 || c->height > 65536 ||
+        (int64_t)c->width * c->height >= (int64_t(1) << 31))
         throw rt::Error{RT_ERR_INVALID_ARGUMENT, "bad image size"};
     for (int a = 0; a < 3; a++)
         if (!std::isfinite(c->pos[a]) || !std::isfinite(c->dir[a]))
@@ -246,6 +276,17 @@ RtLaunchAux aux_of(Replica& r) {
     a.spill = r.d_spill;
     a.spill_cap = r.spill_cap;
     a.grid = r.grid;
+    a.redo = r.d_redo;
+    a.redo_cap = r.redo_cap;
+    a.diag = r.d_counters + 16;
+    a.cand = static_cast<uint64_t*>(r.d_cand);
+    if (r.d_cand) {
+        uint8_t* base = static_cast<uint8_t*>(r.d_cand);
+        const uint64_t k = (uint64_t)rt::packet_candidates();
+        a.cand_drop = reinterpret_cast<float*>(base + r.cand_cap * 8 * k);
+        a.cand_cnt = base + r.cand_cap * (8 * k + 4);
+    }
+    a.cand_cap = r.cand_cap;
     return a;
 }
 
@@ -370,6 +411,7 @@ int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mod
         fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
         // serialise on the replica's stream: the caller's stream waits for it
         std::lock_guard<std::mutex> lk(s->mu);
+        ensure_redo(*r, (uint64_t)cam->width * (uint64_t)nrows);
         HIP_TRY(hipEventRecord(r->ev_in, st));
         HIP_TRY(hipStreamWaitEvent(r->stream, r->ev_in, 0));
         HIP_TRY(rt::launch_trace(r->dev, fp, aux_of(*r), mode, (flags & RT_FLAG_COUNT) != 0, r->stream,
@@ -415,6 +457,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         fp.hit_pos = d.pos;
         fp.rgb = d.rgb;
         fp.hit_count = d.hit_count;
+        ensure_redo(r, npx);
         HIP_TRY(hipEventRecord(r.ev0, r.stream));
         HIP_TRY(rt::launch_trace(r.dev, fp, aux_of(r), mode, false, r.stream, literal_stack_bound(s)));
         HIP_TRY(hipEventRecord(r.ev1, r.stream));
@@ -441,7 +484,7 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         Replica& r = replica_for(s, device);
         DevGuard g(device);
         HIP_TRY(hipDeviceSynchronize());
-        unsigned long long c[16];
+        unsigned long long c[32];
         HIP_TRY(hipMemcpy(c, r.d_counters, sizeof c, hipMemcpyDeviceToHost));
         out->rays = c[0];
         out->node_fetches = c[1];
@@ -453,6 +496,9 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->wave_nodes = c[7];
         out->wave_leaves = c[8];
         out->wave_tiles = c[9];
+        out->redo_rays = c[10] + c[11];
+        out->redo_chain = c[11];
+        for (int q = 0; q < 8; q++) out->diag_cycles[q] = c[16 + q];
         if (reset) HIP_TRY(hipMemset(r.d_counters, 0, sizeof c));
         return RT_OK;
     } catch (const rt::Error& e) {

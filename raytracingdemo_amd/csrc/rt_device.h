@@ -24,6 +24,18 @@
 #define RT_LEAF_MAX_FIRST 0x07FFFFFFu
 #define RT_CHILD_REF 6       // u32 slot of the child ref in a 32-B child record
 #define RT_TRI64_DOUBLES 10  // v0, e1, e2 (9 doubles) + {u32 rank, u32 leaf}: 80 B
+// Work-queue block (RtLaunchAux::tile_ctr, RT_QUEUE_WORDS u32, zeroed per
+// launch): RT_QUEUES tile queues RT_QUEUE_STRIDE words apart (one per XCD,
+// separate cache lines), the redo-list length, and the hit-count partials.
+#define RT_QUEUES 8
+#define RT_QUEUE_STRIDE 16
+#define RT_REDO_COUNT (RT_QUEUES * RT_QUEUE_STRIDE)
+// then RT_HIT_SLOTS hit-count partial sums RT_QUEUE_STRIDE words apart
+#define RT_HIT_SLOTS 64
+#define RT_HIT_BASE 1024
+#define RT_QUEUE_WORDS (RT_HIT_BASE + RT_HIT_SLOTS * RT_QUEUE_STRIDE)
+// tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
+#define RT_TRI32_PAD 4
 
 #ifdef __cplusplus
 static inline constexpr uint32_t rt_node_bytes(int W) { return (uint32_t)(32 * W); }
@@ -32,19 +44,29 @@ static inline constexpr uint32_t rt_make_leaf(uint32_t first, uint32_t count) {
 }
 #endif
 
+// Device passes see every pointer member as a global-memory pointer, so
+// kernels that read these structs out of the kernarg block (not only as
+// kernel parameters) still emit global_* rather than flat_* accesses.  The
+// layout is the same on host and device.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_G __attribute__((address_space(1)))
+#else
+#define RT_G
+#endif
+
 struct RtDevScene {
-    const uint8_t* nodes;
-    const float* tri32;      // 12 floats per triangle: v0,e1,e2, max|e1|,max|e2|,max|v0|
-    const double* tri64;     // RT_TRI64_DOUBLES per triangle: v0,e1,e2,{rank,leaf}
-    const uint32_t* tri_id;
-    const uint32_t* tri_rank;
-    const uint32_t* tri_leaf;
-    const double* rbox;      // 6 per real node
-    const int32_t* rparent;
-    const double* normal;    // loader order, 3 per triangle
-    const uint32_t* rkid_off;// real tree CSR (literal reference-order mode)
-    const uint32_t* rkid;
-    const uint32_t* rrange;  // real node primitive range [begin, end)
+    const RT_G uint8_t* nodes;
+    const RT_G float* tri32;      // 12 floats per triangle: v0,e1,e2, max|e1|,max|e2|,max|v0|
+    const RT_G double* tri64;     // RT_TRI64_DOUBLES per triangle: v0,e1,e2,{rank,leaf}
+    const RT_G uint32_t* tri_id;
+    const RT_G uint32_t* tri_rank;
+    const RT_G uint32_t* tri_leaf;
+    const RT_G double* rbox;      // 6 per real node
+    const RT_G int32_t* rparent;
+    const RT_G double* normal;    // loader order, 3 per triangle
+    const RT_G uint32_t* rkid_off;// real tree CSR (literal reference-order mode)
+    const RT_G uint32_t* rkid;
+    const RT_G uint32_t* rrange;  // real node primitive range [begin, end)
     uint32_t root_ref;
     float root_box[6];
     uint32_t n_tris;
@@ -55,23 +77,30 @@ struct RtDevScene {
 
 // Per-launch resources of the persistent exact kernel.
 struct RtLaunchAux {
-    uint32_t* tile_ctr;   // work-queue head, zeroed before every launch
-    uint64_t* spill;      // traversal-stack spill: spill_cap entries per lane
+    RT_G uint32_t* tile_ctr;   // work-queue block (RT_QUEUE_WORDS words), zeroed before every launch
+    RT_G uint64_t* spill;      // traversal-stack spill: spill_cap entries per lane
     uint32_t spill_cap;
     int32_t grid;         // persistent blocks (CUs x resident blocks per CU)
+    RT_G uint32_t* redo;       // packet kernel -> k_fixup: pixel index | start-pass bit
+    uint64_t redo_cap;    // entries (>= pixels of the launch)
+    RT_G unsigned long long* diag;  // 8 cycle-split accumulators (RT_DIAG_TIMING builds)
+    RT_G uint64_t* cand;       // packet kernel -> k_resolve: {tri, t lower bound} per entry, [K][pixels]
+    RT_G uint8_t* cand_cnt;    // entries per pixel (0xFF: overflow)
+    uint64_t cand_cap;         // pixels the candidate buffers hold
+    RT_G float* cand_drop;     // per pixel: smallest t bound of a dropped candidate (if flagged)
 };
 
 struct RtFrameParams {
     double pos[3], dir[3], right[3], up[3];
-    const double* px;  // W pixel-plane x coefficients (camera.hpp:35)
-    const double* py;  // H pixel-plane y coefficients (camera.hpp:37)
+    const RT_G double* px;  // W pixel-plane x coefficients (camera.hpp:35)
+    const RT_G double* py;  // H pixel-plane y coefficients (camera.hpp:37)
     int32_t W, H;
     int32_t row0, row_stride, nrows;
-    uint32_t* hit_id;
-    double* dist;
-    double* hit_pos;
-    uint8_t* rgb;
-    unsigned long long* hit_count;
-    unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits, chain_nodes] or NULL
+    RT_G uint32_t* hit_id;
+    RT_G double* dist;
+    RT_G double* hit_pos;
+    RT_G uint8_t* rgb;
+    RT_G unsigned long long* hit_count;
+    RT_G unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits, chain_nodes] or NULL
     float pad;                     // world-space slab margin of the fp32 traversal
 };

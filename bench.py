@@ -31,11 +31,13 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec (primary, 1spp) on Sponza 1920×1080; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-TRI32_BYTES = 48       # fp32 pre-filter record (v0, e1, e2 + 3 bounds) per pre-test
+TRI32_BYTES = 48       # fp32 pre-filter record (v0, e1, e2 + 3 bounds)
 TRI64_BYTES = 80       # fp64 record (v0, e1, e2, rank, leaf) per exact Moller-Trumbore test
 CHAIN_BYTES = 52       # fp64 box (48 B) + parent (4 B) per re-verified ancestor
 OUT_BYTES = 7          # u32 hit-id + 3 B rgb written per ray
-CAM_BYTES = 16         # px[i] + py[j] per ray
+CAM_BYTES = 16         # px[i] + py[j] per ray (per-lane kernel)
+CAM_TILE_BYTES = 128   # 8 px + 8 py doubles per 8x8 tile (packet kernel)
+CAND_BYTES = 8         # one candidate entry {triangle, t bound} handed to the resolve kernel
 
 
 def parse():
@@ -53,6 +55,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="committed rocprofv3 PMC summary supplying roofline.traffic")
+    p.add_argument("--key-out", default="", help="write this run's workload key (for tools/pmc_traffic.py)")
     return p.parse_args()
 
 
@@ -118,14 +121,15 @@ def main():
     stream = torch.cuda.current_stream(dev)
     mode = a.mode
 
-    def render_step(events=None):
+    def render_step(events=None, ktiming=True):
         cnt.zero_()
         for f, (pos, d) in enumerate(cams):
             if events is not None:
                 events[f][0].record(stream)
             scene.render_rows_device(local, pos, d, W, H, rank, world, my_rows, hit_id=ids[f].data_ptr(),
                                      rgb=rgb[f].data_ptr(), hit_count=cnt[f:f + 1].data_ptr(),
-                                     stream=stream.cuda_stream, mode=mode)
+                                     stream=stream.cuda_stream, mode=mode,
+                                     timing=events is not None and ktiming)
             if events is not None:
                 events[f][1].record(stream)
         if world > 1:
@@ -138,9 +142,13 @@ def main():
 
     # exactness check of the headline workload (outside timing): frame 0 vs
     # a full-frame render through the single-GPU path on this rank
+    # warm-up with kernel timing on, so the library's per-launch timing events
+    # exist before the timed region (they are recycled, not re-created)
+    warm_events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
     for _ in range(a.warmup):
-        render_step()
+        render_step(warm_events)
     torch.cuda.synchronize(dev)
+    scene.frame_stats(local, reset=True)
 
     # counting pass for algorithmic bytes (outside the timed region)
     scene.frame_stats(local, reset=True)
@@ -150,9 +158,20 @@ def main():
                                  stream=stream.cuda_stream, mode=mode, count=True)
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
-    launches = F
-    alg_bytes_per_launch = (cs["node_fetches"] * st["node_bytes"] + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
-                            cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * (OUT_BYTES + CAM_BYTES)) / launches
+    nb = st["node_bytes"]
+    # SURVEY.md 8(d)'s per-ray figure: what each ray's own traversal touches
+    survey_bytes_per_ray = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
+                            cs["rays"] * OUT_BYTES) / max(cs["rays"], 1)
+    if cs["wave_tiles"]:
+        # packet traversal kernel (the dominant kernel): a node or triangle
+        # record is fetched once per wave for its 64 rays; plus the camera
+        # coefficients of each tile and the candidate lists it writes
+        trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES + cs["wave_tiles"] * CAM_TILE_BYTES +
+                       cs["rays"] * 1 + cs["tri_tests"] * CAND_BYTES)
+    else:  # per-lane kernel: each ray fetches its own records
+        trace_bytes = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
+                       cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * (OUT_BYTES + CAM_BYTES))
+    alg_bytes_per_launch = trace_bytes / F
 
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
     kernel_ms = []
@@ -161,15 +180,17 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        render_step(events)
+        render_step(events, ktiming=not os.environ.get("RT_BENCH_NO_KTIMING"))
         torch.cuda.synchronize(dev)  # needed to read this step's events; also part of the step
         kernel_ms.extend(e0.elapsed_time(e1) for e0, e1 in events)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # diagnostic builds: per-wave clock split of the timed launches
-    diag = scene.frame_stats(local, reset=True)["diag_cycles"]
+    # per-kernel HIP-event times of the timed launches (library stream), and
+    # in diagnostic builds the per-wave clock split
+    ks = scene.frame_stats(local, reset=True)
+    diag = ks["diag_cycles"]
     tiles_timed = a.steps * F * ((W + 7) // 8) * ((my_rows + 7) // 8)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -178,16 +199,22 @@ def main():
 
     total_rays = a.steps * F * W * H
     value = total_rays / elapsed / 1e6
-    avg_kernel_s = float(np.mean(kernel_ms)) * 1e-3
+    launches_timed = max(ks["timed_launches"], 1)
+    # dominant (traversal) kernel; without library timing, the whole frame
+    avg_kernel_s = (ks["trace_ms"] / launches_timed if ks["timed_launches"] else float(np.mean(kernel_ms))) * 1e-3
     achieved = alg_bytes_per_launch / avg_kernel_s / 1e9
 
     if rank == 0:
+        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}"
+        if a.key_out:
+            with open(a.key_out, "w") as fh:
+                fh.write(key + "\n")
         traffic = None
         try:
             pm = json.load(open(a.pmc))
-            if pm.get("workload_key") == f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}":
-                traffic = pm.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
+            if pm.get("workload_key") == key:
+                traffic = round(float(pm["hbm_bytes_per_launch"]))
+        except (OSError, ValueError, KeyError):
             pass
         cpu = None
         if world == 1 and not a.no_cpu:
@@ -204,8 +231,11 @@ def main():
                        "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_trace_packet" if cs["wave_tiles"] else "k_trace_exact",
                          "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(alg_bytes_per_launch),
+                         "frame_ms_avg": round(float(np.mean(kernel_ms)), 4),
+                         "survey_bytes_per_ray": round(survey_bytes_per_ray, 1),
                          "per_ray": {"node_fetches": round(cs["node_fetches"] / max(cs["rays"], 1), 3),
                                      "tri_prefilter": round(cs["tri_prefilter"] / max(cs["rays"], 1), 3),
                                      "tri_tests_fp64": round(cs["tri_tests"] / max(cs["rays"], 1), 3),
@@ -213,6 +243,7 @@ def main():
                                      "chain_nodes": round(cs["chain_nodes"] / max(cs["rays"], 1), 4),
                                      "wave_nodes_per_tile": round(cs["wave_nodes"] / max(cs["wave_tiles"], 1), 2),
                                      "wave_leaves_per_tile": round(cs["wave_leaves"] / max(cs["wave_tiles"], 1), 2),
+                                     "wave_tris_per_tile": round(cs["wave_tris"] / max(cs["wave_tiles"], 1), 2),
                                      "redo_rays": round(cs["redo_rays"] / max(cs["rays"], 1), 7),
                                      "redo_chain": round(cs["redo_chain"] / max(cs["rays"], 1), 7),
                                      **({"diag_ticks_per_tile": [round(x / tiles_timed) for x in diag]}

@@ -51,7 +51,9 @@ extern "C" {
 #define RT_MODE_FP64 1  /* fp64 traversal throughout (simple, slower)          */
 
 /* render flags */
-#define RT_FLAG_COUNT 1u /* also count node/triangle fetches (rt_frame_stats) */
+#define RT_FLAG_COUNT 1u  /* also count node/triangle fetches (rt_frame_stats) */
+#define RT_FLAG_TIMING 2u /* time the pipeline kernels with HIP events on the
+                             launching stream (rt_frame_stats)              */
 
 #define RT_MISS 0xFFFFFFFFu
 
@@ -111,11 +113,15 @@ typedef struct {
     uint64_t wave_nodes;    /* packet kernel: inner-node visits per wave */
     uint64_t wave_leaves;   /* packet kernel: leaf visits per wave       */
     uint64_t wave_tiles;    /* packet kernel: 8x8 tiles traced           */
+    uint64_t wave_tris;     /* packet kernel: triangle records fetched per wave */
     uint64_t redo_rays;     /* rays finished by the fix-up kernel (exact per-lane path) */
     uint64_t redo_chain;    /*   of which: winner invisible to the reference (chain check) */
     uint64_t diag_cycles[8]; /* diagnostic builds only (else 0): wave clock ticks in
                                 node-load wait, node work, leaves, stack pops, ray
                                 set-up, exact resolve, output, tile fetch */
+    uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
+    double trace_ms;         /*   summed traversal-kernel time (HIP events
+                                  recorded around it on the launch stream) */
 } rt_frame_stats_t;
 
 /* objl::Loader + ObjectLoader::loadFromFile (object_loader.hpp:14-70,

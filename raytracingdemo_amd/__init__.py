@@ -180,14 +180,18 @@ class Scene:
 
     def render_rows_device(self, device: int, pos, d, W: int, H: int, row0: int, row_stride: int, nrows: int,
                            hit_id=0, dist=0, hit_pos=0, rgb=0, hit_count=0, stream=0, mode: str = "exact",
-                           count: bool = False):
-        """Asynchronous shard render into device pointers (ints) on `stream`."""
+                           count: bool = False, timing: bool = False):
+        """Asynchronous shard render into device pointers (ints) on `stream`.
+
+        count: accumulate fetch counters; timing: time the pipeline kernels with
+        HIP events on the library's launch stream (both read by frame_stats)."""
         o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
         cam = _camera(pos, d, W, H)
         m = N.RT_MODE_FP64 if mode in ("fp64", "literal") else N.RT_MODE_EXACT
         N.check(N.lib().rt_render_rows_device(self._h, int(device), C.byref(cam), m, int(row0), int(row_stride),
                                               int(nrows), C.byref(o), C.c_void_p(stream or None),
-                                              N.RT_FLAG_COUNT if count else 0))
+                                              (N.RT_FLAG_COUNT if count else 0) |
+                                              (N.RT_FLAG_TIMING if timing else 0)))
 
     def frame_stats(self, device: int = 0, reset: bool = True) -> dict:
         s = N.rt_frame_stats_t()

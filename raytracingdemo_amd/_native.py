@@ -26,6 +26,7 @@ STATUS_NAMES = {1: "invalid_argument", 2: "out_of_range", 3: "runtime_error", 4:
 RT_MODE_EXACT = 0
 RT_MODE_FP64 = 1
 RT_FLAG_COUNT = 1
+RT_FLAG_TIMING = 2
 RT_MISS = 0xFFFFFFFF
 
 # Every symbol include/rt.h declares (checked by tests/test_abi.py).
@@ -70,8 +71,8 @@ class rt_frame_stats_t(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("node_fetches", C.c_uint64), ("tri_tests", C.c_uint64),
                 ("chain_checks", C.c_uint64), ("hits", C.c_uint64), ("chain_nodes", C.c_uint64),
                 ("tri_prefilter", C.c_uint64), ("wave_nodes", C.c_uint64), ("wave_leaves", C.c_uint64),
-                ("wave_tiles", C.c_uint64), ("redo_rays", C.c_uint64), ("redo_chain", C.c_uint64),
-                ("diag_cycles", C.c_uint64 * 8)]
+                ("wave_tiles", C.c_uint64), ("wave_tris", C.c_uint64), ("redo_rays", C.c_uint64), ("redo_chain", C.c_uint64),
+                ("diag_cycles", C.c_uint64 * 8), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
 
 
 _lib = None

@@ -213,7 +213,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
     const float oly = (q.oy + pd) * q.iy, ohy = (q.oy - pd) * q.iy;
     const float olz = (q.oz + pd) * q.iz, ohz = (q.oz - pd) * q.iz;
 
-    uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0;  // COUNT only
+    uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0, w_tris = 0;  // COUNT only
     float tcull = valid ? __builtin_huge_valf() : -1.f;
     int nc = 0;         // candidates in the lane's list
     float drop = __builtin_huge_valf();  // smallest t lower bound of a dropped candidate
@@ -320,7 +320,10 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
                 RT_TSTAMP(t_l0);
                 const uint32_t first = cur & RT_LEAF_FIRST_MASK;
                 const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
-                if (COUNT) w_leaves++;
+                if (COUNT) {
+                    w_leaves++;
+                    w_tris += cnt;
+                }
                 // triangles come in chunks of kLeafChunk records: all their
                 // scalar loads are issued, then waited on once (tri32 carries
                 // kLeafChunk padding records, so reading past a leaf is safe)
@@ -381,6 +384,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
         atomicAdd(&fp.counters[7], (unsigned long long)w_nodes);
         atomicAdd(&fp.counters[8], (unsigned long long)w_leaves);
         atomicAdd(&fp.counters[9], 1ull);
+        atomicAdd(&fp.counters[12], (unsigned long long)w_tris);
     }
     if (!valid) return;
     // hand the lane's surviving candidates to k_resolve: count per pixel,
@@ -416,6 +420,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
 template <bool COUNT>
 __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
     __shared__ uint32_t wave_hits[4];
+    // the traversal kernel is done with the tile queues: clear them for the
+    // next launch (the packet pipeline needs no memset)
+    if (blockIdx.x == 0 && threadIdx.x < RT_QUEUES) aux.tile_ctr[threadIdx.x * RT_QUEUE_STRIDE] = 0;
     const size_t npix = (size_t)fp.W * fp.nrows;
     const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
     const bool active = o < npix;
@@ -513,6 +520,13 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
     args_p A = (args_p)&s_args;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
+    if (blockIdx.x == 0) {
+        // self-reset for this launch's k_resolve / k_fixup (the previous
+        // launch's fix-up has completed: stream order)
+        RT_G uint32_t* const q = kload(&A->aux.tile_ctr);
+        if (threadIdx.x == 0) q[RT_REDO_COUNT] = 0;
+        if (threadIdx.x < RT_HIT_SLOTS) q[RT_HIT_BASE + threadIdx.x * RT_QUEUE_STRIDE] = 0;
+    }
     uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     (void)tacc;
     // tile scheduling: one queue per XCD (blocks are dealt to the 8 XCDs

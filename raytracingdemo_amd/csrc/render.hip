@@ -411,25 +411,31 @@ bool use_packet(uint32_t stack_bound) {
 
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
-                        hipStream_t s) {
-    const dim3 grid((unsigned)aux.grid);
+                        hipStream_t s, const hipEvent_t* ev) {
+    const dim3 grid((unsigned)aux.grid), blk(256);
+    // RT_FLAG_TIMING: two markers bracket the traversal kernel only (the
+    // rest of the pipeline is timed as frame minus traversal by the caller)
+    if (ev) (void)hipEventRecord(ev[0], s);
     if (use_packet(sc.stack_bound)) {
         const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
         const dim3 rgrid((unsigned)(((uint64_t)fp.W * fp.nrows + 255) / 256));
         if (count) {
-            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true>), grid, dim3(256), 0, s,
+            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true>), grid, blk, 0, s,
                                PacketArgs{sc, fp, aux});
-            hipLaunchKernelGGL((k_resolve<true>), rgrid, dim3(256), 0, s, sc, fp, aux);
-            hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, dim3(256), 0, s, sc, fp, aux);
+            if (ev) (void)hipEventRecord(ev[1], s);
+            hipLaunchKernelGGL((k_resolve<true>), rgrid, blk, 0, s, sc, fp, aux);
+            hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, blk, 0, s, sc, fp, aux);
         } else {
-            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false>), grid, dim3(256), 0, s,
+            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false>), grid, blk, 0, s,
                                PacketArgs{sc, fp, aux});
-            hipLaunchKernelGGL((k_resolve<false>), rgrid, dim3(256), 0, s, sc, fp, aux);
-            hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, dim3(256), 0, s, sc, fp, aux);
+            if (ev) (void)hipEventRecord(ev[1], s);
+            hipLaunchKernelGGL((k_resolve<false>), rgrid, blk, 0, s, sc, fp, aux);
+            hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, blk, 0, s, sc, fp, aux);
         }
     } else {
-        if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true, 3>), grid, dim3(256), 0, s, sc, fp, aux);
-        else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false, 3>), grid, dim3(256), 0, s, sc, fp, aux);
+        if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true, 3>), grid, blk, 0, s, sc, fp, aux);
+        else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false, 3>), grid, blk, 0, s, sc, fp, aux);
+        if (ev) (void)hipEventRecord(ev[1], s);
     }
     return hipGetLastError();
 }
@@ -470,16 +476,25 @@ int packet_candidates() { return kCandidates; }
 
 // Host entry: validates the launch geometry against what the kernels assume
 // and dispatches on node width.  mode 0 = exact fast, 1 = literal.
+// ev (optional, 2 events): recorded around the traversal kernel on `s`
+// (RT_FLAG_TIMING).
+// fresh: the work-queue block is known to be zero (no memset needed);
+// *fresh_after: whether it will be zero again once this launch completes
+// (the packet pipeline clears it itself; the per-lane kernel does not).
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
-                        hipStream_t s, uint32_t literal_stack) {
+                        hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after) {
+    *fresh_after = fresh;
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
     if (mode == 1) {
         const long tiles = (long)((fp.W + 7) / 8) * (long)((fp.nrows + 7) / 8);
         const dim3 grid((unsigned)((tiles + 3) / 4));
-        if (literal_stack <= 64) return launch_literal_s<64>(sc, fp, count, grid, s);
-        if (literal_stack <= 256) return launch_literal_s<256>(sc, fp, count, grid, s);
-        if (literal_stack <= 1024) return launch_literal_s<1024>(sc, fp, count, grid, s);
-        return hipErrorInvalidValue;
+        if (literal_stack > 1024) return hipErrorInvalidValue;
+        if (ev) (void)hipEventRecord(ev[0], s);
+        hipError_t e = literal_stack <= 64    ? launch_literal_s<64>(sc, fp, count, grid, s)
+                       : literal_stack <= 256 ? launch_literal_s<256>(sc, fp, count, grid, s)
+                                              : launch_literal_s<1024>(sc, fp, count, grid, s);
+        if (ev) (void)hipEventRecord(ev[1], s);
+        return e;
     }
     if (aux.spill_cap + kLdsStack < sc.stack_bound || !aux.tile_ctr || !aux.spill || aux.grid <= 0)
         return hipErrorInvalidValue;
@@ -488,13 +503,17 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
         (!aux.redo || aux.redo_cap < (uint64_t)fp.W * (uint64_t)fp.nrows || !aux.cand || !aux.cand_cnt || !aux.cand_drop ||
          aux.cand_cap < (uint64_t)fp.W * (uint64_t)fp.nrows))
         return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);  // queues, redo count
-    if (e != hipSuccess) return e;
+    const bool packet = use_packet(sc.stack_bound);
+    if (!fresh || !packet) {
+        hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);  // queues, counts
+        if (e != hipSuccess) return e;
+    }
+    *fresh_after = packet;
     switch (sc.width) {
-        case 2: return launch_exact<2>(sc, fp, aux, count, s);
-        case 4: return launch_exact<4>(sc, fp, aux, count, s);
-        case 8: return launch_exact<8>(sc, fp, aux, count, s);
-        case 16: return launch_exact<16>(sc, fp, aux, count, s);
+        case 2: return launch_exact<2>(sc, fp, aux, count, s, ev);
+        case 4: return launch_exact<4>(sc, fp, aux, count, s, ev);
+        case 8: return launch_exact<8>(sc, fp, aux, count, s, ev);
+        case 16: return launch_exact<16>(sc, fp, aux, count, s, ev);
         default: return hipErrorInvalidValue;
     }
 }

@@ -11,13 +11,14 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "rt_internal.h"
 
 namespace rt {
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
-                        hipStream_t s, uint32_t literal_stack);
+                        hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after);
 int exact_blocks_per_cu(int width, uint32_t stack_bound);
 int packet_candidates();
 int exact_lds_stack();
@@ -79,7 +80,17 @@ struct Replica {
     uint64_t redo_cap = 0;
     void* d_cand = nullptr;      // packet kernel -> resolve kernel candidate lists
     uint64_t cand_cap = 0;       // pixels
+    // RT_FLAG_TIMING: events around the traversal kernel per timed launch,
+    // read and recycled by rt_frame_stats
+    std::vector<std::array<hipEvent_t, 2>> tev;
+    size_t tev_used = 0;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    // Launches on a replica are ordered on the caller's stream; only when the
+    // stream changes does the new stream wait for the previous one (no
+    // per-frame cross-stream round trip).
+    hipStream_t last = nullptr;
+    bool used = false;
+    bool fresh = true;  // work-queue block known to be zero (packet pipeline self-resets it)
 };
 
 }  // namespace
@@ -107,6 +118,8 @@ void free_replica(Replica& r) {
     if (r.d_spill) hipFree(r.d_spill);
     if (r.d_redo) hipFree(r.d_redo);
     if (r.d_cand) hipFree(r.d_cand);
+    for (auto& a : r.tev)
+        for (hipEvent_t e : a) hipEventDestroy(e);
     if (r.ev_in) hipEventDestroy(r.ev_in);
     if (r.ev_out) hipEventDestroy(r.ev_out);
     if (r.ev0) hipEventDestroy(r.ev0);
@@ -189,6 +202,7 @@ void upload_one(rt_scene* s, int device) {
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
     HIP_TRY(hipMalloc(&r.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(r.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&r.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
     s->reps.push_back(r);
 }
@@ -212,7 +226,7 @@ void ensure_camera(Replica& r, int W, int H, hipStream_t stream) {
 // (grown, never shrunk).
 void ensure_redo(Replica& r, uint64_t pixels) {
     if (r.cand_cap < pixels) {
-        HIP_TRY(hipStreamSynchronize(r.stream));  // earlier launches may still use it
+        HIP_TRY(hipDeviceSynchronize());  // earlier launches may still use it
         if (r.d_cand) HIP_TRY(hipFree(r.d_cand));
         r.d_cand = nullptr;
         r.cand_cap = 0;
@@ -222,7 +236,7 @@ void ensure_redo(Replica& r, uint64_t pixels) {
         r.cand_cap = pixels;
     }
     if (r.redo_cap >= pixels) return;
-    HIP_TRY(hipStreamSynchronize(r.stream));  // earlier launches may still use it
+    HIP_TRY(hipDeviceSynchronize());  // earlier launches may still use it
     if (r.d_redo) HIP_TRY(hipFree(r.d_redo));
     r.d_redo = nullptr;
     r.redo_cap = 0;
@@ -270,6 +284,20 @@ RtFrameParams frame_params(const rt_scene* s, Replica& r, const rt_camera* c, in
     return fp;
 }
 
+// Order this launch after every earlier launch on the replica.
+void order_on(Replica& r, hipStream_t st) {
+    if (r.used && r.last != st) {
+        HIP_TRY(hipEventRecord(r.ev_in, r.last));
+        HIP_TRY(hipStreamWaitEvent(st, r.ev_in, 0));
+    }
+    r.last = st;
+    r.used = true;
+}
+
+// Runs the pipeline and tracks whether its work-queue block is left zeroed.
+void launch(const rt_scene* s, Replica& r, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
+            const hipEvent_t* tev);
+
 RtLaunchAux aux_of(Replica& r) {
     RtLaunchAux a{};
     a.tile_ctr = r.d_tiles;
@@ -303,6 +331,15 @@ uint32_t literal_stack_bound(const rt_scene* s) {
         for (int32_t k : n.kids) st.push_back({k, it.sb + (uint32_t)n.kids.size() - 1});
     }
     return best + 1;
+}
+
+void launch(const rt_scene* s, Replica& r, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
+            const hipEvent_t* tev) {
+    bool fresh_after = false;
+    const hipError_t e =
+        rt::launch_trace(r.dev, fp, aux_of(r), mode, count, st, literal_stack_bound(s), tev, r.fresh, &fresh_after);
+    r.fresh = e == hipSuccess && fresh_after;
+    HIP_TRY(e);
 }
 
 }  // namespace
@@ -412,12 +449,17 @@ int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mod
         // serialise on the replica's stream: the caller's stream waits for it
         std::lock_guard<std::mutex> lk(s->mu);
         ensure_redo(*r, (uint64_t)cam->width * (uint64_t)nrows);
-        HIP_TRY(hipEventRecord(r->ev_in, st));
-        HIP_TRY(hipStreamWaitEvent(r->stream, r->ev_in, 0));
-        HIP_TRY(rt::launch_trace(r->dev, fp, aux_of(*r), mode, (flags & RT_FLAG_COUNT) != 0, r->stream,
-                                 literal_stack_bound(s)));
-        HIP_TRY(hipEventRecord(r->ev_out, r->stream));
-        HIP_TRY(hipStreamWaitEvent(st, r->ev_out, 0));
+        const hipEvent_t* tev = nullptr;
+        if (flags & RT_FLAG_TIMING) {
+            if (r->tev_used == r->tev.size()) {
+                std::array<hipEvent_t, 2> a{};
+                for (auto& e : a) HIP_TRY(hipEventCreate(&e));
+                r->tev.push_back(a);
+            }
+            tev = r->tev[r->tev_used++].data();
+        }
+        order_on(*r, st);
+        launch(s, *r, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, tev);
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
@@ -449,6 +491,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         d.pos = out->pos ? reinterpret_cast<double*>(base + o_pos) : nullptr;
         d.rgb = reinterpret_cast<uint8_t*>(base + o_rgb);  // always shaded (shadeScreen)
         d.hit_count = reinterpret_cast<unsigned long long*>(base + o_cnt);
+        order_on(r, r.stream);
         ensure_camera(r, cam->width, cam->height, r.stream);
         HIP_TRY(hipMemsetAsync(d.hit_count, 0, 8, r.stream));
         RtFrameParams fp = frame_params(s, r, cam, 0, 1, cam->height);
@@ -458,8 +501,9 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         fp.rgb = d.rgb;
         fp.hit_count = d.hit_count;
         ensure_redo(r, npx);
+        order_on(r, r.stream);
         HIP_TRY(hipEventRecord(r.ev0, r.stream));
-        HIP_TRY(rt::launch_trace(r.dev, fp, aux_of(r), mode, false, r.stream, literal_stack_bound(s)));
+        launch(s, r, fp, mode, false, r.stream, nullptr);
         HIP_TRY(hipEventRecord(r.ev1, r.stream));
         if (out->hit_id) HIP_TRY(hipMemcpyAsync(out->hit_id, d.hit_id, npx * 4, hipMemcpyDeviceToHost, r.stream));
         if (out->dist) HIP_TRY(hipMemcpyAsync(out->dist, d.dist, npx * 8, hipMemcpyDeviceToHost, r.stream));
@@ -496,9 +540,18 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->wave_nodes = c[7];
         out->wave_leaves = c[8];
         out->wave_tiles = c[9];
+        out->wave_tris = c[12];
         out->redo_rays = c[10] + c[11];
         out->redo_chain = c[11];
         for (int q = 0; q < 8; q++) out->diag_cycles[q] = c[16 + q];
+        out->timed_launches = r.tev_used;
+        out->trace_ms = 0.0;
+        for (size_t k = 0; k < r.tev_used; k++) {
+            float a = 0;
+            HIP_TRY(hipEventElapsedTime(&a, r.tev[k][0], r.tev[k][1]));
+            out->trace_ms += a;
+        }
+        if (reset) r.tev_used = 0;
         if (reset) HIP_TRY(hipMemset(r.d_counters, 0, sizeof c));
         return RT_OK;
     } catch (const rt::Error& e) {

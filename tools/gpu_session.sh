@@ -28,13 +28,16 @@ for s in $STEPS; do
         bench) run bench 600 python bench.py ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
                    -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
-        pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o fetch \
-                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \
+        pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
+                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu --key-out gpurun_out/pmc_key.txt && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
-                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu ;;
+                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \
+               python tools/pmc_traffic.py gpurun_out/pmc/fetch_counter_collection.csv \
+                   gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
         list)  run list 120 rocprofv3 -L ;;
         waves) for w in 3 4 5; do RT_WAVES=$w run bench_w$w 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
         quick) run bench_quick 300 python bench.py --no-cpu --steps 5 ;;
+        notime) RT_BENCH_NO_KTIMING=1 run bench_notime 300 python bench.py --no-cpu --steps 5 ;;
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}" 300 \
                           python bench.py --no-cpu --steps 5 || exit 1; done ;;

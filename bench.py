@@ -91,6 +91,7 @@ def main():
 
     import raytracingdemo_amd as rt
     from raytracingdemo_amd.scenes import sponza_scene
+    from raytracingdemo_amd.shards import deinterleave, rows_per_rank, shard_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -111,8 +112,8 @@ def main():
     path = rt.CameraPath(center, 36)
     cams = [path.circular_path(f % 36) for f in range(F)]
 
-    rows = (H + world - 1) // world            # rows per rank (padded)
-    my_rows = len(range(rank, H, world))
+    rows = rows_per_rank(H, world)             # rows per rank (padded)
+    my_rows = len(shard_rows(rank, world, H))
     ids = torch.empty((F, rows, W), dtype=torch.int32, device=dev)
     rgb = torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev)
     cnt = torch.zeros((F,), dtype=torch.int64, device=dev)
@@ -136,8 +137,7 @@ def main():
             dist.gather(ids, gather_ids, dst=0)
             dist.gather(rgb, gather_rgb, dst=0)
             if rank == 0:  # de-interleave: image row j = r*world + rank
-                full = torch.stack(gather_rgb).permute(1, 2, 0, 3, 4).reshape(F, rows * world, W, 3)[:, :H]
-                return full
+                return deinterleave(torch.stack(gather_rgb), H)
         return rgb
 
     # exactness check of the headline workload (outside timing): frame 0 vs

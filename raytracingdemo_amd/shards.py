@@ -1,0 +1,32 @@
+"""Row-interleaved image shards for the one-process-per-GPU driver.
+
+Image row j is rendered by rank j mod world (interleaving
+balances the depth-complexity gradient of a frame).  Every rank holds
+`rows_per_rank(H, world)` rows (the last one padding where H % world != 0), so
+the shards gather with one equal-sized collective; rank 0 de-interleaves.
+"""
+from __future__ import annotations
+
+
+def rows_per_rank(H: int, world: int) -> int:
+    return (H + world - 1) // world
+
+
+def shard_rows(rank: int, world: int, H: int) -> range:
+    """Image rows of `rank`'s shard, in shard order (row r of the shard is image row rank + r*world)."""
+    return range(rank, H, world)
+
+
+def deinterleave(gathered, H: int):
+    """Full images from gathered shards.
+
+    gathered: tensor [world, F, rows, W, ...] (shard k from rank k, rows =
+    rows_per_rank(H, world)).  Returns [F, H, W, ...] with image row
+    j = r*world + k taken from shard k, row r; padding rows are dropped.
+    """
+    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+    rest = tuple(gathered.shape[3:])
+    nd = gathered.dim()
+    perm = (1, 2, 0) + tuple(range(3, nd))
+    full = gathered.permute(*perm).reshape((F, rows * world) + rest)
+    return full[:, :H]

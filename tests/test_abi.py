@@ -1,0 +1,92 @@
+"""The C ABI library (CPU-only checks: no compute call needs a GPU here).
+
+librtmi355x.so loads, exports every function include/rt.h declares, reports
+the header's ABI version, and its host-only entry points (loader, scene build,
+camera path, tree dump) work without a device.  Device entry points must fail
+loudly (RT_ERR_NO_DEVICE) rather than fall back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "rt.h")
+
+
+def _lib():
+    from raytracingdemo_amd import _native as N
+    if not os.path.exists(N.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "raytracingdemo_amd", "csrc")], check=True)
+    return N, N.lib()
+
+
+def declared_functions() -> list[str]:
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(rt_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    assert "rt_render_frame" in names and "rt_scene_create" in names
+    assert len(names) >= 15
+
+
+def test_library_exports_every_declared_symbol():
+    N, L = _lib()
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+    assert sorted(N.EXPORTS) == declared_functions()
+
+
+def test_abi_version_matches_header():
+    _, L = _lib()
+    v = int(re.search(r"#define RT_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert L.rt_abi_version() == v
+
+
+def test_status_codes_match_header():
+    N, _ = _lib()
+    src = open(HEADER).read()
+    for name in ("RT_OK", "RT_ERR_INVALID_ARGUMENT", "RT_ERR_OUT_OF_RANGE", "RT_ERR_RUNTIME", "RT_ERR_HIP",
+                 "RT_ERR_NO_DEVICE", "RT_MODE_EXACT", "RT_MODE_FP64", "RT_FLAG_COUNT", "RT_FLAG_TIMING"):
+        v = int(re.search(rf"#define {name} (\d+)", src).group(1))
+        assert getattr(N, name) == v, name
+
+
+def test_frame_stats_struct_matches_header():
+    """The ctypes mirror has exactly the header's rt_frame_stats_t fields, in order."""
+    N, _ = _lib()
+    src = open(HEADER).read()
+    end = src.index("} rt_frame_stats_t;")
+    body = src[src.rindex("typedef struct {", 0, end) + len("typedef struct {"):end]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        for name in decl.split(None, 1)[1].split(","):
+            fields.append(re.sub(r"\[.*\]", "", name).strip())
+    assert [f for f, _ in N.rt_frame_stats_t._fields_] == fields
+
+
+def test_last_error_is_a_string():
+    _, L = _lib()
+    assert isinstance(L.rt_last_error(), bytes)
+
+
+def test_device_calls_fail_loudly_without_upload():
+    """No CPU fallback: rendering a scene that is on no device is an error."""
+    import numpy as np
+    import raytracingdemo_amd as rt
+    tri = np.array([[-1.0, -1.0, 0.0, 1.0, -1.0, 0.0, 0.0, 1.0, 0.0]])
+    s = rt.Scene(tri, "bsah", 2)
+    with pytest.raises(rt.RTError, match="not uploaded"):
+        s.calculate_screen([0, 0, 5], [0, 0, -1], 8, 8)

@@ -182,6 +182,45 @@ def test_edge_scenes(oracle):
     compare_with_oracle(oracle, s, deg, c + np.array([0.0, 0.0, 5.0]), [0.0, 0.0, -1.0], 80, 60, "sah", 4)
 
 
+def _stack_scene(eps: float, n: int, far_hit: bool) -> np.ndarray:
+    """n triangles stacked along -z with a corner at (eps, eps): the centre ray
+    of an odd-sized frame (direction exactly (0, 0, -1)) grazes every corner,
+    so the fp32 filter can only call them borderline."""
+    tris = [[eps, eps, -k, 1.0, eps, -k, eps, 1.0, -k] for k in range(1, n + 1)]
+    if far_hit:  # one robust hit far behind the stack
+        tris.append([-3.0, -3.0, -30.0, 3.0, -3.0, -30.0, 0.0, 3.0, -30.0])
+    return np.array(tris, dtype=np.float64)
+
+
+def test_candidate_overflow_paths(oracle):
+    """More borderline candidates than the per-lane list holds (K = 8).
+
+    (a) corners exactly on the ray: the nearest is a real hit and is certified
+        against the smallest dropped bound;
+    (b) corners 1e-7 off the ray: every listed candidate fails the exact test,
+        the real hit was dropped, so the pixel must be redone by the fix-up
+        kernel.  Both must equal the reference traversal."""
+    torch = pytest.importorskip("torch")
+    for eps, far, need_redo in ((0.0, False, False), (1e-7, True, True)):
+        tris = _stack_scene(eps, 14, far)
+        s = rt.Scene(tris, "bsah", 8).upload([0])
+        for W in (33, 65):
+            compare_with_oracle(oracle, s, tris, [0.0, 0.0, 10.0], [0.0, 0.0, -1.0], W, W, "bsah", 8)
+        W = 33
+        ids = torch.empty(W * W, dtype=torch.int32, device="cuda:0")
+        st = torch.cuda.current_stream()
+        s.frame_stats(0, reset=True)
+        s.render_rows_device(0, [0.0, 0.0, 10.0], [0.0, 0.0, -1.0], W, W, 0, 1, W, hit_id=ids.data_ptr(),
+                             stream=st.cuda_stream, count=True)
+        torch.cuda.synchronize()
+        fs = s.frame_stats(0, reset=True)
+        # redo because of the bounded list (not because the reference cannot
+        # see the winner: with d = (0, 0, -1) the reference's (0 - 0) * inf slab
+        # terms are NaN, and chain failures are expected on the corner pixel)
+        over = fs["redo_rays"] - fs["redo_chain"]
+        assert (over > 0) == need_redo, (fs["redo_rays"], fs["redo_chain"])
+
+
 def test_row_shards_reassemble_to_full_frame():
     """Row-interleaved shards (multi-GPU partition) rebuild the full frame bit for bit."""
     torch = pytest.importorskip("torch")

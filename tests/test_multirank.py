@@ -1,0 +1,93 @@
+"""Multi-rank path of bench.py on CPU: world size 2 (and 3) over gloo.
+
+Each rank takes the image rows `shard_rows(rank, world, H)` of a frame, pads
+its shard to `rows_per_rank`, the shards are gathered to rank 0 with one
+collective (bench.py uses RCCL; the logic is backend-independent) and
+`deinterleave` must rebuild the single-process frame bit for bit.  The frame
+content comes from the oracle (test infrastructure), rendered on the CPU.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from raytracingdemo_amd.shards import deinterleave, rows_per_rank, shard_rows  # noqa: E402
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _frames(W: int, H: int, F: int) -> np.ndarray:
+    """F reference-semantics frames (rgb) of a small scene, from the oracle."""
+    import pyoracle
+    from conftest import golden_scene
+    o = pyoracle.Oracle()
+    tris = golden_scene("teapot.obj")
+    b = o.bvh(tris, "bsah", 4)
+    c = o.scene_center(tris)
+    out = []
+    for f in range(F):
+        pos, d = o.camera_path(c, 36, 3 * f)
+        out.append(b.render(pos, d, W, H, want=("rgb",))["rgb"].reshape(H, W, 3))
+    return np.stack(out)
+
+
+def _worker(rank: int, world: int, port: int, W: int, H: int, F: int, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = _frames(W, H, F)
+        rows = rows_per_rank(H, world)
+        mine = list(shard_rows(rank, world, H))
+        shard = torch.full((F, rows, W, 3), 255, dtype=torch.uint8)  # padding rows stay 255
+        shard[:, : len(mine)] = torch.from_numpy(full[:, mine])
+        gathered = [torch.empty_like(shard) for _ in range(world)] if rank == 0 else None
+        dist.gather(shard, gathered, dst=0)
+        if rank == 0:
+            img = deinterleave(torch.stack(gathered), H).numpy()
+            q.put(("ok", bool(np.array_equal(img, full)), img.shape))
+    except Exception as e:  # surface worker failures to the test
+        q.put(("err", repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H", [(2, 37), (2, 40), (3, 29)])
+def test_row_interleaved_shards_gather_to_full_frame(world, H):
+    W, F = 24, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, F, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    status, ok, shape = q.get(timeout=10)
+    assert status == "ok", ok
+    assert ok and shape == (F, H, W, 3)
+
+
+def test_deinterleave_single_process():
+    H, W, F = 11, 5, 3
+    full = torch.arange(F * H * W, dtype=torch.int32).reshape(F, H, W)
+    for world in (1, 2, 3, 4, 8, 11, 13):
+        rows = rows_per_rank(H, world)
+        sh = torch.full((world, F, rows, W), -1, dtype=torch.int32)
+        for r in range(world):
+            idx = list(shard_rows(r, world, H))
+            sh[r, :, : len(idx)] = full[:, idx]
+        assert torch.equal(deinterleave(sh, H), full)

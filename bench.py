@@ -35,8 +35,6 @@ TRI32_BYTES = 48       # fp32 pre-filter record (v0, e1, e2 + 3 bounds)
 TRI64_BYTES = 80       # fp64 record (v0, e1, e2, rank, leaf) per exact Moller-Trumbore test
 CHAIN_BYTES = 52       # fp64 box (48 B) + parent (4 B) per re-verified ancestor
 OUT_BYTES = 7          # u32 hit-id + 3 B rgb written per ray
-CAM_BYTES = 16         # px[i] + py[j] per ray (per-lane kernel)
-CAM_TILE_BYTES = 128   # 8 px + 8 py doubles per 8x8 tile (packet kernel)
 CAND_BYTES = 8         # one candidate entry {triangle, t bound} handed to the resolve kernel
 
 
@@ -164,13 +162,13 @@ def main():
                             cs["rays"] * OUT_BYTES) / max(cs["rays"], 1)
     if cs["wave_tiles"]:
         # packet traversal kernel (the dominant kernel): a node or triangle
-        # record is fetched once per wave for its 64 rays; plus the camera
-        # coefficients of each tile and the candidate lists it writes
-        trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES + cs["wave_tiles"] * CAM_TILE_BYTES +
+        # record is fetched once per wave for its 64 rays; plus the candidate
+        # lists it writes (rays are generated in-kernel: no camera reads)
+        trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES +
                        cs["rays"] * 1 + cs["tri_tests"] * CAND_BYTES)
     else:  # per-lane kernel: each ray fetches its own records
         trace_bytes = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
-                       cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * (OUT_BYTES + CAM_BYTES))
+                       cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * OUT_BYTES)
     alg_bytes_per_launch = trace_bytes / F
 
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]

@@ -16,14 +16,23 @@ namespace {
 inline double len3(double x, double y, double z) { return std::sqrt(x * x + y * y + z * z); }
 }  // namespace
 
-void pixel_caches(int W, int H, std::vector<double>& px, std::vector<double>& py) {
+// Camera constructor constants (camera.hpp:20-38): 1/W, 1/H, tan(fov/2), W/H.
+void pixel_constants(int W, int H, double& iw, double& ih, double& half, double& aspect) {
     const unsigned w = (unsigned)W, h = (unsigned)H;
     const double fov = 90.0 * (std::numbers::pi / 180.0);
-    const double half = std::tan(fov * 0.5);
-    const double aspect = static_cast<double>(w) / h;
-    const double iw = 1.0 / w, ih = 1.0 / h;
-    px.resize(w);
-    py.resize(h);
+    half = std::tan(fov * 0.5);
+    aspect = static_cast<double>(w) / h;
+    iw = 1.0 / w;
+    ih = 1.0 / h;
+}
+
+// The camera's pixel caches (camera.hpp:35-37); the kernels evaluate the same
+// expressions per pixel (kernels_common.h pixel_x / pixel_y).
+void pixel_caches(int W, int H, std::vector<double>& px, std::vector<double>& py) {
+    double iw, ih, half, aspect;
+    pixel_constants(W, H, iw, ih, half, aspect);
+    px.resize((unsigned)W);
+    py.resize((unsigned)H);
     for (int x = 0; x < W; ++x) px[x] = (2.0 * (x + 0.5) * iw - 1.0) * half * aspect;
     for (int y = 0; y < H; ++y) py[y] = (1.0 - 2.0 * (y + 0.5) * ih) * half;
 }

@@ -146,18 +146,40 @@ __device__ __forceinline__ int tri_classify(const float4 A, const float4 B, cons
     if (Us < -errU || Vs < -errV || Ts < -errT) return 0;
     if (Us + Vs > aa + errU + errV + errA) return 0;
     if (Ts - errT > tcull * (aa + errA)) return 0;  // t > tcull: cannot improve
+    // bounds through v_rcp_f32 (<= 1 ulp) and one rounded multiply: the
+    // 2^-20 factors cover both roundings with room to spare
+#ifndef RT_RCP_BOUNDS
+#define RT_RCP_BOUNDS 1
+#endif
+#if RT_RCP_BOUNDS
+    tl = fmaxf((Ts - errT) * __builtin_amdgcn_rcpf(aa + errA), 0.f) * (1.f - 0x1p-20f);
+#else
     tl = fmaxf((Ts - errT) / (aa + errA), 0.f) * (1.f - 0x1p-20f);
+#endif
     const float EPS = 1e-8f;
     const bool certain = Us >= errU && Vs >= errV && Us + Vs <= aa - errU - errV - errA && aa - errA >= 2.f * EPS &&
                          Ts - errT >= 2.f * EPS * (aa + errA);
     if (!certain) return 1;
+#if RT_RCP_BOUNDS
+    tu = (Ts + errT) * __builtin_amdgcn_rcpf(aa - errA) * (1.f + 0x1p-20f);
+#else
     tu = (Ts + errT) / (aa - errA) * (1.f + 0x1p-20f);
+#endif
     return 2;
+}
+
+// Camera pixel caches (camera.hpp:35-37), evaluated per pixel in the same
+// operation order as the host's pixel_caches (no contraction): bit-identical.
+__device__ __forceinline__ double pixel_x(const RtFrameParams& fp, int x) {
+    return (2.0 * ((double)x + 0.5) * fp.cam_iw - 1.0) * fp.cam_half * fp.cam_aspect;
+}
+__device__ __forceinline__ double pixel_y(const RtFrameParams& fp, int y) {
+    return (1.0 - 2.0 * ((double)y + 0.5) * fp.cam_ih) * fp.cam_half;
 }
 
 // main.cpp:332-337: d = dir + up*py + right*px; d *= 1/|d|; Ray{pos, d}
 __device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) {
-    const double px = fp.px[i], py = fp.py[j];
+    const double px = pixel_x(fp, i), py = pixel_y(fp, j);
     double dx = (fp.dir[0] + fp.up[0] * py) + fp.right[0] * px;
     double dy = (fp.dir[1] + fp.up[1] * py) + fp.right[1] * px;
     double dz = (fp.dir[2] + fp.up[2] * py) + fp.right[2] * px;

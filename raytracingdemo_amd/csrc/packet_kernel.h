@@ -47,6 +47,15 @@
 #define RT_TACC(slot, t0)
 #endif
 
+// Packed (lo, hi) slab fma (measured: no gain over scalar fma); next-tile
+// prefetch (measured: slower, a reserved tile lengthens the tail).
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 0
+#endif
+#ifndef RT_TILE_PREFETCH
+#define RT_TILE_PREFETCH 0
+#endif
+
 // Node record fetch: 0 scalar loads (default), 1 uniform vector loads.
 #ifndef RT_NODE_FETCH
 #define RT_NODE_FETCH 0
@@ -67,6 +76,7 @@ struct __attribute__((aligned(32))) ChildRec {  // 32-B child record (rt_device.
     uint32_t ref, pad;
 };
 typedef const __attribute__((address_space(4))) float* cfloat_p;
+typedef float f2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(4))) ChildRec* cchild_p;
 
 // Field-wise reads through the constant address space: adjacent uniform loads
@@ -93,6 +103,24 @@ __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x) {
     asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
     return v;
 }
+// BIT if any lane is set in the wave mask, else 0 — two SALU instructions
+// (the compiler otherwise routes the uniform bool through a VGPR).
+template <uint32_t BIT>
+__device__ __forceinline__ uint32_t any_bit(uint64_t m) {
+    uint32_t r;
+    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, %2, 0" : "=s"(r) : "s"(m), "i"(BIT) : "scc");
+    return r;
+}
+
+// Bit c set iff any lane of hm[c] is set (W x two SALU instructions).
+template <int W>
+__device__ __forceinline__ uint32_t any_mask(const uint64_t (&hm)[W]) {
+    uint32_t m = 0;
+    [&]<int... C>(std::integer_sequence<int, C...>) { ((m |= any_bit<1u << C>(hm[C])), ...); }(
+        std::make_integer_sequence<int, W>{});
+    return m;
+}
+
 // A zero the compiler must treat as per-lane (forces vector-memory loads).
 __device__ __forceinline__ int vzero() {
     int z;
@@ -212,6 +240,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
     const float olx = (q.ox + pd) * q.ix, ohx = (q.ox - pd) * q.ix;
     const float oly = (q.oy + pd) * q.iy, ohy = (q.oy - pd) * q.iy;
     const float olz = (q.oz + pd) * q.iz, ohz = (q.oz - pd) * q.iz;
+    const f2 nox{-olx, -ohx}, noy{-oly, -ohy}, noz{-olz, -ohz};
 
     uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0, w_tris = 0;  // COUNT only
     float tcull = valid ? __builtin_huge_valf() : -1.f;
@@ -282,20 +311,24 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
 #endif
                 RT_TACC(0, t_n0);
                 RT_TSTAMP(t_n1);
-                uint32_t mask = 0;
+                uint64_t hm[W];  // per child: lanes whose ray enters it
 #pragma unroll
                 for (int c = 0; c < W; c++) {
-                    const float tlx = __builtin_fmaf(bx[c][0], q.ix, -olx);
-                    const float thx = __builtin_fmaf(bx[c][1], q.ix, -ohx);
-                    const float tly = __builtin_fmaf(bx[c][2], q.iy, -oly);
-                    const float thy = __builtin_fmaf(bx[c][3], q.iy, -ohy);
-                    const float tlz = __builtin_fmaf(bx[c][4], q.iz, -olz);
-                    const float thz = __builtin_fmaf(bx[c][5], q.iz, -ohz);
-                    const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
-                    const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
-                    mask |= __ballot(t0 <= t1) != 0 ? (1u << c) : 0u;
+#if RT_PK_SLAB
+                    // (lo, hi) plane pairs in one packed fma each (v_pk_fma_f32)
+                    const f2 tx = __builtin_elementwise_fma(f2{bx[c][0], bx[c][1]}, f2{q.ix, q.ix}, nox);
+                    const f2 ty = __builtin_elementwise_fma(f2{bx[c][2], bx[c][3]}, f2{q.iy, q.iy}, noy);
+                    const f2 tz = __builtin_elementwise_fma(f2{bx[c][4], bx[c][5]}, f2{q.iz, q.iz}, noz);
+#else
+                    const f2 tx{__builtin_fmaf(bx[c][0], q.ix, nox.x), __builtin_fmaf(bx[c][1], q.ix, nox.y)};
+                    const f2 ty{__builtin_fmaf(bx[c][2], q.iy, noy.x), __builtin_fmaf(bx[c][3], q.iy, noy.y)};
+                    const f2 tz{__builtin_fmaf(bx[c][4], q.iz, noz.x), __builtin_fmaf(bx[c][5], q.iz, noz.y)};
+#endif
+                    const float t0 = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), 0.f));
+                    const float t1 = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fminf(fmaxf(tz.x, tz.y), tcull));
+                    hm[c] = __ballot(t0 <= t1);
                 }
-                mask &= (1u << (meta >> 2)) - 1u;
+                uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);
                 if (mask != 0) {
                     // children are sorted along `axis`: walk them front to back
                     // for the tile's direction (lowest index first when the
@@ -536,28 +569,34 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
 #if RT_TILE_SCHED == 2
     uint32_t iter = 0;  // diagnostic: static round-robin, no atomics
 #endif
+    // The next tile index is fetched one tile ahead, so the queue atomic's
+    // round trip overlaps the current tile's walk.
+    auto fetch = [&]() -> int {
+        int t = 0;
+#if RT_TILE_SCHED == 0
+        if (lane == 0) t = (int)atomicAdd(kload(&A->aux.tile_ctr), 1u);
+#elif RT_TILE_SCHED == 1
+        if (lane == 0) t = (int)(xq + RT_QUEUES * atomicAdd(kload(&A->aux.tile_ctr) + xq * RT_QUEUE_STRIDE, 1u));
+#else
+        t = (int)((blockIdx.x * 4 + wv) + iter++ * gridDim.x * 4);
+#endif
+        return t;
+    };
+    int next = RT_TILE_PREFETCH ? fetch() : 0;
     for (;;) {
         A = launder(A);
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
-        RT_G uint32_t* const qblk = kload(&A->aux.tile_ctr);
         const int tiles_x = (W_ + 7) >> 3;
         const int tiles = tiles_x * ((nrows + 7) >> 3);
-        int tile = 0;
         RT_TSTAMP(t_q0);
-#if RT_TILE_SCHED == 0
-        if (lane == 0) tile = (int)atomicAdd(qblk, 1u);
-        tile = __shfl(tile, 0);
-#elif RT_TILE_SCHED == 1
-        if (lane == 0) tile = (int)(xq + RT_QUEUES * atomicAdd(qblk + xq * RT_QUEUE_STRIDE, 1u));
-        tile = __shfl(tile, 0);
-#else
-        tile = (int)((blockIdx.x * 4 + wv) + iter++ * gridDim.x * 4);
-#endif
+        if (!RT_TILE_PREFETCH) next = fetch();
+        const int tile = __shfl(next, 0);
 #ifdef RT_DIAG_TIMING
         asm volatile("" ::"v"(tile));
 #endif
         RT_TACC(7, t_q0);
         if (tile >= tiles) break;
+        if (RT_TILE_PREFETCH) next = fetch();
         const int i = (tile % tiles_x) * 8 + (lane & 7);
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
         trace_packet<W, SP, K, COUNT>(A, i, r, i < W_ && r < nrows, stacks[wv], cands[wv], tacc);

@@ -62,8 +62,6 @@ struct Replica {
     void* blob = nullptr;       // one allocation for the whole scene
     size_t blob_bytes = 0;
     RtDevScene dev{};
-    double* d_cam = nullptr;    // px[W] ++ py[H]
-    int cam_w = 0, cam_h = 0;
     unsigned long long* d_counters = nullptr;  // [0..15] RT_FLAG_COUNT counters, [16..23] diagnostics
     // staging for the host-output frame call
     void* frame = nullptr;
@@ -111,7 +109,6 @@ void free_replica(Replica& r) {
     hipGetDevice(&prev);
     hipSetDevice(r.device);
     if (r.blob) hipFree(r.blob);
-    if (r.d_cam) hipFree(r.d_cam);
     if (r.d_counters) hipFree(r.d_counters);
     if (r.frame) hipFree(r.frame);
     if (r.d_tiles) hipFree(r.d_tiles);
@@ -207,21 +204,6 @@ void upload_one(rt_scene* s, int device) {
     s->reps.push_back(r);
 }
 
-// Coefficients for (W, H) on the replica's device (re-uploaded on change).
-void ensure_camera(Replica& r, int W, int H, hipStream_t stream) {
-    if (r.cam_w == W && r.cam_h == H) return;
-    std::vector<double> px, py;
-    rt::pixel_caches(W, H, px, py);
-    if (r.d_cam) HIP_TRY(hipFree(r.d_cam));
-    r.d_cam = nullptr;
-    HIP_TRY(hipMalloc(&r.d_cam, sizeof(double) * (size_t)(W + H)));
-    px.insert(px.end(), py.begin(), py.end());
-    HIP_TRY(hipMemcpyAsync(r.d_cam, px.data(), sizeof(double) * px.size(), hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    r.cam_w = W;
-    r.cam_h = H;
-}
-
 // Redo list and candidate buffers large enough for every pixel of a launch
 // (grown, never shrunk).
 void ensure_redo(Replica& r, uint64_t pixels) {
@@ -274,8 +256,7 @@ RtFrameParams frame_params(const rt_scene* s, Replica& r, const rt_camera* c, in
         fp.dir[a] = c->dir[a];
     }
     rt::camera_basis(c->dir, fp.right, fp.up);
-    fp.px = r.d_cam;
-    fp.py = r.d_cam + c->width;
+    rt::pixel_constants(c->width, c->height, fp.cam_iw, fp.cam_ih, fp.cam_half, fp.cam_aspect);
     fp.W = c->width;
     fp.H = c->height;
     fp.row0 = row0;
@@ -438,7 +419,6 @@ int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mod
         }
         DevGuard g(device);
         hipStream_t st = (hipStream_t)stream;
-        ensure_camera(*r, cam->width, cam->height, st);
         RtFrameParams fp = frame_params(s, *r, cam, row0, row_stride, nrows);
         fp.hit_id = out->hit_id;
         fp.dist = out->dist;
@@ -492,7 +472,6 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         d.rgb = reinterpret_cast<uint8_t*>(base + o_rgb);  // always shaded (shadeScreen)
         d.hit_count = reinterpret_cast<unsigned long long*>(base + o_cnt);
         order_on(r, r.stream);
-        ensure_camera(r, cam->width, cam->height, r.stream);
         HIP_TRY(hipMemsetAsync(d.hit_count, 0, 8, r.stream));
         RtFrameParams fp = frame_params(s, r, cam, 0, 1, cam->height);
         fp.hit_id = d.hit_id;

@@ -92,8 +92,8 @@ struct RtLaunchAux {
 
 struct RtFrameParams {
     double pos[3], dir[3], right[3], up[3];
-    const RT_G double* px;  // W pixel-plane x coefficients (camera.hpp:35)
-    const RT_G double* py;  // H pixel-plane y coefficients (camera.hpp:37)
+    double cam_iw, cam_ih;        // 1/W, 1/H            (camera.hpp:33-34)
+    double cam_half, cam_aspect;  // tan(fov/2), W/H      (camera.hpp:29-30)
     int32_t W, H;
     int32_t row0, row_stride, nrows;
     RT_G uint32_t* hit_id;

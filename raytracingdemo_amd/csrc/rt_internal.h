@@ -64,6 +64,7 @@ struct Flat {
 Flat flatten(const Soup& s, const Tree& t, int width_hint);
 
 // Camera helpers (camera.hpp:20-38, main.cpp:325-329, camera_path.hpp:18-26)
+void pixel_constants(int W, int H, double& iw, double& ih, double& half, double& aspect);
 void pixel_caches(int W, int H, std::vector<double>& px, std::vector<double>& py);
 void camera_basis(const double dir[3], double right[3], double up[3]);
 void camera_path(const double center[3], int res, int step, double pos[3], double dir[3]);

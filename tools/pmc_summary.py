@@ -23,7 +23,7 @@ def main() -> None:
             name = row["Kernel_Name"]
             if a.match not in name:
                 continue
-            short = name.split("(")[0].replace("void (anonymous namespace)::", "")
+            short = name.replace("void (anonymous namespace)::", "").split("(")[0]
             tot[short][row["Counter_Name"]] += float(row["Counter_Value"])
             disp[short].add((path, row["Dispatch_Id"]))
     for k, cs in tot.items():

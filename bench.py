@@ -244,7 +244,13 @@ def main():
                                      "wave_tris_per_tile": round(cs["wave_tris"] / max(cs["wave_tiles"], 1), 2),
                                      "redo_rays": round(cs["redo_rays"] / max(cs["rays"], 1), 7),
                                      "redo_chain": round(cs["redo_chain"] / max(cs["rays"], 1), 7),
-                                     **({"diag_ticks_per_tile": [round(x / tiles_timed) for x in diag]}
+                                     **({"diag_ticks_per_tile": [round(x / tiles_timed) for x in diag[:8]],
+                                         "diag_wave_life_mean_us": round(diag[8] / max(diag[10], 1) / 100, 2),
+                                         "diag_wave_life_max_us": round(diag[9] / 100, 2),
+                                         "diag_busy_fraction": round(diag[8] / max(diag[10], 1) / 100 /
+                                                                     (avg_kernel_s * 1e6), 3),
+                                         "diag_waves_per_launch": round(diag[10] / launches_timed, 1),
+                                         "diag_max_tiles_per_wave": int(diag[11])}
                                         if any(diag) else {}),
                                      "node_bytes": st["node_bytes"], "tri32_bytes": TRI32_BYTES,
                                      "tri64_bytes": TRI64_BYTES}},

@@ -116,9 +116,11 @@ typedef struct {
     uint64_t wave_tris;     /* packet kernel: triangle records fetched per wave */
     uint64_t redo_rays;     /* rays finished by the fix-up kernel (exact per-lane path) */
     uint64_t redo_chain;    /*   of which: winner invisible to the reference (chain check) */
-    uint64_t diag_cycles[8]; /* diagnostic builds only (else 0): wave clock ticks in
+    uint64_t diag_cycles[12]; /* diagnostic builds only (else 0): wave clock ticks in
                                 node-load wait, node work, leaves, stack pops, ray
-                                set-up, exact resolve, output, tile fetch */
+                                set-up, candidate output, -, tile fetch; then
+                                traversal-wave lifetime sum and max (10-ns ticks),
+                                wave count, max tiles per wave */
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */
@@ -162,6 +164,11 @@ int rt_render_rows_device(rt_scene *s, int device, const rt_camera *cam, int mod
 int rt_frame_stats(rt_scene *s, int device, int reset, rt_frame_stats_t *out);
 
 int rt_scene_stats(const rt_scene *s, rt_scene_stats_t *out);
+
+/* Diagnostics: copy up to n words of the device's raw counter block (the
+ * rt_frame_stats counters followed by the diagnostic-build accumulators;
+ * tools/diag_hist.py).  Synchronises the device. */
+int rt_diag_raw(rt_scene *s, int device, uint64_t *out, size_t n);
 
 /* Reference visit order rank of every triangle (loader index -> rank) and
  * the real tree in reference visit order, for tree-parity tests:

@@ -33,7 +33,7 @@ RT_MISS = 0xFFFFFFFF
 EXPORTS = [
     "rt_load_obj", "rt_free", "rt_scene_center", "rt_camera_path", "rt_scene_create", "rt_scene_upload",
     "rt_render_frame", "rt_render_rows_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
-    "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name",
+    "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
 ]
 
 
@@ -72,7 +72,7 @@ class rt_frame_stats_t(C.Structure):
                 ("chain_checks", C.c_uint64), ("hits", C.c_uint64), ("chain_nodes", C.c_uint64),
                 ("tri_prefilter", C.c_uint64), ("wave_nodes", C.c_uint64), ("wave_leaves", C.c_uint64),
                 ("wave_tiles", C.c_uint64), ("wave_tris", C.c_uint64), ("redo_rays", C.c_uint64), ("redo_chain", C.c_uint64),
-                ("diag_cycles", C.c_uint64 * 8), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
+                ("diag_cycles", C.c_uint64 * 12), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
 
 
 _lib = None
@@ -123,6 +123,7 @@ def lib() -> C.CDLL:
                                         C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
     L.rt_frame_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(rt_frame_stats_t)]
     L.rt_scene_stats.argtypes = [C.c_void_p, C.POINTER(rt_scene_stats_t)]
+    L.rt_diag_raw.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
     L.rt_scene_tree_dump.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.rt_scene_destroy.argtypes = [C.c_void_p]
     _lib = L

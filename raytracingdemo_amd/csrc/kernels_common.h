@@ -252,11 +252,13 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDev
     }
     if (fp.hit_id) fp.hit_id[o] = b.tri >= 0 ? sc.tri_id[b.tri] : RT_INVALID_REF;
     if (fp.dist) fp.dist[o] = b.tri >= 0 ? b.dist : -1.0;
+#ifndef RT_DIAG_TILECOST
     if (fp.hit_pos) {
         fp.hit_pos[3 * o] = b.tri >= 0 ? b.px : 0.0;
         fp.hit_pos[3 * o + 1] = b.tri >= 0 ? b.py : 0.0;
         fp.hit_pos[3 * o + 2] = b.tri >= 0 ? b.pz : 0.0;
     }
+#endif
     if (count_hit && fp.hit_count) {  // one atomic per wave (all active lanes reach this)
         const uint64_t hits = __ballot(b.tri >= 0);
         const uint64_t act = __ballot(1);

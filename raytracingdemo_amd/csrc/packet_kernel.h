@@ -47,6 +47,17 @@
 #define RT_TACC(slot, t0)
 #endif
 
+#ifdef RT_DIAG_TILECOST
+#define RT_DIAG_WAVE_STATS 1
+#else
+#define RT_DIAG_WAVE_STATS 0
+#endif
+
+// Diagnostic accumulators (aux.diag): [0..7] cycle split, then RT_DIAG_SLOTS
+// spread slots of 8 words from RT_DIAG_SPREAD.
+#define RT_DIAG_SPREAD 16
+#define RT_DIAG_SLOTS 64
+
 // Packed (lo, hi) slab fma (measured: no gain over scalar fma); next-tile
 // prefetch (measured: slower, a reserved tile lengthens the tail).
 #ifndef RT_PK_SLAB
@@ -216,6 +227,39 @@ __device__ __forceinline__ T kword(const __attribute__((address_space(3))) T* p)
     return __builtin_bit_cast(T, uni(*(const __attribute__((address_space(3))) uint32_t*)p));
 }
 
+// Slab test of one node's W children for every lane's ray (fp32, outward
+// planes).  OCT >= 0: all rays share the direction signs OCT (bit a set =
+// negative along axis a), so each axis's near plane is the hi plane for a
+// negative direction and the lo plane otherwise — exactly what the per-axis
+// min/max of the general test (OCT = -1) selects, since t(lo) <= t(hi) for a
+// positive reciprocal and t(hi) <= t(lo) for a negative one.
+template <int W, int OCT>
+__device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32& q, const f2 nox, const f2 noy,
+                                           const f2 noz, float tcull, uint64_t (&hm)[W]) {
+    // fresh copies per specialisation: stops the compiler from hoisting the
+    // (identical) plane fmas of every switch case above the switch
+    float ix = q.ix, iy = q.iy, iz = q.iz;
+    asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
+#pragma unroll
+    for (int c = 0; c < W; c++) {
+        const float tlx = __builtin_fmaf(bx[c][0], ix, nox.x), thx = __builtin_fmaf(bx[c][1], ix, nox.y);
+        const float tly = __builtin_fmaf(bx[c][2], iy, noy.x), thy = __builtin_fmaf(bx[c][3], iy, noy.y);
+        const float tlz = __builtin_fmaf(bx[c][4], iz, noz.x), thz = __builtin_fmaf(bx[c][5], iz, noz.y);
+        float t0, t1;
+        if constexpr (OCT < 0) {
+            t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
+            t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
+        } else {
+            const float nx = (OCT & 1) ? thx : tlx, fx = (OCT & 1) ? tlx : thx;
+            const float ny = (OCT & 2) ? thy : tly, fy = (OCT & 2) ? tly : thy;
+            const float nz = (OCT & 4) ? thz : tlz, fz = (OCT & 4) ? tlz : thz;
+            t0 = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+            t1 = fminf(fminf(fx, fy), fminf(fz, tcull));
+        }
+        hm[c] = __ballot(t0 <= t1);
+    }
+}
+
 template <int W, int SP, int K, bool COUNT>
 __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid, uint32_t* __restrict__ wstack,
                                              uint2* __restrict__ cand, uint64_t* tacc) {
@@ -233,7 +277,10 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
         pd = fp.pad;
     }
     // direction sign bits (x, y, z) of lane 0's ray: the tile's ordering key
-    const uint32_t dsg = uni((q.ix < 0.f ? 1u : 0u) | (q.iy < 0.f ? 2u : 0u) | (q.iz < 0.f ? 4u : 0u));
+    const uint32_t lsg = (q.ix < 0.f ? 1u : 0u) | (q.iy < 0.f ? 2u : 0u) | (q.iz < 0.f ? 4u : 0u);
+    const uint32_t dsg = uni(lsg);
+    // the tile's octant if every ray that takes part shares lane 0's signs, else 8
+    const int oct = __ballot(valid && lsg != dsg) == 0 ? (int)dsg : 8;
     const RT_G uint8_t* const nodes = kload(&A->sc.nodes);
     const RT_G float* const tri32 = kload(&A->sc.tri32);
     // slab offsets for the lo / hi planes (pad moves lo down and hi up)
@@ -264,7 +311,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
         if (cur != RT_INVALID_REF) {
             if (!(cur & RT_LEAF_BIT)) {
                 RT_TSTAMP(t_n0);
-                if (COUNT) {
+                if (COUNT || RT_DIAG_WAVE_STATS) {
                     w_nodes++;
                     n_nodes += valid;
                 }
@@ -312,21 +359,19 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
                 RT_TACC(0, t_n0);
                 RT_TSTAMP(t_n1);
                 uint64_t hm[W];  // per child: lanes whose ray enters it
-#pragma unroll
-                for (int c = 0; c < W; c++) {
-#if RT_PK_SLAB
-                    // (lo, hi) plane pairs in one packed fma each (v_pk_fma_f32)
-                    const f2 tx = __builtin_elementwise_fma(f2{bx[c][0], bx[c][1]}, f2{q.ix, q.ix}, nox);
-                    const f2 ty = __builtin_elementwise_fma(f2{bx[c][2], bx[c][3]}, f2{q.iy, q.iy}, noy);
-                    const f2 tz = __builtin_elementwise_fma(f2{bx[c][4], bx[c][5]}, f2{q.iz, q.iz}, noz);
-#else
-                    const f2 tx{__builtin_fmaf(bx[c][0], q.ix, nox.x), __builtin_fmaf(bx[c][1], q.ix, nox.y)};
-                    const f2 ty{__builtin_fmaf(bx[c][2], q.iy, noy.x), __builtin_fmaf(bx[c][3], q.iy, noy.y)};
-                    const f2 tz{__builtin_fmaf(bx[c][4], q.iz, noz.x), __builtin_fmaf(bx[c][5], q.iz, noz.y)};
-#endif
-                    const float t0 = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), 0.f));
-                    const float t1 = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fminf(fmaxf(tz.x, tz.y), tcull));
-                    hm[c] = __ballot(t0 <= t1);
+                // all lanes' rays share the tile's direction signs (nearly every
+                // tile): the near/far plane of each axis is known, no per-axis
+                // min/max; otherwise the general test
+                switch (oct) {
+                    case 0: child_hits<W, 0>(bx, q, nox, noy, noz, tcull, hm); break;
+                    case 1: child_hits<W, 1>(bx, q, nox, noy, noz, tcull, hm); break;
+                    case 2: child_hits<W, 2>(bx, q, nox, noy, noz, tcull, hm); break;
+                    case 3: child_hits<W, 3>(bx, q, nox, noy, noz, tcull, hm); break;
+                    case 4: child_hits<W, 4>(bx, q, nox, noy, noz, tcull, hm); break;
+                    case 5: child_hits<W, 5>(bx, q, nox, noy, noz, tcull, hm); break;
+                    case 6: child_hits<W, 6>(bx, q, nox, noy, noz, tcull, hm); break;
+                    case 7: child_hits<W, 7>(bx, q, nox, noy, noz, tcull, hm); break;
+                    default: child_hits<W, -1>(bx, q, nox, noy, noz, tcull, hm); break;
                 }
                 uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);
                 if (mask != 0) {
@@ -353,7 +398,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
                 RT_TSTAMP(t_l0);
                 const uint32_t first = cur & RT_LEAF_FIRST_MASK;
                 const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
-                if (COUNT) {
+                if (COUNT || RT_DIAG_WAVE_STATS) {
                     w_leaves++;
                     w_tris += cnt;
                 }
@@ -419,6 +464,16 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
         atomicAdd(&fp.counters[9], 1ull);
         atomicAdd(&fp.counters[12], (unsigned long long)w_tris);
     }
+#ifdef RT_DIAG_TILECOST
+    {   // wave-level visits of this tile into hit_pos[3 * tile + 1 / + 2]
+        RT_G double* hp = fp.hit_pos;
+        const int tile = (r >> 3) * ((fp.W + 7) >> 3) + (i >> 3);
+        if (hp && (threadIdx.x & 63) == 0) {
+            hp[3 * (size_t)tile + 1] = (double)w_nodes + 1e6 * (double)w_leaves;
+            hp[3 * (size_t)tile + 2] = (double)w_tris;
+        }
+    }
+#endif
     if (!valid) return;
     // hand the lane's surviving candidates to k_resolve: count per pixel,
     // entry c of pixel o at cand[c * npix + o] (coalesced across a row)
@@ -562,6 +617,10 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
     }
     uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     (void)tacc;
+#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE)
+    const uint64_t t_life = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
+    uint32_t n_tiles = 0;
+#endif
     // tile scheduling: one queue per XCD (blocks are dealt to the 8 XCDs
     // round-robin, so block b's XCD is b % 8): queue x hands out tiles
     // x, x + 8, x + 16, ...; every queue is drained by the blocks b = x mod 8.
@@ -596,14 +655,52 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
 #endif
         RT_TACC(7, t_q0);
         if (tile >= tiles) break;
+#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE)
+        n_tiles++;
+#endif
         if (RT_TILE_PREFETCH) next = fetch();
         const int i = (tile % tiles_x) * 8 + (lane & 7);
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
+#if defined(RT_DIAG_HIST) || defined(RT_DIAG_TILECOST)
+        const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
+#endif
         trace_packet<W, SP, K, COUNT>(A, i, r, i < W_ && r < nrows, stacks[wv], cands[wv], tacc);
+#ifdef RT_DIAG_TILECOST
+        {   // per-tile duration (10-ns ticks) into hit_pos[3 * tile] (diagnostic build:
+            // shade_store leaves hit_pos alone)
+            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - th0;
+            RT_G double* hp = kload(&A->fp.hit_pos);
+            if (hp && lane == 0) hp[3 * (size_t)tile] = (double)dt;
+        }
+#endif
+#ifdef RT_DIAG_HIST
+        {   // per-tile duration histogram: 64 bins of 2 us (10-ns ticks)
+            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - th0;
+            RT_G unsigned long long* const dg = kload(&A->aux.diag);
+            const uint32_t bin = dt / 200 < 63 ? (uint32_t)(dt / 200) : 63u;
+            if (dg && lane == 0) atomicAdd(dg + RT_DIAG_SPREAD + bin * 8 + 4, 1ull);
+            // and where it was: rows of tiles, 64 bands, summed duration
+            const uint32_t band = (uint32_t)(tile / tiles_x) * 64u / (uint32_t)((nrows + 7) >> 3);
+            if (dg && lane == 0) atomicAdd(dg + RT_DIAG_SPREAD + (band & 63) * 8 + 5, dt);
+            const uint32_t cband = (uint32_t)(tile % tiles_x) * 64u / (uint32_t)tiles_x;
+            if (dg && lane == 0) atomicAdd(dg + RT_DIAG_SPREAD + (cband & 63) * 8 + 6, dt);
+        }
+#endif
     }
-#ifdef RT_DIAG_TIMING
+#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE)
     RT_G unsigned long long* const diag = kload(&A->aux.diag);
-    if (diag && lane == 0)
+    if (diag && lane == 0) {
+#ifdef RT_DIAG_TIMING
         for (int q = 0; q < 8; q++) atomicAdd(diag + q, (unsigned long long)tacc[q]);
+#endif
+        // tail: wave lifetimes (10-ns ticks) and tiles per wave, accumulated
+        // over RT_DIAG_SLOTS cache lines (one hot address would serialise)
+        const unsigned long long life = __builtin_amdgcn_s_memrealtime() - t_life;
+        RT_G unsigned long long* slot = diag + RT_DIAG_SPREAD + (blockIdx.x % RT_DIAG_SLOTS) * 8;
+        atomicAdd(slot + 0, life);
+        atomicMax(slot + 1, life);
+        atomicAdd(slot + 2, 1ull);
+        atomicMax(slot + 3, (unsigned long long)n_tiles);
+    }
 #endif
 }

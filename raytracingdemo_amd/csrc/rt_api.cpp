@@ -57,6 +57,10 @@ size_t align_up(size_t x) {
     return (x + 255) & ~size_t(255);
 }
 
+// d_counters: [0..15] RT_FLAG_COUNT counters, [16..) diagnostic block
+// (packet_kernel.h RT_DIAG_*: 16 words, then 64 spread slots of 8 words)
+constexpr size_t kCounterWords = 16 + 16 + 64 * 8;
+
 struct Replica {
     int device = -1;
     void* blob = nullptr;       // one allocation for the whole scene
@@ -188,8 +192,8 @@ void upload_one(rt_scene* s, int device) {
     d.node_bytes = rt_node_bytes(f.width);
     d.width = f.width;
     d.stack_bound = f.stack_bound;
-    HIP_TRY(hipMalloc(&r.d_counters, 32 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemset(r.d_counters, 0, 32 * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&r.d_counters, kCounterWords * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(r.d_counters, 0, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
@@ -501,14 +505,28 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
     }
 }
 
+int rt_diag_raw(rt_scene* s, int device, uint64_t* out, size_t n) {
+    if (!s || (!out && n)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    try {
+        Replica& r = replica_for(s, device);
+        DevGuard g(device);
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(out, r.d_counters, std::min(n, kCounterWords) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
 int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
     if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     try {
         Replica& r = replica_for(s, device);
         DevGuard g(device);
         HIP_TRY(hipDeviceSynchronize());
-        unsigned long long c[32];
-        HIP_TRY(hipMemcpy(c, r.d_counters, sizeof c, hipMemcpyDeviceToHost));
+        std::vector<unsigned long long> cv(kCounterWords);
+        HIP_TRY(hipMemcpy(cv.data(), r.d_counters, cv.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        const unsigned long long* c = cv.data();
         out->rays = c[0];
         out->node_fetches = c[1];
         out->tri_tests = c[2];
@@ -523,6 +541,19 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->redo_rays = c[10] + c[11];
         out->redo_chain = c[11];
         for (int q = 0; q < 8; q++) out->diag_cycles[q] = c[16 + q];
+        // spread slots: lifetime sum, lifetime max, waves, max tiles per wave
+        uint64_t lsum = 0, lmax = 0, nw = 0, tmax = 0;
+        for (int q = 0; q < 64; q++) {
+            const unsigned long long* sl = c + 32 + 8 * q;
+            lsum += sl[0];
+            lmax = std::max<uint64_t>(lmax, sl[1]);
+            nw += sl[2];
+            tmax = std::max<uint64_t>(tmax, sl[3]);
+        }
+        out->diag_cycles[8] = lsum;
+        out->diag_cycles[9] = lmax;
+        out->diag_cycles[10] = nw;
+        out->diag_cycles[11] = tmax;
         out->timed_launches = r.tev_used;
         out->trace_ms = 0.0;
         for (size_t k = 0; k < r.tev_used; k++) {
@@ -531,7 +562,7 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
             out->trace_ms += a;
         }
         if (reset) r.tev_used = 0;
-        if (reset) HIP_TRY(hipMemset(r.d_counters, 0, sizeof c));
+        if (reset) HIP_TRY(hipMemset(r.d_counters, 0, cv.size() * sizeof(unsigned long long)));
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);

@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 METRIC = "Mrays/sec (primary, 1spp) on Sponza 1920×1080; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 TRI32_BYTES = 48       # fp32 pre-filter record (v0, e1, e2 + 3 bounds)
-TRI64_BYTES = 80       # fp64 record (v0, e1, e2, rank, leaf) per exact Moller-Trumbore test
+TRI64_BYTES = 128      # fp64 record (v0, e1, e2, normal, id, leaf, leaf box) per exact test
 CHAIN_BYTES = 52       # fp64 box (48 B) + parent (4 B) per re-verified ancestor
 OUT_BYTES = 7          # u32 hit-id + 3 B rgb written per ray
 CAND_BYTES = 8         # one candidate entry {triangle, t bound} handed to the resolve kernel

@@ -535,11 +535,30 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
             for (int32_t c : nd.kids) st.push_back(c);
         }
     }
-    // rank and leaf ride in the fp64 record's 10th slot (one 80-B load burst)
+    // normal, loader id, leaf and the leaf box (fp32, rounded inward) complete
+    // the 128-B fp64 record (rt_device.h)
+    auto down = [](double x) {
+        float v = (float)x;
+        if ((double)v > x) v = std::nextafter(v, -std::numeric_limits<float>::infinity());
+        return v;
+    };
+    auto up = [](double x) {
+        float v = (float)x;
+        if ((double)v < x) v = std::nextafter(v, std::numeric_limits<float>::infinity());
+        return v;
+    };
     for (uint64_t i = 0; i < n; i++) {
-        uint32_t* w = reinterpret_cast<uint32_t*>(f.tri64.data() + i * RT_TRI64_DOUBLES + 9);
-        w[0] = f.tri_rank[i];
-        w[1] = f.tri_leaf[i];
+        double* q = f.tri64.data() + i * RT_TRI64_DOUBLES;
+        const uint32_t id = f.tri_id[i], leaf = f.tri_leaf[i];
+        for (int a = 0; a < 3; a++) q[RT_T64_NORMAL + a] = s.normal[(size_t)id * 3 + a];
+        uint32_t* w = reinterpret_cast<uint32_t*>(q + RT_T64_IDLEAF);
+        w[0] = id;
+        w[1] = leaf;
+        float* b = reinterpret_cast<float*>(q + RT_T64_BOX);
+        for (int a = 0; a < 3; a++) {
+            b[a] = up(f.rbox[(size_t)leaf * 6 + a]);
+            b[3 + a] = down(f.rbox[(size_t)leaf * 6 + 3 + a]);
+        }
     }
     // --- wide nodes
     Flattener F(s, t, f);

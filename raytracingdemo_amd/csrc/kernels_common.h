@@ -221,12 +221,27 @@ __device__ __forceinline__ double hit_dist(const Ray64& r, double t, double& px,
 // shadeScreen body (main.cpp:356-377) + PPM byte cast (benchmark.hpp:105-114)
 // count_hit: add this pixel's hit to fp.hit_count here (one atomic per wave);
 // k_resolve instead reduces per block and k_fixup adds the block sums once.
-__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDevScene& sc, size_t o, const Best& b,
+// Shading inputs of the winner, from its fp64 record (rt_device.h).
+struct Shade {
+    double nx, ny, nz;
+    uint32_t id;
+};
+__device__ __forceinline__ Shade shade_of(const RtDevScene& sc, int32_t tri) {
+    Shade s{0.0, 0.0, 0.0, RT_INVALID_REF};
+    if (tri >= 0) {
+        const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)tri;
+        s.nx = T[RT_T64_NORMAL];
+        s.ny = T[RT_T64_NORMAL + 1];
+        s.nz = T[RT_T64_NORMAL + 2];
+        s.id = reinterpret_cast<const RT_G uint2*>(T + RT_T64_IDLEAF)->x;
+    }
+    return s;
+}
+__device__ __forceinline__ void shade_store(const RtFrameParams& fp, size_t o, const Best& b, const Shade& sh,
                                             bool count_hit = true) {
     uint8_t c0 = 0, c1 = 0, c2 = 0;
     if (b.tri >= 0 && fp.rgb) {
-        const uint32_t id = sc.tri_id[b.tri];
-        double nx = sc.normal[3 * (size_t)id], ny = sc.normal[3 * (size_t)id + 1], nz = sc.normal[3 * (size_t)id + 2];
+        double nx = sh.nx, ny = sh.ny, nz = sh.nz;
         const double nl = __builtin_sqrt(nx * nx + ny * ny + nz * nz);
         if (nl > 0.0) {
             const double s = 1.0 / nl;
@@ -250,7 +265,7 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDev
         fp.rgb[3 * o + 1] = c1;
         fp.rgb[3 * o + 2] = c2;
     }
-    if (fp.hit_id) fp.hit_id[o] = b.tri >= 0 ? sc.tri_id[b.tri] : RT_INVALID_REF;
+    if (fp.hit_id) fp.hit_id[o] = b.tri >= 0 ? sh.id : RT_INVALID_REF;
     if (fp.dist) fp.dist[o] = b.tri >= 0 ? b.dist : -1.0;
 #ifndef RT_DIAG_TILECOST
     if (fp.hit_pos) {
@@ -265,6 +280,10 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDev
         if (hits != 0 && (int)(threadIdx.x & 63) == __builtin_ctzll(act))
             atomicAdd(fp.hit_count, (unsigned long long)__builtin_popcountll(hits));
     }
+}
+__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDevScene& sc, size_t o, const Best& b,
+                                            bool count_hit = true) {
+    shade_store(fp, o, b, shade_of(sc, b.tri), count_hit);
 }
 
 template <int W>
@@ -330,6 +349,23 @@ __device__ __forceinline__ bool chain_fast_ok(const double* __restrict__ b, cons
         const double m = 0x1p-48 * (__builtin_fabs(b[a]) + __builtin_fabs(b[3 + a]) + __builtin_fabs(o[a]) +
                                     __builtin_fabs(p[a]));
         if (!(p[a] - b[a] >= m && b[3 + a] - p[a] >= m)) return false;
+    }
+    return true;
+}
+// The same test on the record's fp32 leaf box, rounded inward (lo up, hi
+// down): a point inside it with the margin is inside the real box with more.
+// The margin is widened by 2^-20 relative (and 2^-190 absolute) to cover the
+// rounding gap between the fp32 and the real bounds in its own terms.
+__device__ __forceinline__ bool chain_fast_ok32(const float (&b)[6], const Ray64& r, double px, double py,
+                                                double pz) {
+    if (r.dx == 0.0 || r.dy == 0.0 || r.dz == 0.0) return false;
+    const double o[3] = {r.ox, r.oy, r.oz}, p[3] = {px, py, pz};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double lo = (double)b[a], hi = (double)b[3 + a];
+        const double m = 0x1p-48 * ((__builtin_fabs(lo) + __builtin_fabs(hi)) * (1.0 + 0x1p-20) +
+                                    __builtin_fabs(o[a]) + __builtin_fabs(p[a])) + 0x1p-190;
+        if (!(p[a] - lo >= m && hi - p[a] >= m)) return false;
     }
     return true;
 }

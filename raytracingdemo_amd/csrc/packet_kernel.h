@@ -523,23 +523,47 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
     out.px = out.py = out.pz = 0.0;
     uint32_t redo = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
     const uint32_t nlist = cnt & ~kCandDropped;
+    Shade sh{0.0, 0.0, 0.0, RT_INVALID_REF};
     if (cnt != 0) {
         const Ray64 ray = gen_ray(fp, i, fp.row0 + r * fp.row_stride);
         double best_t = 0.0;
+        uint32_t leaf = 0;
+        float lb[6];
         for (uint32_t c = 0; c < nlist; c++) {
             const uint2 e = reinterpret_cast<const RT_G uint2*>(aux.cand)[(size_t)c * npix + o];
             if (COUNT) n_tris++;
+            // one 128-B record: triangle, normal, id, leaf and its box
             const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)e.x;
             double t;
             if (!mt64(T, ray, t)) continue;
             double hx, hy, hz;
             const double d = hit_dist(ray, t, hx, hy, hz);
-            const uint32_t rank = reinterpret_cast<const RT_G uint2*>(T + 9)->x;
-            if (d < out.dist || (d == out.dist && rank < out.rank)) {
+            bool take = d < out.dist;
+            if (!take && d == out.dist) {  // tie: the reference keeps the earlier visit
+                if (out.tri < 0) {
+                    take = true;
+                } else {
+                    if (out.rank == 0xFFFFFFFFu) out.rank = sc.tri_rank[out.tri];
+                    const uint32_t rank = sc.tri_rank[e.x];
+                    take = rank < out.rank;
+                    if (take) out.rank = rank;
+                }
+            } else if (take) {
+                out.rank = 0xFFFFFFFFu;  // visit ranks are loaded on a tie only
+            }
+            if (take) {
                 out.dist = d;
-                out.rank = rank;
                 out.tri = (int32_t)e.x;
                 best_t = t;
+                sh.nx = T[RT_T64_NORMAL];
+                sh.ny = T[RT_T64_NORMAL + 1];
+                sh.nz = T[RT_T64_NORMAL + 2];
+                const uint2 il = *reinterpret_cast<const RT_G uint2*>(T + RT_T64_IDLEAF);
+                sh.id = il.x;
+                leaf = il.y;
+                const RT_G float* B = reinterpret_cast<const RT_G float*>(T + RT_T64_BOX);
+#pragma unroll
+                for (int a = 0; a < 6; a++) lb[a] = B[a];
             }
         }
         if (cnt & kCandDropped) {
@@ -554,11 +578,8 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
         if (!redo && out.tri >= 0) {
             (void)hit_dist(ray, best_t, out.px, out.py, out.pz);
             // the reference must see the winner: re-verify its ancestor chain
-            const uint32_t leaf =
-                reinterpret_cast<const RT_G uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)out.tri + 9)->y;
             if (COUNT) n_chain++;
-            if (!chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, out.px, out.py, out.pz) &&
-                !chain_ok(sc, leaf, ray, n_chain_nodes))
+            if (!chain_fast_ok32(lb, ray, out.px, out.py, out.pz) && !chain_ok(sc, leaf, ray, n_chain_nodes))
                 redo = 2;
         }
     }
@@ -567,7 +588,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
             const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
             aux.redo[slot] = (uint32_t)o | (redo == 2u ? kRedoPass1 : 0u);
         } else {
-            shade_store(fp, sc, o, out, false);
+            shade_store(fp, o, out, sh, false);
         }
     }
     // hit count: block sums spread over RT_HIT_SLOTS counters (k_fixup adds

@@ -208,19 +208,20 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
                     if (!mt64(T, ray, t)) continue;
                     double hx, hy, hz;
                     const double d = hit_dist(ray, t, hx, hy, hz);
-                    const uint2 rl = *reinterpret_cast<const uint2*>(T + 9);  // {rank, leaf}
-                    if (!(d < best.dist || (d == best.dist && rl.x < best.rank))) continue;
+                    const uint32_t rank = sc.tri_rank[k];
+                    if (!(d < best.dist || (d == best.dist && rank < best.rank))) continue;
                     if (pass == 1) {
-                        if (rl.y != chain_leaf) {
+                        const uint32_t leaf = reinterpret_cast<const uint2*>(T + RT_T64_IDLEAF)->y;
+                        if (leaf != chain_leaf) {
                             if (COUNT) n_chain++;
-                            chain_leaf = rl.y;
-                            chain_res = chain_ok(sc, rl.y, ray, n_chain_nodes);
+                            chain_leaf = leaf;
+                            chain_res = chain_ok(sc, leaf, ray, n_chain_nodes);
                         }
                         if (!chain_res) continue;
                     }
                     best.dist = d;
                     best.t = t;
-                    best.rank = rl.x;
+                    best.rank = rank;
                     best.tri = (int32_t)k;
                     tcull = round_up_f((d + tslack) * (1.0 + 0x1p-20));
                 }
@@ -240,7 +241,8 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
         const Ray64 ray = gen_ray(fp, opaque(i), j);
         double hx, hy, hz;
         (void)hit_dist(ray, best.t, hx, hy, hz);
-        const uint32_t leaf = reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + 9)->y;
+        const uint32_t leaf =
+            reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + RT_T64_IDLEAF)->y;
         if (COUNT) n_chain++;
         if (chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz)) break;
         if (chain_ok(sc, leaf, ray, n_chain_nodes)) break;

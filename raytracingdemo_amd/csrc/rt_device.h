@@ -23,7 +23,17 @@
 #define RT_LEAF_FIRST_MASK 0x07FFFFFFu
 #define RT_LEAF_MAX_FIRST 0x07FFFFFFu
 #define RT_CHILD_REF 6       // u32 slot of the child ref in a 32-B child record
-#define RT_TRI64_DOUBLES 10  // v0, e1, e2 (9 doubles) + {u32 rank, u32 leaf}: 80 B
+// fp64 triangle record, one 128-B line in BVH order: everything k_resolve
+// needs for a candidate in one round trip.
+//   [0..8]   v0, e1, e2 (doubles)         Moller-Trumbore (triangle.hpp:42)
+//   [9..11]  normal (triangle.hpp:17)      shading
+//   [12]     {u32 loader id, u32 real leaf}
+//   [13..15] leaf box as 6 floats rounded inward (chain_fast_ok32)
+// The visit rank (ties only) stays in RtDevScene::tri_rank.
+#define RT_TRI64_DOUBLES 16
+#define RT_T64_NORMAL 9
+#define RT_T64_IDLEAF 12
+#define RT_T64_BOX 13
 // Work-queue block (RtLaunchAux::tile_ctr, RT_QUEUE_WORDS u32, zeroed per
 // launch): RT_QUEUES tile queues RT_QUEUE_STRIDE words apart (one per XCD,
 // separate cache lines), the redo-list length, and the hit-count partials.
@@ -57,7 +67,7 @@ static inline constexpr uint32_t rt_make_leaf(uint32_t first, uint32_t count) {
 struct RtDevScene {
     const RT_G uint8_t* nodes;
     const RT_G float* tri32;      // 12 floats per triangle: v0,e1,e2, max|e1|,max|e2|,max|v0|
-    const RT_G double* tri64;     // RT_TRI64_DOUBLES per triangle: v0,e1,e2,{rank,leaf}
+    const RT_G double* tri64;     // RT_TRI64_DOUBLES per triangle (layout above)
     const RT_G uint32_t* tri_id;
     const RT_G uint32_t* tri_rank;
     const RT_G uint32_t* tri_leaf;

@@ -550,7 +550,15 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     for (uint64_t i = 0; i < n; i++) {
         double* q = f.tri64.data() + i * RT_TRI64_DOUBLES;
         const uint32_t id = f.tri_id[i], leaf = f.tri_leaf[i];
-        for (int a = 0; a < 3; a++) q[RT_T64_NORMAL + a] = s.normal[(size_t)id * 3 + a];
+        // shadeScreen's normal.normalize() (main.cpp:361, vector3.hpp), done
+        // once here with the same IEEE operations the kernel would run
+        double nx = s.normal[(size_t)id * 3], ny = s.normal[(size_t)id * 3 + 1], nz = s.normal[(size_t)id * 3 + 2];
+        const double nl = std::sqrt(nx * nx + ny * ny + nz * nz);
+        if (nl > 0.0) {
+            const double inv = 1.0 / nl;
+            nx = nx * inv; ny = ny * inv; nz = nz * inv;
+        }
+        q[RT_T64_NORMAL] = nx; q[RT_T64_NORMAL + 1] = ny; q[RT_T64_NORMAL + 2] = nz;
         uint32_t* w = reinterpret_cast<uint32_t*>(q + RT_T64_IDLEAF);
         w[0] = id;
         w[1] = leaf;

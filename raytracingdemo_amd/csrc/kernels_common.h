@@ -178,6 +178,9 @@ __device__ __forceinline__ double pixel_y(const RtFrameParams& fp, int y) {
 }
 
 // main.cpp:332-337: d = dir + up*py + right*px; d *= 1/|d|; Ray{pos, d}
+// INV: also the reciprocal direction (slab tests); k_resolve adds it only
+// when it falls back to the chain walk (with_inv).
+template <bool INV = true>
 __device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) {
     const double px = pixel_x(fp, i), py = pixel_y(fp, j);
     double dx = (fp.dir[0] + fp.up[0] * py) + fp.right[0] * px;
@@ -194,10 +197,21 @@ __device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) 
     r.dx = dx;
     r.dy = dy;
     r.dz = dz;
+    if (INV) {
+        const double inf = __builtin_huge_val();
+        r.ix = dx != 0.0 ? 1.0 / dx : inf;
+        r.iy = dy != 0.0 ? 1.0 / dy : inf;
+        r.iz = dz != 0.0 ? 1.0 / dz : inf;
+    } else {
+        r.ix = r.iy = r.iz = 0.0;
+    }
+    return r;
+}
+__device__ __forceinline__ Ray64 with_inv(Ray64 r) {
     const double inf = __builtin_huge_val();
-    r.ix = dx != 0.0 ? 1.0 / dx : inf;
-    r.iy = dy != 0.0 ? 1.0 / dy : inf;
-    r.iz = dz != 0.0 ? 1.0 / dz : inf;
+    r.ix = r.dx != 0.0 ? 1.0 / r.dx : inf;
+    r.iy = r.dy != 0.0 ? 1.0 / r.dy : inf;
+    r.iz = r.dz != 0.0 ? 1.0 / r.dz : inf;
     return r;
 }
 
@@ -241,14 +255,14 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, size_t o, c
                                             bool count_hit = true) {
     uint8_t c0 = 0, c1 = 0, c2 = 0;
     if (b.tri >= 0 && fp.rgb) {
-        double nx = sh.nx, ny = sh.ny, nz = sh.nz;
-        const double nl = __builtin_sqrt(nx * nx + ny * ny + nz * nz);
-        if (nl > 0.0) {
-            const double s = 1.0 / nl;
-            nx = nx * s; ny = ny * s; nz = nz * s;
-        }
+        // the record holds the normal already normalised as shadeScreen does
+        // it (main.cpp:361; bvh_build.cpp flatten, same IEEE operations)
+        const double nx = sh.nx, ny = sh.ny, nz = sh.nz;
         double lx = fp.pos[0] - b.px, ly = fp.pos[1] - b.py, lz = fp.pos[2] - b.pz;
-        const double dist = __builtin_sqrt(lx * lx + ly * ly + lz * lz);
+        // the light sits at the ray origin, so |light - p| is bit-for-bit the
+        // hit distance hit_dist returned ((o - p) = -(p - o) exactly, same
+        // sum order): reuse it instead of a second fp64 sqrt
+        const double dist = b.dist;
         if (dist > 0.0) {
             const double s = 1.0 / dist;
             lx = lx * s; ly = ly * s; lz = lz * s;

@@ -30,7 +30,12 @@
 #pragma once
 
 // Tile scheduling of the packet kernel: 0 one device-wide queue, 1 one queue
-// per XCD (default), 2 static round-robin (diagnostic).
+// per XCD over interleaved tile columns (default), 2 static round-robin
+// (diagnostic), 3 one queue per XCD over a contiguous band of tile rows (the
+// XCD's L2 holds its band's subtrees), stealing from the other bands once
+// its own is drained.  4 = 1 with the tile index scattered by a
+// multiplicative permutation (t * P mod tiles): the tiles in flight at any
+// moment are spread over the whole image instead of a band of ~30 tile rows.
 #ifndef RT_TILE_SCHED
 #define RT_TILE_SCHED 1
 #endif
@@ -39,6 +44,9 @@
 // deltas accumulated over the whole persistent loop and flushed once per wave
 // into aux.diag[0..7]: node-load wait, node work, leaves, stack pops, ray
 // set-up, exact resolve, output stores, tile fetch.
+#if defined(RT_DIAG_TILECOST) && RT_DIAG_TILECOST >= 2 && !defined(RT_DIAG_TIMING)
+#define RT_DIAG_TIMING 1  // per-tile cycle split (tools/tile_costs.py)
+#endif
 #ifdef RT_DIAG_TIMING
 #define RT_TSTAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define RT_TACC(slot, t0) (tacc[slot] += __builtin_amdgcn_s_memtime() - (t0))
@@ -65,6 +73,23 @@
 #endif
 #ifndef RT_TILE_PREFETCH
 #define RT_TILE_PREFETCH 0
+#endif
+
+// L2 prefetch of pushed children (their records are fetched when popped,
+// many steps later): 0 off, 1 first 128-B line, 2 both lines.  One vector
+// load per pushed child whose value is consumed at the next push, so its
+// wait lands a whole step later.  (A no-return atomic add of 0 as the
+// prefetch measured 3.6x slower.)
+#ifndef RT_PREFETCH
+#define RT_PREFETCH 0
+#endif
+
+// Tail shortening: a wave that has spent RT_PRIO_STEPS loop steps on its tile
+// raises its issue priority (s_setprio 1, 2 at twice, 3 at three times
+// that), so the long tiles that set the kernel's end get the SIMD first and
+// the cheap tiles fill in around them.  0 = off.
+#ifndef RT_PRIO_STEPS
+#define RT_PRIO_STEPS 0
 #endif
 
 // Node record fetch: 0 scalar loads (default), 1 uniform vector loads.
@@ -290,6 +315,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
     const f2 nox{-olx, -ohx}, noy{-oly, -ohy}, noz{-olz, -ohz};
 
     uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0, w_tris = 0;  // COUNT only
+#if RT_PREFETCH
+    uint32_t pf_sink = 0, pf_val = 0, pf_val2 = 0;  // L2 prefetch loads (values unused)
+#endif
     float tcull = valid ? __builtin_huge_valf() : -1.f;
     int nc = 0;         // candidates in the lane's list
     float drop = __builtin_huge_valf();  // smallest t lower bound of a dropped candidate
@@ -307,7 +335,16 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
     }
     int sp = 0;
     RT_TACC(4, t_setup);
+#if RT_PRIO_STEPS
+    uint32_t steps = 0;
+#endif
     for (;;) {
+#if RT_PRIO_STEPS
+        steps++;
+        if (steps == RT_PRIO_STEPS) __builtin_amdgcn_s_setprio(1);
+        if (steps == 2 * RT_PRIO_STEPS) __builtin_amdgcn_s_setprio(2);
+        if (steps == 3 * RT_PRIO_STEPS) __builtin_amdgcn_s_setprio(3);
+#endif
         if (cur != RT_INVALID_REF) {
             if (!(cur & RT_LEAF_BIT)) {
                 RT_TSTAMP(t_n0);
@@ -386,7 +423,19 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
                         const uint32_t below = pm & ((1u << (lane & 31)) - 1u);
                         const uint32_t above = (pm >> (lane & 31)) >> 1;
                         const int slot = (int)__builtin_popcount(rev ? below : above);
-                        if ((pm >> (lane & 31)) & 1u & (lane < W)) wstack[sp + slot] = refv;
+                        if ((pm >> (lane & 31)) & 1u & (lane < W)) {
+                            wstack[sp + slot] = refv;
+#if RT_PREFETCH
+                            const RT_G uint8_t* pa =
+                                (refv & RT_LEAF_BIT)
+                                    ? (const RT_G uint8_t*)(tri32 + 12 * (size_t)(refv & RT_LEAF_FIRST_MASK))
+                                    : nodes + (size_t)refv * (32 * W);
+                            // consume the previous push's prefetch (long returned), issue this one
+                            pf_sink ^= pf_val ^ pf_val2;
+                            pf_val = *(const RT_G uint32_t*)pa;
+                            if (RT_PREFETCH >= 2) pf_val2 = *(const RT_G uint32_t*)(pa + 128);
+#endif
+                        }
                         sp += __builtin_popcount(pm);
                     }
                     cur = (uint32_t)__builtin_amdgcn_readlane((int)refv, near_c);
@@ -447,7 +496,12 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
             }
         }
         RT_TSTAMP(t_p0);
-        if (sp == 0) break;
+        if (sp == 0) {
+#if RT_PRIO_STEPS
+            if (steps >= RT_PRIO_STEPS) __builtin_amdgcn_s_setprio(0);
+#endif
+            break;
+        }
         sp--;
         cur = uni(wstack[sp]);
 #ifdef RT_DIAG_TIMING
@@ -456,6 +510,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
         RT_TACC(3, t_p0);
     }
     RT_TSTAMP(t_r0);
+#if RT_PREFETCH
+    asm volatile("" ::"v"(pf_sink ^ pf_val ^ pf_val2));  // keeps the prefetch loads
+#endif
     A = launder(A);
     const RtFrameParams fp = kload(&A->fp);
     if (COUNT && fp.counters && lane == 0) {
@@ -525,7 +582,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
     const uint32_t nlist = cnt & ~kCandDropped;
     Shade sh{0.0, 0.0, 0.0, RT_INVALID_REF};
     if (cnt != 0) {
-        const Ray64 ray = gen_ray(fp, i, fp.row0 + r * fp.row_stride);
+        const Ray64 ray = gen_ray<false>(fp, i, fp.row0 + r * fp.row_stride);
         double best_t = 0.0;
         uint32_t leaf = 0;
         float lb[6];
@@ -579,7 +636,8 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
             (void)hit_dist(ray, best_t, out.px, out.py, out.pz);
             // the reference must see the winner: re-verify its ancestor chain
             if (COUNT) n_chain++;
-            if (!chain_fast_ok32(lb, ray, out.px, out.py, out.pz) && !chain_ok(sc, leaf, ray, n_chain_nodes))
+            if (!chain_fast_ok32(lb, ray, out.px, out.py, out.pz) &&
+                !chain_ok(sc, leaf, with_inv(ray), n_chain_nodes))
                 redo = 2;
         }
     }
@@ -646,8 +704,15 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
     // round-robin, so block b's XCD is b % 8): queue x hands out tiles
     // x, x + 8, x + 16, ...; every queue is drained by the blocks b = x mod 8.
     const uint32_t xq = blockIdx.x % RT_QUEUES;
+    bool first = true;
+    // waves drained through queue xq: 4 per block b = xq (mod 8)
+    const uint32_t nwx = 4u * ((gridDim.x + RT_QUEUES - 1 - xq) / RT_QUEUES);
+    (void)first;
+    (void)nwx;
 #if RT_TILE_SCHED == 2
     uint32_t iter = 0;  // diagnostic: static round-robin, no atomics
+#elif RT_TILE_SCHED == 3
+    uint32_t drained = 0;  // bands this wave found empty (bit per queue)
 #endif
     // The next tile index is fetched one tile ahead, so the queue atomic's
     // round trip overlaps the current tile's walk.
@@ -655,8 +720,36 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
         int t = 0;
 #if RT_TILE_SCHED == 0
         if (lane == 0) t = (int)atomicAdd(kload(&A->aux.tile_ctr), 1u);
-#elif RT_TILE_SCHED == 1
-        if (lane == 0) t = (int)(xq + RT_QUEUES * atomicAdd(kload(&A->aux.tile_ctr) + xq * RT_QUEUE_STRIDE, 1u));
+#elif RT_TILE_SCHED == 1 || RT_TILE_SCHED == 4 || RT_TILE_SCHED == 5
+        // a wave's first tile is its own slot in the queue (no atomic: the
+        // whole grid starting at once would serialise on the 8 counters for
+        // ~10 us); the counter hands out the slots after the XCD's waves
+        if (first) {
+            first = false;
+            t = (int)(xq + RT_QUEUES * ((blockIdx.x / RT_QUEUES) * 4 + wv));
+        } else if (lane == 0) {
+            t = (int)(xq + RT_QUEUES * (nwx + atomicAdd(kload(&A->aux.tile_ctr) + xq * RT_QUEUE_STRIDE, 1u)));
+        }
+#elif RT_TILE_SCHED == 3
+        {
+            const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
+            const uint32_t tiles = (uint32_t)(((W_ + 7) >> 3) * ((nrows + 7) >> 3));
+            t = (int)tiles;
+            for (uint32_t k = 0; k < RT_QUEUES; k++) {
+                const uint32_t x = (xq + k) & (RT_QUEUES - 1);
+                if ((drained >> x) & 1u) continue;
+                const uint32_t b0 = (uint32_t)((uint64_t)tiles * x / RT_QUEUES);
+                const uint32_t b1 = (uint32_t)((uint64_t)tiles * (x + 1) / RT_QUEUES);
+                uint32_t c = 0;
+                if (lane == 0) c = atomicAdd(kload(&A->aux.tile_ctr) + x * RT_QUEUE_STRIDE, 1u);
+                c = (uint32_t)__shfl((int)c, 0);
+                if (b0 + c < b1) {
+                    t = (int)(b0 + c);
+                    break;
+                }
+                drained |= 1u << x;
+            }
+        }
 #else
         t = (int)((blockIdx.x * 4 + wv) + iter++ * gridDim.x * 4);
 #endif
@@ -670,7 +763,16 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
         const int tiles = tiles_x * ((nrows + 7) >> 3);
         RT_TSTAMP(t_q0);
         if (!RT_TILE_PREFETCH) next = fetch();
-        const int tile = __shfl(next, 0);
+        int tile = __shfl(next, 0);
+#if RT_TILE_SCHED == 5
+        if (tile < tiles) tile = tiles - 1 - tile;  // diagnostic: bottom rows first
+#endif
+#if RT_TILE_SCHED == 4
+        if (tile < tiles) {
+            const uint32_t P = (tiles % 7919) ? 7919u : 7927u;  // primes: coprime to tiles
+            tile = (int)(((uint64_t)(uint32_t)tile * P) % (uint32_t)tiles);
+        }
+#endif
 #ifdef RT_DIAG_TIMING
         asm volatile("" ::"v"(tile));
 #endif
@@ -685,13 +787,22 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
 #if defined(RT_DIAG_HIST) || defined(RT_DIAG_TILECOST)
         const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef RT_DIAG_TILECOST
+        uint64_t tb[6];
+        for (int k = 0; k < 6; k++) tb[k] = tacc[k];
+#endif
         trace_packet<W, SP, K, COUNT>(A, i, r, i < W_ && r < nrows, stacks[wv], cands[wv], tacc);
 #ifdef RT_DIAG_TILECOST
         {   // per-tile duration (10-ns ticks) into hit_pos[3 * tile] (diagnostic build:
-            // shade_store leaves hit_pos alone)
+            // shade_store leaves hit_pos alone), and the tile's cycle split
+            // (s_memtime) into hit_pos[3 * tiles + 8 * tile + k]
             const uint64_t dt = __builtin_amdgcn_s_memrealtime() - th0;
             RT_G double* hp = kload(&A->fp.hit_pos);
-            if (hp && lane == 0) hp[3 * (size_t)tile] = (double)dt;
+            if (hp && lane == 0) {
+                hp[3 * (size_t)tile] = (double)dt;
+                for (int k = 0; k < 6; k++) hp[3 * (size_t)tiles + 8 * (size_t)tile + k] = (double)(tacc[k] - tb[k]);
+                hp[3 * (size_t)tiles + 8 * (size_t)tile + 6] = (double)th0;  // start (10-ns ticks)
+            }
         }
 #endif
 #ifdef RT_DIAG_HIST

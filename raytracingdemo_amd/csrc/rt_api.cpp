@@ -199,7 +199,12 @@ void upload_one(rt_scene* s, int device) {
     HIP_TRY(hipEventCreate(&r.ev1));
     HIP_TRY(hipEventCreateWithFlags(&r.ev_in, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&r.ev_out, hipEventDisableTiming));
-    r.grid = prop.multiProcessorCount * rt::exact_blocks_per_cu(f.width, f.stack_bound);
+    int bpc = rt::exact_blocks_per_cu(f.width, f.stack_bound);
+    if (const char* e = std::getenv("RT_BLOCKS_PER_CU")) {  // diagnostic: lower the persistent grid
+        const int v = std::atoi(e);
+        if (v >= 1 && v < bpc) bpc = v;
+    }
+    r.grid = prop.multiProcessorCount * bpc;
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
     HIP_TRY(hipMalloc(&r.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));

@@ -26,7 +26,7 @@
 // fp64 triangle record, one 128-B line in BVH order: everything k_resolve
 // needs for a candidate in one round trip.
 //   [0..8]   v0, e1, e2 (doubles)         Moller-Trumbore (triangle.hpp:42)
-//   [9..11]  normal (triangle.hpp:17)      shading
+//   [9..11]  unit normal (triangle.hpp:17, normalised as main.cpp:361 does)
 //   [12]     {u32 loader id, u32 real leaf}
 //   [13..15] leaf box as 6 floats rounded inward (chain_fast_ok32)
 // The visit rank (ties only) stays in RtDevScene::tri_rank.

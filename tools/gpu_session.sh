@@ -37,6 +37,7 @@ for s in $STEPS; do
         list)  run list 120 rocprofv3 -L ;;
         waves) for w in 3 4 5; do RT_WAVES=$w run bench_w$w 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
         quick) run bench_quick 300 python bench.py --no-cpu --steps 5 ;;
+        occ)   for b in 3 4 5 6; do RT_BLOCKS_PER_CU=$b run bench_b$b 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
         notime) RT_BENCH_NO_KTIMING=1 run bench_notime 300 python bench.py --no-cpu --steps 5 ;;
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}" 300 \
@@ -46,7 +47,8 @@ for s in $STEPS; do
         sq)    for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
                            "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD" \
                            "SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_TC_DATA_READ_REQ SQC_TC_STALL SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
-                           "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
+                           "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" \
+                           "SQC_DCACHE_MISSES_DUPLICATE SQC_DCACHE_REQ_READ_16 SQC_DCACHE_REQ_READ_8 SQC_DCACHE_REQ_READ_4 TCC_TAG_STALL_sum TCC_LATENCY_FIFO_FULL_sum"; do
                    n=$((${n:-0}+1))
                    run sq$n 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$n \
                        -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu || exit 1

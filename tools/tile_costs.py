@@ -37,7 +37,7 @@ def main():
     ids = torch.empty(W * H, dtype=torch.int32, device="cuda:0")
     hp = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda:0")
     st = torch.cuda.current_stream()
-    costs = []
+    costs, split = [], []
     for rep in range(2):
         for f in range(36):
             pos, d = path.circular_path(f)
@@ -46,9 +46,22 @@ def main():
             torch.cuda.synchronize()
             if rep == 1:
                 costs.append(hp[0:3 * tx * ty].cpu().numpy().reshape(-1, 3).copy())
+                split.append(hp[3 * tx * ty:11 * tx * ty].cpu().numpy().reshape(-1, 8)[:, :6].copy())
     A = np.stack(costs)  # [36, tiles, 3]: 10-ns ticks, nodes + 1e6 leaves, triangles
+    S = np.stack(split)  # [36, tiles, 6]: s_memtime split (node wait, node work, leaves, pops, setup, out)
+    names = ["node-wait", "node-work", "leaves", "pops", "setup", "out"]
+    for f in (0, 12, 30):
+        top = np.argsort(-A[f, :, 0])[:100]
+        for label, sel in (("all", slice(None)), ("top100", top)):
+            sp = S[f][sel].mean(axis=0)
+            nodes = (A[f][sel, 1] % 1e6).mean()
+            leaves = (A[f][sel, 1] // 1e6).mean()
+            tris = A[f][sel, 2].mean()
+            print(f"f{f:2d} {label:7s} us {A[f][sel, 0].mean() / 100:6.1f} nodes {nodes:5.1f} leaves {leaves:5.1f} "
+                  f"tris {tris:5.1f} | " + " ".join(f"{n} {v:8.0f}" for n, v in zip(names, sp)) +
+                  f" | per-node wait {sp[0] / max(nodes, 1):6.0f} per-tri {sp[2] / max(tris, 1):6.0f}")
     C = A[:, :, 0]
-    np.savez_compressed("gpurun_out/tile_costs.npz", costs=C, visits=A[:, :, 1], tris=A[:, :, 2], tx=tx, ty=ty)
+    np.savez_compressed("gpurun_out/tile_costs.npz", costs=C, visits=A[:, :, 1], tris=A[:, :, 2], split=S, tx=tx, ty=ty)
     P = 7168
     print("tiles", tx * ty, "mean tile us", C.mean() / 100, "p99", np.percentile(C, 99) / 100)
     print("frame sum/P (ideal) vs row-major vs LPT-oracle vs prev-frame vs prev-frame shifted (us):")

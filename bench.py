@@ -115,22 +115,26 @@ def main():
     ids = torch.empty((F, rows, W), dtype=torch.int32, device=dev)
     rgb = torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev)
     cnt = torch.zeros((F,), dtype=torch.int64, device=dev)
+    # the library writes frame f at f * W * my_rows: a short shard renders
+    # into contiguous buffers and is copied into the padded gather layout
+    padded = my_rows != rows
+    r_ids = torch.empty((F, my_rows, W), dtype=torch.int32, device=dev) if padded else ids
+    r_rgb = torch.zeros((F, my_rows, W, 3), dtype=torch.uint8, device=dev) if padded else rgb
     gather_ids = [torch.empty_like(ids) for _ in range(world)] if (world > 1 and rank == 0) else None
     gather_rgb = [torch.empty_like(rgb) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev)
     mode = a.mode
 
-    def render_step(events=None, ktiming=True):
+    def render_step(timing=False, count=False):
+        # the whole camera orbit in one batched call (the library launches up
+        # to 12 frames per traversal / resolve / fix-up launch)
         cnt.zero_()
-        for f, (pos, d) in enumerate(cams):
-            if events is not None:
-                events[f][0].record(stream)
-            scene.render_rows_device(local, pos, d, W, H, rank, world, my_rows, hit_id=ids[f].data_ptr(),
-                                     rgb=rgb[f].data_ptr(), hit_count=cnt[f:f + 1].data_ptr(),
-                                     stream=stream.cuda_stream, mode=mode,
-                                     timing=events is not None and ktiming)
-            if events is not None:
-                events[f][1].record(stream)
+        scene.render_batch_device(local, cams, W, H, rank, world, my_rows, hit_id=r_ids.data_ptr(),
+                                  rgb=r_rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
+                                  mode=mode, timing=timing, count=count)
+        if padded:
+            ids[:, :my_rows] = r_ids
+            rgb[:, :my_rows] = r_rgb
         if world > 1:
             dist.gather(ids, gather_ids, dst=0)
             dist.gather(rgb, gather_rgb, dst=0)
@@ -138,22 +142,16 @@ def main():
                 return deinterleave(torch.stack(gather_rgb), H)
         return rgb
 
-    # exactness check of the headline workload (outside timing): frame 0 vs
-    # a full-frame render through the single-GPU path on this rank
     # warm-up with kernel timing on, so the library's per-launch timing events
     # exist before the timed region (they are recycled, not re-created)
-    warm_events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
+    ktiming = not os.environ.get("RT_BENCH_NO_KTIMING")
     for _ in range(a.warmup):
-        render_step(warm_events)
+        render_step(timing=ktiming)
     torch.cuda.synchronize(dev)
     scene.frame_stats(local, reset=True)
 
     # counting pass for algorithmic bytes (outside the timed region)
-    scene.frame_stats(local, reset=True)
-    for f, (pos, d) in enumerate(cams):
-        scene.render_rows_device(local, pos, d, W, H, rank, world, my_rows, hit_id=ids[f].data_ptr(),
-                                 rgb=rgb[f].data_ptr(), hit_count=cnt[f:f + 1].data_ptr(),
-                                 stream=stream.cuda_stream, mode=mode, count=True)
+    render_step(count=True)
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
     nb = st["node_bytes"]
@@ -169,18 +167,14 @@ def main():
     else:  # per-lane kernel: each ray fetches its own records
         trace_bytes = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
                        cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * OUT_BYTES)
-    alg_bytes_per_launch = trace_bytes / F
+    alg_bytes_per_frame = trace_bytes / F
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(F)]
-    kernel_ms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        render_step(events, ktiming=not os.environ.get("RT_BENCH_NO_KTIMING"))
-        torch.cuda.synchronize(dev)  # needed to read this step's events; also part of the step
-        kernel_ms.extend(e0.elapsed_time(e1) for e0, e1 in events)
+        render_step(timing=ktiming)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -198,12 +192,18 @@ def main():
     total_rays = a.steps * F * W * H
     value = total_rays / elapsed / 1e6
     launches_timed = max(ks["timed_launches"], 1)
-    # dominant (traversal) kernel; without library timing, the whole frame
-    avg_kernel_s = (ks["trace_ms"] / launches_timed if ks["timed_launches"] else float(np.mean(kernel_ms))) * 1e-3
+    frames_timed = a.steps * F
+    frame_s = elapsed / frames_timed
+    # dominant (traversal) kernel, HIP events around each of its launches
+    # (one launch = up to 12 frames); without library timing, whole frames
+    trace_s = ks["trace_ms"] * 1e-3 if ks["timed_launches"] else elapsed
+    avg_kernel_s = trace_s / launches_timed if ks["timed_launches"] else frame_s
+    frames_per_launch = frames_timed / launches_timed if ks["timed_launches"] else 1.0
+    alg_bytes_per_launch = alg_bytes_per_frame * frames_per_launch
     achieved = alg_bytes_per_launch / avg_kernel_s / 1e9
 
     if rank == 0:
-        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}"
+        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}|fpl{frames_per_launch:g}"
         if a.key_out:
             with open(a.key_out, "w") as fh:
                 fh.write(key + "\n")
@@ -232,7 +232,10 @@ def main():
                          "kernel": "k_trace_packet" if cs["wave_tiles"] else "k_trace_exact",
                          "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(alg_bytes_per_launch),
-                         "frame_ms_avg": round(float(np.mean(kernel_ms)), 4),
+                         "frames_per_launch": round(frames_per_launch, 3),
+                         "alg_bytes_per_frame": int(alg_bytes_per_frame),
+                         "trace_ms_per_frame": round(trace_s / frames_timed * 1e3, 4),
+                         "frame_ms_avg": round(frame_s * 1e3, 4),
                          "survey_bytes_per_ray": round(survey_bytes_per_ray, 1),
                          "per_ray": {"node_fetches": round(cs["node_fetches"] / max(cs["rays"], 1), 3),
                                      "tri_prefilter": round(cs["tri_prefilter"] / max(cs["rays"], 1), 3),

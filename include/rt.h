@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* status codes */
 #define RT_OK 0
@@ -158,6 +158,19 @@ int rt_render_frame(rt_scene *s, const rt_camera *cam, int mode, rt_frame_out *o
  * flags: RT_FLAG_COUNT accumulates into the scene's per-device counters. */
 int rt_render_rows_device(rt_scene *s, int device, const rt_camera *cam, int mode, int row0, int row_stride,
                           int nrows, const rt_device_out *out, void *stream, uint32_t flags);
+
+/* A batch of nframes camera poses of one image geometry (all cams share
+ * width/height), rendered as rt_render_rows_device would render each of them
+ * in turn (the reference's runTest loop over its camera path, main.cpp:234-281,
+ * with calculateScreen + shadeScreen per pose, main.cpp:253-262).  Frame f's
+ * outputs start f * width * nrows pixels into every buffer of `out` (rgb and
+ * pos: 3 values per pixel), and its hit counter is out->hit_count[f].  The
+ * library launches up to 12 frames at a time (one persistent traversal launch,
+ * one resolve launch, one fix-up launch), so per-launch ramp-up, tail and
+ * launch gaps are paid once per batch.  Results are identical to per-frame
+ * calls. */
+int rt_render_batch_device(rt_scene *s, int device, const rt_camera *cams, int nframes, int mode, int row0,
+                           int row_stride, int nrows, const rt_device_out *out, void *stream, uint32_t flags);
 
 /* Read (and optionally reset) the per-device counters filled by
  * RT_FLAG_COUNT renders (synchronises the device). */

@@ -181,19 +181,19 @@ __device__ __forceinline__ double pixel_y(const RtFrameParams& fp, int y) {
 // INV: also the reciprocal direction (slab tests); k_resolve adds it only
 // when it falls back to the chain walk (with_inv).
 template <bool INV = true>
-__device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, int i, int j) {
+__device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, const RtFrameCam& cam, int i, int j) {
     const double px = pixel_x(fp, i), py = pixel_y(fp, j);
-    double dx = (fp.dir[0] + fp.up[0] * py) + fp.right[0] * px;
-    double dy = (fp.dir[1] + fp.up[1] * py) + fp.right[1] * px;
-    double dz = (fp.dir[2] + fp.up[2] * py) + fp.right[2] * px;
+    double dx = (cam.dir[0] + cam.up[0] * py) + cam.right[0] * px;
+    double dy = (cam.dir[1] + cam.up[1] * py) + cam.right[1] * px;
+    double dz = (cam.dir[2] + cam.up[2] * py) + cam.right[2] * px;
     const double s = 1.0 / __builtin_sqrt(dx * dx + dy * dy + dz * dz);
     dx = dx * s;
     dy = dy * s;
     dz = dz * s;
     Ray64 r;
-    r.ox = fp.pos[0];
-    r.oy = fp.pos[1];
-    r.oz = fp.pos[2];
+    r.ox = cam.pos[0];
+    r.oy = cam.pos[1];
+    r.oz = cam.pos[2];
     r.dx = dx;
     r.dy = dy;
     r.dz = dz;
@@ -251,14 +251,19 @@ __device__ __forceinline__ Shade shade_of(const RtDevScene& sc, int32_t tri) {
     }
     return s;
 }
-__device__ __forceinline__ void shade_store(const RtFrameParams& fp, size_t o, const Best& b, const Shade& sh,
-                                            bool count_hit = true) {
+// Output slot of pixel o (row-major in the shard) of frame f of the launch.
+__device__ __forceinline__ size_t out_index(const RtFrameParams& fp, int f, size_t o) {
+    return (size_t)f * ((size_t)fp.W * (size_t)fp.nrows) + o;
+}
+__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtFrameCam& cam, int f, size_t o,
+                                            const Best& b, const Shade& sh, bool count_hit = true) {
+    o = out_index(fp, f, o);
     uint8_t c0 = 0, c1 = 0, c2 = 0;
     if (b.tri >= 0 && fp.rgb) {
         // the record holds the normal already normalised as shadeScreen does
         // it (main.cpp:361; bvh_build.cpp flatten, same IEEE operations)
         const double nx = sh.nx, ny = sh.ny, nz = sh.nz;
-        double lx = fp.pos[0] - b.px, ly = fp.pos[1] - b.py, lz = fp.pos[2] - b.pz;
+        double lx = cam.pos[0] - b.px, ly = cam.pos[1] - b.py, lz = cam.pos[2] - b.pz;
         // the light sits at the ray origin, so |light - p| is bit-for-bit the
         // hit distance hit_dist returned ((o - p) = -(p - o) exactly, same
         // sum order): reuse it instead of a second fp64 sqrt
@@ -292,12 +297,12 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, size_t o, c
         const uint64_t hits = __ballot(b.tri >= 0);
         const uint64_t act = __ballot(1);
         if (hits != 0 && (int)(threadIdx.x & 63) == __builtin_ctzll(act))
-            atomicAdd(fp.hit_count, (unsigned long long)__builtin_popcountll(hits));
+            atomicAdd(fp.hit_count + f, (unsigned long long)__builtin_popcountll(hits));
     }
 }
-__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtDevScene& sc, size_t o, const Best& b,
-                                            bool count_hit = true) {
-    shade_store(fp, o, b, shade_of(sc, b.tri), count_hit);
+__device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtFrameCam& cam, int f,
+                                            const RtDevScene& sc, size_t o, const Best& b, bool count_hit = true) {
+    shade_store(fp, cam, f, o, b, shade_of(sc, b.tri), count_hit);
 }
 
 template <int W>

@@ -175,6 +175,13 @@ __device__ __forceinline__ uint32_t lanes_of(const ChildRec (&ch)[W]) {
 constexpr uint32_t kRedoPass1 = 0x80000000u;
 constexpr int kLeafChunk = 4;  // triangle records fetched per scalar round trip
 constexpr uint32_t kCandDropped = 0x80;  // cand_cnt flag: candidates were dropped (bound in cand_drop)
+constexpr uint32_t kCandSpilled = 0x40;  // cand_cnt flag: entries in the HBM overflow slots
+constexpr uint32_t kCandCount = 0x3F;    // cand_cnt: entries in slots [0, count)
+// A lane whose LDS list (K entries) is full appends further candidates
+// straight to its pixel's HBM overflow slots [K, K + kCandSpill) (terminated
+// by a tri = ~0 entry when not full); only past those is a candidate dropped
+// (certified by the dropped bound, else the pixel is redone exactly).
+constexpr int kCandSpill = RT_CAND_SLOTS - RT_CAND_LDS;
 static_assert(kLeafChunk == RT_TRI32_PAD, "tri32 padding must cover a leaf chunk");
 
 // Forces uniform values to be materialised (their loads waited on) here, so
@@ -286,7 +293,7 @@ __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32&
 }
 
 template <int W, int SP, int K, bool COUNT>
-__device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid, uint32_t* __restrict__ wstack,
+__device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool valid, uint32_t* __restrict__ wstack,
                                              uint2* __restrict__ cand, uint64_t* tacc) {
     const int lane = threadIdx.x & 63;
     RT_TSTAMP(t_setup);
@@ -294,12 +301,16 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
     Ray32 q;
     float tsl;  // distance slack (see trace_exact), fp32 rounded up
     float pd;
+    uint32_t ob;
     {
         const RtFrameParams fp = kload(&A->fp);
-        const Ray64 ray = gen_ray(fp, i, fp.row0 + r * fp.row_stride);
-        q = make_ray32(ray, fp.pad);
+        const RtFrameCam cam = kload(&A->fp.cam[f]);  // this tile's frame
+        const Ray64 ray = gen_ray(fp, cam, i, fp.row0 + r * fp.row_stride);
+        q = make_ray32(ray, cam.pad);
         tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
-        pd = fp.pad;
+        pd = cam.pad;
+        // the lane's pixel in the batch (< 2^31, host-checked)
+        ob = (uint32_t)out_index(fp, f, (size_t)r * fp.W + i);
     }
     // direction sign bits (x, y, z) of lane 0's ray: the tile's ordering key
     const uint32_t lsg = (q.ix < 0.f ? 1u : 0u) | (q.iy < 0.f ? 2u : 0u) | (q.iz < 0.f ? 4u : 0u);
@@ -320,6 +331,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
 #endif
     float tcull = valid ? __builtin_huge_valf() : -1.f;
     int nc = 0;         // candidates in the lane's list
+    int nsp = 0;        // candidates in the pixel's HBM overflow slots
     float drop = __builtin_huge_valf();  // smallest t lower bound of a dropped candidate
     uint32_t cur = kword(&A->sc.root_ref);
     {
@@ -483,6 +495,14 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
                             if (nc < K) {
                                 cand[nc * 64 + lane] = make_uint2(k, __float_as_uint(tl));
                                 nc++;
+                            } else if (nsp < kCandSpill) {
+                                // LDS list full: append to the pixel's HBM overflow slots
+                                const args_p A2 = launder(A);  // (A itself stays uniform)
+                                const size_t np = (size_t)kword(&A2->fp.W) * kword(&A2->fp.nrows) *
+                                                  kword(&A2->fp.nframes);
+                                RT_G uint2* const hc = reinterpret_cast<RT_G uint2*>(kload(&A2->aux.cand));
+                                hc[(size_t)(K + nsp) * np + ob] = make_uint2(k, __float_as_uint(tl));
+                                nsp++;
                             } else {
                                 // full: keep the K smallest lower bounds, remember the
                                 // smallest bound dropped (k_resolve certifies the winner
@@ -533,10 +553,11 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
 #endif
     if (!valid) return;
     // hand the lane's surviving candidates to k_resolve: count per pixel,
-    // entry c of pixel o at cand[c * npix + o] (coalesced across a row)
+    // entry c of batch pixel o at cand[c * npix + o] (coalesced across a row;
+    // frame f's pixels follow frame f-1's)
     const RtLaunchAux aux = kload(&A->aux);
-    const size_t o = (size_t)r * fp.W + i;
-    const size_t npix = (size_t)fp.W * fp.nrows;
+    const size_t o = ob;
+    const size_t npix = (size_t)fp.W * fp.nrows * fp.nframes;
     uint32_t m = 0;
     for (int c = 0; c < nc; c++) {
         const uint2 e = cand[c * 64 + lane];
@@ -546,7 +567,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int i, int r, bool valid,
     }
     const bool dropped = drop < __builtin_huge_valf() && drop <= tcull;  // a dropped candidate could still win
     if (dropped) aux.cand_drop[o] = drop;
-    aux.cand_cnt[o] = (uint8_t)(m | (dropped ? kCandDropped : 0u));
+    if (nsp > 0 && nsp < kCandSpill)  // terminate the overflow slots
+        reinterpret_cast<RT_G uint2*>(aux.cand)[(size_t)(K + nsp) * npix + o] = make_uint2(~0u, 0u);
+    aux.cand_cnt[o] = (uint8_t)(m | (dropped ? kCandDropped : 0u) | (nsp > 0 ? kCandSpilled : 0u));
     RT_TACC(5, t_r0);
     if (COUNT && fp.counters) {
         atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
@@ -568,10 +591,17 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
     // the traversal kernel is done with the tile queues: clear them for the
     // next launch (the packet pipeline needs no memset)
     if (blockIdx.x == 0 && threadIdx.x < RT_QUEUES) aux.tile_ctr[threadIdx.x * RT_QUEUE_STRIDE] = 0;
-    const size_t npix = (size_t)fp.W * fp.nrows;
-    const size_t o = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const bool active = o < npix;
-    const int i = (int)(o % (size_t)fp.W), r = (int)(o / (size_t)fp.W);
+    // blocks never straddle frames: frame f owns blocks [f * bpf, (f + 1) * bpf)
+    const uint32_t fpix = (uint32_t)fp.W * (uint32_t)fp.nrows;
+    const uint32_t bpf = (fpix + 255u) / 256u;
+    const int f = (int)(blockIdx.x / bpf);
+    const uint32_t fb = blockIdx.x - (uint32_t)f * bpf;  // block within the frame
+    const size_t po = (size_t)fb * 256 + threadIdx.x;    // pixel within the frame
+    const bool active = po < fpix;
+    const size_t npix = (size_t)fpix * fp.nframes;       // candidate-list stride
+    const size_t o = out_index(fp, f, po);               // pixel of the batch
+    const int i = (int)(po % (size_t)fp.W), r = (int)(po / (size_t)fp.W);
+    const RtFrameCam& cam = fp.cam[f];
     const uint32_t cnt = active ? aux.cand_cnt[o] : 0u;
     Best out;
     out.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
@@ -579,20 +609,20 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
     out.tri = -1;
     out.px = out.py = out.pz = 0.0;
     uint32_t redo = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
-    const uint32_t nlist = cnt & ~kCandDropped;
+    const uint32_t nlist = cnt & kCandCount;
     Shade sh{0.0, 0.0, 0.0, RT_INVALID_REF};
     if (cnt != 0) {
-        const Ray64 ray = gen_ray<false>(fp, i, fp.row0 + r * fp.row_stride);
+        const Ray64 ray = gen_ray<false>(fp, cam, i, fp.row0 + r * fp.row_stride);
         double best_t = 0.0;
         uint32_t leaf = 0;
         float lb[6];
-        for (uint32_t c = 0; c < nlist; c++) {
-            const uint2 e = reinterpret_cast<const RT_G uint2*>(aux.cand)[(size_t)c * npix + o];
+        // exact test of candidate e, kept if it is the (distance, visit rank) minimum
+        auto consider = [&](const uint2 e) {
             if (COUNT) n_tris++;
             // one 128-B record: triangle, normal, id, leaf and its box
             const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)e.x;
             double t;
-            if (!mt64(T, ray, t)) continue;
+            if (!mt64(T, ray, t)) return;
             double hx, hy, hz;
             const double d = hit_dist(ray, t, hx, hy, hz);
             bool take = d < out.dist;
@@ -622,6 +652,15 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
 #pragma unroll
                 for (int a = 0; a < 6; a++) lb[a] = B[a];
             }
+        };
+        const RT_G uint2* const cl = reinterpret_cast<const RT_G uint2*>(aux.cand);
+        for (uint32_t c = 0; c < nlist; c++) consider(cl[(size_t)c * npix + o]);
+        if (cnt & kCandSpilled) {
+            for (uint32_t c = RT_CAND_LDS; c < (uint32_t)RT_CAND_SLOTS; c++) {
+                const uint2 e = cl[(size_t)c * npix + o];
+                if (e.x == ~0u) break;
+                consider(e);
+            }
         }
         if (cnt & kCandDropped) {
             // every dropped candidate has t >= drop, so its distance is at
@@ -646,7 +685,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
             const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
             aux.redo[slot] = (uint32_t)o | (redo == 2u ? kRedoPass1 : 0u);
         } else {
-            shade_store(fp, o, out, sh, false);
+            shade_store(fp, cam, f, po, out, sh, false);
         }
     }
     // hit count: block sums spread over RT_HIT_SLOTS counters (k_fixup adds
@@ -656,7 +695,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
     __syncthreads();
     if (threadIdx.x == 0 && fp.hit_count) {
         const uint32_t sum = wave_hits[0] + wave_hits[1] + wave_hits[2] + wave_hits[3];
-        if (sum) atomicAdd(aux.tile_ctr + RT_HIT_BASE + (blockIdx.x % RT_HIT_SLOTS) * RT_QUEUE_STRIDE, sum);
+        if (sum) atomicAdd(aux.tile_ctr + RT_HIT_BASE + (f * RT_HIT_SLOTS + fb % RT_HIT_SLOTS) * RT_QUEUE_STRIDE, sum);
     }
     if (!active) return;
     if (COUNT && fp.counters) {
@@ -692,7 +731,8 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
         // launch's fix-up has completed: stream order)
         RT_G uint32_t* const q = kload(&A->aux.tile_ctr);
         if (threadIdx.x == 0) q[RT_REDO_COUNT] = 0;
-        if (threadIdx.x < RT_HIT_SLOTS) q[RT_HIT_BASE + threadIdx.x * RT_QUEUE_STRIDE] = 0;
+        const int nslots = kword(&A->fp.nframes) * RT_HIT_SLOTS;
+        for (int k = threadIdx.x; k < nslots; k += blockDim.x) q[RT_HIT_BASE + k * RT_QUEUE_STRIDE] = 0;
     }
     uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     (void)tacc;
@@ -733,7 +773,7 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
 #elif RT_TILE_SCHED == 3
         {
             const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
-            const uint32_t tiles = (uint32_t)(((W_ + 7) >> 3) * ((nrows + 7) >> 3));
+            const uint32_t tiles = (uint32_t)(((W_ + 7) >> 3) * ((nrows + 7) >> 3) * kword(&A->fp.nframes));
             t = (int)tiles;
             for (uint32_t k = 0; k < RT_QUEUES; k++) {
                 const uint32_t x = (xq + k) & (RT_QUEUES - 1);
@@ -760,7 +800,8 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
         A = launder(A);
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
         const int tiles_x = (W_ + 7) >> 3;
-        const int tiles = tiles_x * ((nrows + 7) >> 3);
+        const int tiles_f = tiles_x * ((nrows + 7) >> 3);  // tiles per frame
+        const int tiles = tiles_f * kword(&A->fp.nframes);
         RT_TSTAMP(t_q0);
         if (!RT_TILE_PREFETCH) next = fetch();
         int tile = __shfl(next, 0);
@@ -782,8 +823,10 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
         n_tiles++;
 #endif
         if (RT_TILE_PREFETCH) next = fetch();
-        const int i = (tile % tiles_x) * 8 + (lane & 7);
-        const int r = (tile / tiles_x) * 8 + (lane >> 3);
+        const int f = tile / tiles_f;  // frame of the batch
+        const int ft = tile - f * tiles_f;
+        const int i = (ft % tiles_x) * 8 + (lane & 7);
+        const int r = (ft / tiles_x) * 8 + (lane >> 3);
 #if defined(RT_DIAG_HIST) || defined(RT_DIAG_TILECOST)
         const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -791,7 +834,7 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
         uint64_t tb[6];
         for (int k = 0; k < 6; k++) tb[k] = tacc[k];
 #endif
-        trace_packet<W, SP, K, COUNT>(A, i, r, i < W_ && r < nrows, stacks[wv], cands[wv], tacc);
+        trace_packet<W, SP, K, COUNT>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv], tacc);
 #ifdef RT_DIAG_TILECOST
         {   // per-tile duration (10-ns ticks) into hit_pos[3 * tile] (diagnostic build:
             // shade_store leaves hit_pos alone), and the tile's cycle split

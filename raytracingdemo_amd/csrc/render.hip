@@ -102,15 +102,16 @@ struct Win {
 // Fast exact kernel (persistent).
 // --------------------------------------------------------------------------
 template <int W, int S, bool COUNT>
-__device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int i, int r,
+__device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
                                             LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
     constexpr int G = W < 4 ? W : 4;  // children tested per load group
     const int j = fp.row0 + r * fp.row_stride;
+    const RtFrameCam& cam = fp.cam[f];
     Ray32 q;
     double tslack;
     {
-        const Ray64 ray = gen_ray(fp, i, j);
-        q = make_ray32(ray, fp.pad);
+        const Ray64 ray = gen_ray(fp, cam, i, j);
+        q = make_ray32(ray, cam.pad);
         // dist = |fl(o + d t) - o| differs from t by <= 2^-52 |o| + 2^-50 t:
         // covered by tslack + the 2^-20 relative margin of tcull
         tslack = 0x1p-40 * ((double)q.co + 1.0);
@@ -202,7 +203,7 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
                     if (COUNT) n_pre++;
                     if (!tri_prefilter(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull)) continue;
                     if (COUNT) n_tris++;
-                    const Ray64 ray = gen_ray(fp, opaque(i), j);
+                    const Ray64 ray = gen_ray(fp, cam, opaque(i), j);
                     const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)k;
                     double t;
                     if (!mt64(T, ray, t)) continue;
@@ -238,7 +239,7 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
         }
         if (pass == 1 || best.tri < 0) break;
         // deferred re-verification of the winner's reference ancestor chain
-        const Ray64 ray = gen_ray(fp, opaque(i), j);
+        const Ray64 ray = gen_ray(fp, cam, opaque(i), j);
         double hx, hy, hz;
         (void)hit_dist(ray, best.t, hx, hy, hz);
         const uint32_t leaf =
@@ -254,11 +255,11 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
     out.tri = best.tri;
     out.px = out.py = out.pz = 0.0;
     if (best.tri >= 0) {
-        const Ray64 ray = gen_ray(fp, opaque(i), j);
+        const Ray64 ray = gen_ray(fp, cam, opaque(i), j);
         (void)hit_dist(ray, best.t, out.px, out.py, out.pz);
     }
     const size_t o = (size_t)r * fp.W + i;
-    shade_store(fp, sc, o, out);
+    shade_store(fp, cam, f, sc, o, out);
     if (COUNT && fp.counters) {
         if (!fixup) atomicAdd(&fp.counters[0], 1ull);  // a fixed-up ray was counted by the packet kernel
         atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
@@ -279,18 +280,18 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
 template <int W, int S, bool COUNT>
 __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
     __shared__ uint2 lds[S][256];
-    __shared__ unsigned long long block_sum;
+    __shared__ unsigned long long frame_sum[RT_MAX_BATCH];
     const int tid = threadIdx.x;
     if (blockIdx.x == 0 && fp.hit_count && aux.cand) {
-        // fold k_resolve's hit-count partials into the caller's counter
-        if (tid == 0) block_sum = 0;
+        // fold k_resolve's per-frame hit-count partials into the caller's counters
+        if (tid < RT_MAX_BATCH) frame_sum[tid] = 0;
         __syncthreads();
-        if (tid < RT_HIT_SLOTS) {
-            const uint32_t v = aux.tile_ctr[RT_HIT_BASE + tid * RT_QUEUE_STRIDE];
-            if (v) atomicAdd(&block_sum, (unsigned long long)v);
+        for (int k = tid; k < fp.nframes * RT_HIT_SLOTS; k += 256) {
+            const uint32_t v = aux.tile_ctr[RT_HIT_BASE + k * RT_QUEUE_STRIDE];
+            if (v) atomicAdd(&frame_sum[k / RT_HIT_SLOTS], (unsigned long long)v);
         }
         __syncthreads();
-        if (tid == 0 && block_sum) atomicAdd(fp.hit_count, block_sum);
+        if (tid < fp.nframes && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
     }
     const uint32_t n = *(volatile uint32_t*)(aux.tile_ctr + RT_REDO_COUNT);
     if (n == 0) return;
@@ -299,11 +300,14 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
     st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
     st.tid = tid;
     st.top = 0;
+    const uint32_t npix = (uint32_t)fp.W * (uint32_t)fp.nrows;
     for (uint32_t e = blockIdx.x * 256u + (uint32_t)tid; e < n; e += gridDim.x * 256u) {
         const uint32_t v = aux.redo[e];
-        const uint32_t o = v & ~kRedoPass1;
+        const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: frame * npix + pixel
+        const int f = (int)(ob / npix);
+        const uint32_t o = ob - (uint32_t)f * npix;
         const int i = (int)(o % (uint32_t)fp.W), r = (int)(o / (uint32_t)fp.W);
-        trace_exact<W, S, COUNT>(sc, fp, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
+        trace_exact<W, S, COUNT>(sc, fp, f, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
     }
 }
 
@@ -328,7 +332,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace_exact(RtDevScene sc, RtFram
         if (tile >= tiles) break;
         const int i = (tile % tiles_x) * 8 + (lane & 7);
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
-        if (i < fp.W && r < fp.nrows) trace_exact<W, S, COUNT>(sc, fp, i, r, st);
+        if (i < fp.W && r < fp.nrows) trace_exact<W, S, COUNT>(sc, fp, 0, i, r, st);
     }
 }
 
@@ -351,7 +355,7 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
     int i, r;
     if (!lane_pixel(fp, i, r)) return;
     const int j = fp.row0 + r * fp.row_stride;
-    const Ray64 ray = gen_ray(fp, i, j);
+    const Ray64 ray = gen_ray(fp, fp.cam[0], i, j);
     Best best;
     best.dist = 1.7976931348623157e308;
     best.rank = 0;
@@ -387,7 +391,7 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
             if (sp < SMAX) st[sp++] = sc.rkid[k];
     }
     const size_t o = (size_t)r * fp.W + i;
-    shade_store(fp, sc, o, best);
+    shade_store(fp, fp.cam[0], 0, sc, o, best);
     if (COUNT && fp.counters) {
         atomicAdd(&fp.counters[0], 1ull);
         atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
@@ -398,7 +402,7 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
 
 constexpr int kLdsStack = 16;      // per-lane kernel: LDS ring entries per lane (8 B each)
 constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (4 B each)
-constexpr int kCandidates = 8;     // packet kernel: candidate list entries per lane (8 B each)
+constexpr int kCandidates = RT_CAND_LDS;  // packet kernel: LDS candidate list entries per lane (8 B each)
 constexpr int kFixupGrid = 256;    // k_fixup blocks (the redo list is short)
 
 // Kernel choice: the packet kernel unless its stack cannot hold the tree's
@@ -411,6 +415,20 @@ bool use_packet(uint32_t stack_bound) {
     return !lane_forced && stack_bound <= (uint32_t)kPacketStack;
 }
 
+// Frame f of a batch as a one-frame launch (kernels that run per frame).
+RtFrameParams single_frame(const RtFrameParams& fp, int f) {
+    RtFrameParams o = fp;
+    const size_t off = (size_t)f * (size_t)fp.W * (size_t)fp.nrows;
+    o.nframes = 1;
+    o.cam[0] = fp.cam[f];
+    if (o.hit_id) o.hit_id += off;
+    if (o.dist) o.dist += off;
+    if (o.hit_pos) o.hit_pos += 3 * off;
+    if (o.rgb) o.rgb += 3 * off;
+    if (o.hit_count) o.hit_count += f;
+    return o;
+}
+
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
                         hipStream_t s, const hipEvent_t* ev) {
@@ -420,7 +438,8 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     if (ev) (void)hipEventRecord(ev[0], s);
     if (use_packet(sc.stack_bound)) {
         const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
-        const dim3 rgrid((unsigned)(((uint64_t)fp.W * fp.nrows + 255) / 256));
+        // k_resolve: frame f owns blocks [f * bpf, (f + 1) * bpf)
+        const dim3 rgrid((unsigned)(((uint64_t)fp.W * fp.nrows + 255) / 256 * (uint64_t)fp.nframes));
         if (count) {
             hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true>), grid, blk, 0, s,
                                PacketArgs{sc, fp, aux});
@@ -435,8 +454,17 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
             hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, blk, 0, s, sc, fp, aux);
         }
     } else {
-        if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true, 3>), grid, blk, 0, s, sc, fp, aux);
-        else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false, 3>), grid, blk, 0, s, sc, fp, aux);
+        // per-lane kernel (trees deeper than the packet stack): one launch
+        // per frame of the batch, each on a zeroed work queue
+        for (int f = 0; f < fp.nframes; f++) {
+            const RtFrameParams f1 = single_frame(fp, f);
+            if (f > 0) {
+                hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);
+                if (e != hipSuccess) return e;
+            }
+            if (count) hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, true, 3>), grid, blk, 0, s, sc, f1, aux);
+            else hipLaunchKernelGGL((k_trace_exact<W, kLdsStack, false, 3>), grid, blk, 0, s, sc, f1, aux);
+        }
         if (ev) (void)hipEventRecord(ev[1], s);
     }
     return hipGetLastError();
@@ -474,7 +502,7 @@ int exact_blocks_per_cu(int width, uint32_t stack_bound) {
 }
 
 int exact_lds_stack() { return kLdsStack; }
-int packet_candidates() { return kCandidates; }
+int packet_candidates() { return RT_CAND_SLOTS; }  // HBM slots per pixel (LDS list + overflow)
 
 // Host entry: validates the launch geometry against what the kernels assume
 // and dispatches on node width.  mode 0 = exact fast, 1 = literal.
@@ -486,24 +514,30 @@ int packet_candidates() { return kCandidates; }
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
                         hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after) {
     *fresh_after = fresh;
-    if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
+    if (fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0) return hipSuccess;
+    if (fp.nframes > RT_MAX_BATCH || (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.nframes >= (1ull << 31))
+        return hipErrorInvalidValue;
     if (mode == 1) {
         const long tiles = (long)((fp.W + 7) / 8) * (long)((fp.nrows + 7) / 8);
         const dim3 grid((unsigned)((tiles + 3) / 4));
         if (literal_stack > 1024) return hipErrorInvalidValue;
         if (ev) (void)hipEventRecord(ev[0], s);
-        hipError_t e = literal_stack <= 64    ? launch_literal_s<64>(sc, fp, count, grid, s)
-                       : literal_stack <= 256 ? launch_literal_s<256>(sc, fp, count, grid, s)
-                                              : launch_literal_s<1024>(sc, fp, count, grid, s);
+        hipError_t e = hipSuccess;
+        for (int f = 0; f < fp.nframes && e == hipSuccess; f++) {
+            const RtFrameParams f1 = single_frame(fp, f);
+            e = literal_stack <= 64    ? launch_literal_s<64>(sc, f1, count, grid, s)
+                : literal_stack <= 256 ? launch_literal_s<256>(sc, f1, count, grid, s)
+                                       : launch_literal_s<1024>(sc, f1, count, grid, s);
+        }
         if (ev) (void)hipEventRecord(ev[1], s);
         return e;
     }
     if (aux.spill_cap + kLdsStack < sc.stack_bound || !aux.tile_ctr || !aux.spill || aux.grid <= 0)
         return hipErrorInvalidValue;
     // the redo list must hold every pixel of the shard
+    const uint64_t bpix = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.nframes;  // pixels of the batch
     if (use_packet(sc.stack_bound) &&
-        (!aux.redo || aux.redo_cap < (uint64_t)fp.W * (uint64_t)fp.nrows || !aux.cand || !aux.cand_cnt || !aux.cand_drop ||
-         aux.cand_cap < (uint64_t)fp.W * (uint64_t)fp.nrows))
+        (!aux.redo || aux.redo_cap < bpix || !aux.cand || !aux.cand_cnt || !aux.cand_drop || aux.cand_cap < bpix))
         return hipErrorInvalidValue;
     const bool packet = use_packet(sc.stack_bound);
     if (!fresh || !packet) {

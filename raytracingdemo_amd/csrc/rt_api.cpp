@@ -103,6 +103,7 @@ struct rt_scene {
     rt::Flat flat;
     std::vector<Replica> reps;
     std::mutex mu;
+    uint32_t literal_stack = 0;  // stack bound of the literal (reference-order) traversal
 };
 
 namespace {
@@ -257,14 +258,20 @@ float frame_pad(const rt_scene* s, const rt_camera* c) {
     return f;
 }
 
-RtFrameParams frame_params(const rt_scene* s, Replica& r, const rt_camera* c, int row0, int row_stride, int nrows) {
+// Launch parameters for frames c[0..n-1] (n <= RT_MAX_BATCH) of one image
+// geometry: per-pose camera basis (main.cpp:325-329) and slab margin.
+RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row0, int row_stride, int nrows) {
     RtFrameParams fp{};
-    fp.pad = frame_pad(s, c);
-    for (int a = 0; a < 3; a++) {
-        fp.pos[a] = c->pos[a];
-        fp.dir[a] = c->dir[a];
+    fp.nframes = n;
+    for (int f = 0; f < n; f++) {
+        RtFrameCam& k = fp.cam[f];
+        k.pad = frame_pad(s, &c[f]);
+        for (int a = 0; a < 3; a++) {
+            k.pos[a] = c[f].pos[a];
+            k.dir[a] = c[f].dir[a];
+        }
+        rt::camera_basis(c[f].dir, k.right, k.up);
     }
-    rt::camera_basis(c->dir, fp.right, fp.up);
     rt::pixel_constants(c->width, c->height, fp.cam_iw, fp.cam_ih, fp.cam_half, fp.cam_aspect);
     fp.W = c->width;
     fp.H = c->height;
@@ -272,6 +279,16 @@ RtFrameParams frame_params(const rt_scene* s, Replica& r, const rt_camera* c, in
     fp.row_stride = row_stride;
     fp.nrows = nrows;
     return fp;
+}
+
+// Frames per launch of a batch: RT_MAX_BATCH, or RT_BATCH (1..RT_MAX_BATCH) for A/B runs.
+int batch_frames() {
+    static const int b = [] {
+        const char* e = std::getenv("RT_BATCH");
+        const int v = e ? std::atoi(e) : RT_MAX_BATCH;
+        return v >= 1 && v <= RT_MAX_BATCH ? v : RT_MAX_BATCH;
+    }();
+    return b;
 }
 
 // Order this launch after every earlier launch on the replica.
@@ -327,7 +344,7 @@ void launch(const rt_scene* s, Replica& r, const RtFrameParams& fp, int mode, bo
             const hipEvent_t* tev) {
     bool fresh_after = false;
     const hipError_t e =
-        rt::launch_trace(r.dev, fp, aux_of(r), mode, count, st, literal_stack_bound(s), tev, r.fresh, &fresh_after);
+        rt::launch_trace(r.dev, fp, aux_of(r), mode, count, st, s->literal_stack, tev, r.fresh, &fresh_after);
     r.fresh = e == hipSuccess && fresh_after;
     HIP_TRY(e);
 }
@@ -386,6 +403,7 @@ int rt_scene_create(const double* tri_v, uint64_t n, int algo, int k, int collap
         s->soup = rt::make_soup(tri_v, n);
         s->tree = rt::build_tree(s->soup, algo, k, collapse);
         s->flat = rt::flatten(s->soup, s->tree, 0);
+        s->literal_stack = literal_stack_bound(s.get());
         *out = s.release();
         return RT_OK;
     } catch (const rt::Error& e) {
@@ -413,12 +431,19 @@ int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {
     }
 }
 
-int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mode, int row0, int row_stride,
-                          int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
-    if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+int rt_render_batch_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int mode, int row0,
+                           int row_stride, int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
+    if (!s || !out || (nframes > 0 && !cams)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (nframes < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative frame count");
     if (mode != RT_MODE_EXACT && mode != RT_MODE_FP64) return fail(RT_ERR_INVALID_ARGUMENT, "bad mode");
     try {
-        check_camera(s, cam);
+        for (int f = 0; f < nframes; f++) {
+            check_camera(s, &cams[f]);
+            if (cams[f].width != cams[0].width || cams[f].height != cams[0].height)
+                return fail(RT_ERR_INVALID_ARGUMENT, "frames of a batch must share the image size");
+        }
+        if (nframes == 0) return RT_OK;
+        const rt_camera* cam = &cams[0];
         if (row0 < 0 || row_stride < 1 || nrows < 0 || (nrows > 0 && row0 + (int64_t)(nrows - 1) * row_stride >= cam->height))
             return fail(RT_ERR_INVALID_ARGUMENT, "row shard outside the image");
         Replica* r;
@@ -428,31 +453,45 @@ int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mod
         }
         DevGuard g(device);
         hipStream_t st = (hipStream_t)stream;
-        RtFrameParams fp = frame_params(s, *r, cam, row0, row_stride, nrows);
-        fp.hit_id = out->hit_id;
-        fp.dist = out->dist;
-        fp.hit_pos = out->pos;
-        fp.rgb = out->rgb;
-        fp.hit_count = out->hit_count;
-        fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
+        const uint64_t fpix = (uint64_t)cam->width * (uint64_t)nrows;  // pixels per frame
+        // frames per launch: the batch limit, and batch pixels < 2^31 (redo-list entries)
+        int per = batch_frames();
+        while (per > 1 && fpix * (uint64_t)per >= (1ull << 31)) per--;
         // serialise on the replica's stream: the caller's stream waits for it
         std::lock_guard<std::mutex> lk(s->mu);
-        ensure_redo(*r, (uint64_t)cam->width * (uint64_t)nrows);
-        const hipEvent_t* tev = nullptr;
-        if (flags & RT_FLAG_TIMING) {
-            if (r->tev_used == r->tev.size()) {
-                std::array<hipEvent_t, 2> a{};
-                for (auto& e : a) HIP_TRY(hipEventCreate(&e));
-                r->tev.push_back(a);
-            }
-            tev = r->tev[r->tev_used++].data();
-        }
+        ensure_redo(*r, fpix * (uint64_t)std::min(per, nframes));
         order_on(*r, st);
-        launch(s, *r, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, tev);
+        for (int f0 = 0; f0 < nframes; f0 += per) {
+            const int n = std::min(per, nframes - f0);
+            RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows);
+            const uint64_t off = (uint64_t)f0 * fpix;
+            fp.hit_id = out->hit_id ? out->hit_id + off : nullptr;
+            fp.dist = out->dist ? out->dist + off : nullptr;
+            fp.hit_pos = out->pos ? out->pos + 3 * off : nullptr;
+            fp.rgb = out->rgb ? out->rgb + 3 * off : nullptr;
+            fp.hit_count = out->hit_count ? out->hit_count + f0 : nullptr;
+            fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
+            const hipEvent_t* tev = nullptr;
+            if (flags & RT_FLAG_TIMING) {
+                if (r->tev_used == r->tev.size()) {
+                    std::array<hipEvent_t, 2> a{};
+                    for (auto& e : a) HIP_TRY(hipEventCreate(&e));
+                    r->tev.push_back(a);
+                }
+                tev = r->tev[r->tev_used++].data();
+            }
+            launch(s, *r, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, tev);
+        }
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
     }
+}
+
+int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mode, int row0, int row_stride,
+                          int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
+    if (!cam) return fail(RT_ERR_INVALID_ARGUMENT, "camera is NULL");
+    return rt_render_batch_device(s, device, cam, 1, mode, row0, row_stride, nrows, out, stream, flags);
 }
 
 int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* out) {
@@ -482,7 +521,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         d.hit_count = reinterpret_cast<unsigned long long*>(base + o_cnt);
         order_on(r, r.stream);
         HIP_TRY(hipMemsetAsync(d.hit_count, 0, 8, r.stream));
-        RtFrameParams fp = frame_params(s, r, cam, 0, 1, cam->height);
+        RtFrameParams fp = frame_params(s, cam, 1, 0, 1, cam->height);
         fp.hit_id = d.hit_id;
         fp.dist = d.dist;
         fp.hit_pos = d.pos;

@@ -40,10 +40,22 @@
 #define RT_QUEUES 8
 #define RT_QUEUE_STRIDE 16
 #define RT_REDO_COUNT (RT_QUEUES * RT_QUEUE_STRIDE)
-// then RT_HIT_SLOTS hit-count partial sums RT_QUEUE_STRIDE words apart
+// then, per frame of the launch, RT_HIT_SLOTS hit-count partial sums
+// RT_QUEUE_STRIDE words apart (frame f's slot s at RT_HIT_BASE + (f *
+// RT_HIT_SLOTS + s) * RT_QUEUE_STRIDE)
 #define RT_HIT_SLOTS 64
 #define RT_HIT_BASE 1024
-#define RT_QUEUE_WORDS (RT_HIT_BASE + RT_HIT_SLOTS * RT_QUEUE_STRIDE)
+// Frames per launch: one launch of the packet pipeline renders up to
+// RT_MAX_BATCH frames (camera poses) of the same geometry, so the persistent
+// traversal kernel's ramp-up and tail, and the launch gaps, are paid once per
+// batch instead of once per frame.
+#define RT_MAX_BATCH 12
+#define RT_QUEUE_WORDS (RT_HIT_BASE + RT_MAX_BATCH * RT_HIT_SLOTS * RT_QUEUE_STRIDE)
+// Candidate lists handed from the traversal to the resolve kernel, per pixel:
+// RT_CAND_LDS entries kept in LDS during the walk plus overflow slots written
+// straight to HBM, RT_CAND_SLOTS in all ({triangle, t lower bound}, 8 B each).
+#define RT_CAND_LDS 8
+#define RT_CAND_SLOTS 32
 // tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
 #define RT_TRI32_PAD 4
 
@@ -100,17 +112,28 @@ struct RtLaunchAux {
     RT_G float* cand_drop;     // per pixel: smallest t bound of a dropped candidate (if flagged)
 };
 
-struct RtFrameParams {
+// One camera pose of a launch (Camera, camera.hpp:20-38: position, view
+// direction and the basis main.cpp:325-329 derives from it).
+struct RtFrameCam {
     double pos[3], dir[3], right[3], up[3];
+    float pad;                     // world-space slab margin of the fp32 traversal (per pose)
+    uint32_t reserved;
+};
+
+// One launch: `nframes` frames (poses cam[0..nframes-1]) of the same image
+// geometry and row shard.  Frame f's outputs start f * W * nrows pixels into
+// every output buffer; its hit counter is hit_count[f].
+struct RtFrameParams {
     double cam_iw, cam_ih;        // 1/W, 1/H            (camera.hpp:33-34)
     double cam_half, cam_aspect;  // tan(fov/2), W/H      (camera.hpp:29-30)
     int32_t W, H;
     int32_t row0, row_stride, nrows;
+    int32_t nframes;              // 1..RT_MAX_BATCH
     RT_G uint32_t* hit_id;
     RT_G double* dist;
     RT_G double* hit_pos;
     RT_G uint8_t* rgb;
     RT_G unsigned long long* hit_count;
     RT_G unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits, chain_nodes] or NULL
-    float pad;                     // world-space slab margin of the fp32 traversal
+    RtFrameCam cam[RT_MAX_BATCH];
 };

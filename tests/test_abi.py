@@ -90,3 +90,24 @@ def test_device_calls_fail_loudly_without_upload():
     s = rt.Scene(tri, "bsah", 2)
     with pytest.raises(rt.RTError, match="not uploaded"):
         s.calculate_screen([0, 0, 5], [0, 0, -1], 8, 8)
+
+
+def test_batch_render_rejects_mixed_sizes_and_needs_a_device():
+    """rt_render_batch_device: every pose of a batch shares one image size, and
+    without an uploaded replica the call fails loudly (no CPU fallback)."""
+    N, L = _lib()
+    import numpy as np
+    import raytracingdemo_amd as rt
+    from conftest import golden_scene
+    s = rt.Scene(golden_scene("teapot.obj"), "bsah", 4)
+    cams = (N.rt_camera * 2)(rt._camera([0, 0, 5], [0, 0, -1], 8, 8), rt._camera([0, 0, 5], [0, 0, -1], 8, 6))
+    o = N.rt_device_out()
+    st = L.rt_render_batch_device(s.handle, 0, cams, 2, N.RT_MODE_EXACT, 0, 1, 6, C.byref(o), None, 0)
+    assert st == N.RT_ERR_INVALID_ARGUMENT
+    assert b"share the image size" in L.rt_last_error()
+    cams[1].height = 8
+    st = L.rt_render_batch_device(s.handle, 0, cams, 2, N.RT_MODE_EXACT, 0, 1, 8, C.byref(o), None, 0)
+    assert st != N.RT_OK
+    assert L.rt_render_batch_device(s.handle, 0, cams, -1, N.RT_MODE_EXACT, 0, 1, 8, C.byref(o), None, 0) \
+        == N.RT_ERR_INVALID_ARGUMENT
+    assert np.isfinite(s.tris).all()

@@ -29,9 +29,9 @@ for s in $STEPS; do
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
                    -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
         pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
-                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu --key-out gpurun_out/pmc_key.txt && \
+                   -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu --key-out gpurun_out/pmc_key.txt && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
-                   -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu && \
+                   -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu && \
                python tools/pmc_traffic.py gpurun_out/pmc/fetch_counter_collection.csv \
                    gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
         list)  run list 120 rocprofv3 -L ;;
@@ -42,16 +42,17 @@ for s in $STEPS; do
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}" 300 \
                           python bench.py --no-cpu --steps 5 || exit 1; done ;;
+        batches) for b in 1 4 6 12; do RT_BATCH=$b run bench_b$b 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
         lane)  RT_KERNEL=lane run bench_lane 300 python bench.py --no-cpu --steps 5 ;;
         lanetests) RT_KERNEL=lane run tests_lane 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
-        sq)    for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+        sq)    for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
                            "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD" \
                            "SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_TC_DATA_READ_REQ SQC_TC_STALL SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
                            "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" \
                            "SQC_DCACHE_MISSES_DUPLICATE SQC_DCACHE_REQ_READ_16 SQC_DCACHE_REQ_READ_8 SQC_DCACHE_REQ_READ_4 TCC_TAG_STALL_sum TCC_LATENCY_FIFO_FULL_sum"; do
                    n=$((${n:-0}+1))
                    run sq$n 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$n \
-                       -- python bench.py --steps 1 --warmup 0 --frames 4 --no-cpu || exit 1
+                       -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu || exit 1
                done
                python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt ;;
         *) echo "unknown step $s"; exit 2 ;;

@@ -188,7 +188,8 @@ def _stack_scene(eps: float, n: int, far_hit: bool) -> np.ndarray:
     so the fp32 filter can only call them borderline."""
     tris = [[eps, eps, -k, 1.0, eps, -k, eps, 1.0, -k] for k in range(1, n + 1)]
     if far_hit:  # one robust hit far behind the stack
-        tris.append([-3.0, -3.0, -30.0, 3.0, -3.0, -30.0, 0.0, 3.0, -30.0])
+        z = -float(n + 16)
+        tris.append([-3.0, -3.0, z, 3.0, -3.0, z, 0.0, 3.0, z])
     return np.array(tris, dtype=np.float64)
 
 

@@ -100,6 +100,9 @@ typedef struct {
     uint64_t device_bytes;    /* scene bytes resident per device        */
     uint32_t stack_bound;     /* worst-case traversal stack entries     */
     double node_bytes;        /* bytes of one wide node                 */
+    uint32_t walk_tree;       /* 1: device nodes from the rebuilt SAH walk tree
+                                 (results unchanged), 0: from the
+                                 reference tree itself (RT_WALK=reference) */
 } rt_scene_stats_t;
 
 typedef struct {

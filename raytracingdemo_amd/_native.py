@@ -64,7 +64,8 @@ class rt_scene_stats_t(C.Structure):
     _fields_ = [("triangles", C.c_uint64), ("real_nodes", C.c_uint64), ("real_inner", C.c_uint64),
                 ("real_leaves", C.c_uint64), ("depth", C.c_uint32), ("max_children", C.c_uint32),
                 ("max_leaf_size", C.c_uint32), ("wide_width", C.c_uint32), ("wide_nodes", C.c_uint64),
-                ("device_bytes", C.c_uint64), ("stack_bound", C.c_uint32), ("node_bytes", C.c_double)]
+                ("device_bytes", C.c_uint64), ("stack_bound", C.c_uint32), ("node_bytes", C.c_double),
+                ("walk_tree", C.c_uint32)]
 
 
 class rt_frame_stats_t(C.Structure):

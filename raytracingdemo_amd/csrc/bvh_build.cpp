@@ -391,6 +391,35 @@ struct Flattener {
         p[7] = (uint32_t)longest_axis(mn, mx) | (nvalid << 2);
     }
 
+    // walk-tree child reference: a leaf range or a new wide node whose slots
+    // are the collapsed children, sorted by centre along the node's longest
+    // axis (the packet kernel walks them front to back along it)
+    uint32_t walk_ref(const WalkTree& w, int32_t b, uint32_t depth) {
+        const WalkNode& n = w.nodes[b];
+        if (n.left < 0) {
+            if (n.count == 0) return RT_INVALID_REF;
+            if (n.count > 16) throw Error{RT_ERR_INVALID_ARGUMENT, "leaf larger than 16 primitives"};
+            if (n.first > RT_LEAF_MAX_FIRST) throw Error{RT_ERR_INVALID_ARGUMENT, "scene too large"};
+            return rt_make_leaf(n.first, n.count);
+        }
+        std::vector<int32_t> kids = collapse_children(w, b, W);
+        const int axis = longest_axis(n.mn, n.mx);
+        std::stable_sort(kids.begin(), kids.end(), [&](int32_t x, int32_t y) {
+            return w.nodes[x].mn[axis] + w.nodes[x].mx[axis] < w.nodes[y].mn[axis] + w.nodes[y].mx[axis];
+        });
+        const uint32_t id = alloc_node();
+        wide_depth = std::max(wide_depth, depth + 1);
+        for (size_t c = 0; c < kids.size(); c++) {
+            float b6[6];
+            box32(w.nodes[kids[c]].mn, w.nodes[kids[c]].mx, b6);
+            const uint32_t r = walk_ref(w, kids[c], depth + 1);
+            set_slot(id, (int)c, b6, r);
+        }
+        uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + (size_t)id * nb);
+        p[7] = (uint32_t)axis | ((uint32_t)kids.size() << 2);
+        return id;
+    }
+
     uint32_t emit_inner(const std::vector<int32_t>& kids, uint32_t depth) {
         uint32_t id = alloc_node();
         wide_depth = std::max(wide_depth, depth + 1);
@@ -433,7 +462,7 @@ struct Flattener {
 
 }  // namespace
 
-Flat flatten(const Soup& s, const Tree& t, int width_hint) {
+Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk) {
     Flat f;
     // --- tree statistics
     uint32_t maxk = 0, maxleaf = 0, depth = 0, stack_bound = 1;
@@ -460,6 +489,8 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     f.max_children = maxk;
     f.max_leaf = maxleaf;
     int W = width_hint;
+    if (walk) W = 8;
+    f.walk = walk != nullptr;
     if (W <= 0) {
         W = 2;
         while (W < (int)maxk && W < 16) W *= 2;
@@ -475,15 +506,16 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     f.coord_max = cm;
     f.pad = 0;
 
-    // --- per-triangle data in BVH order
+    // --- per-triangle data in BVH (walk) order
     const uint64_t n = s.n;
+    const std::vector<uint32_t>& worder = walk ? walk->order : t.order;
     f.tri64.resize(n * RT_TRI64_DOUBLES);
     f.tri32.resize((n + RT_TRI32_PAD) * 12, 0.0f);  // + padding records (packet kernel leaf chunks)
     f.tri_id.resize(n);
     f.tri_rank.resize(n);
     f.tri_leaf.resize(n);
     for (uint64_t i = 0; i < n; i++) {
-        uint32_t id = t.order[i];
+        uint32_t id = worder[i];
         const double* p = s.v.data() + (size_t)id * 9;
         double* q = f.tri64.data() + i * RT_TRI64_DOUBLES;
         q[0] = p[0]; q[1] = p[1]; q[2] = p[2];
@@ -524,6 +556,9 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     {
         // visit order of StackBVH::traverse (stack_bvh.hpp:619-641): LIFO,
         // children pushed 0..n-1 so the last child is visited first.
+        // (computed per reference-order position, then placed at each
+        // triangle's walk-order index)
+        std::vector<uint32_t> rrank(n), rleaf(n), wpos(n);
         uint32_t rank = 0;
         std::vector<int32_t> st{0};
         while (!st.empty()) {
@@ -531,8 +566,16 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
             st.pop_back();
             const RNode& nd = t.nodes[ni];
             if (nd.kids.empty())
-                for (int64_t i = nd.begin; i < nd.end; i++) { f.tri_rank[i] = rank++; f.tri_leaf[i] = (uint32_t)ni; }
+                for (int64_t i = nd.begin; i < nd.end; i++) { rrank[i] = rank++; rleaf[i] = (uint32_t)ni; }
             for (int32_t c : nd.kids) st.push_back(c);
+        }
+        for (uint64_t i = 0; i < n; i++) wpos[worder[i]] = (uint32_t)i;
+        f.ref2walk.resize(n);
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t w = wpos[t.order[i]];
+            f.ref2walk[i] = w;
+            f.tri_rank[w] = rrank[i];
+            f.tri_leaf[w] = rleaf[i];
         }
     }
     // normal, loader id, leaf and the leaf box (fp32, rounded inward) complete
@@ -571,7 +614,11 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint) {
     // --- wide nodes
     Flattener F(s, t, f);
     F.box32(t.nodes[0].mn, t.nodes[0].mx, f.root_box);
-    if (n == 0) {
+    if (walk && n > 0) {
+        F.box32(walk->nodes[0].mn, walk->nodes[0].mx, f.root_box);
+        f.root_ref = F.walk_ref(*walk, 0, 0);
+        if (f.n_wide == 0) F.alloc_node();
+    } else if (n == 0) {
         f.root_ref = RT_INVALID_REF;
         F.alloc_node();
     } else {

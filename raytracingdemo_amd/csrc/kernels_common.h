@@ -108,6 +108,9 @@ __device__ __forceinline__ bool tri_prefilter(const float4 A, const float4 B, co
     return true;
 }
 
+#ifndef RT_TRI_UGATE
+#define RT_TRI_UGATE 0
+#endif
 // Classifying variant of tri_prefilter for the deferred fp64 resolve.
 //   0  the exact fp64 test must reject (or t > tcull)
 //   1  borderline: only the fp64 test can decide
@@ -142,6 +145,14 @@ __device__ __forceinline__ int tri_classify(const float4 A, const float4 B, cons
     tu = __builtin_huge_valf();
     if (!(aa > errA)) return 1;  // sign of the determinant uncertain: let fp64 decide
     const float sg = a > 0.f ? 1.f : -1.f;
+#if RT_TRI_UGATE
+    // first gate on u alone (u < 0 or u > 1, triangle.hpp:50): a tile's rays
+    // mostly miss a leaf triangle together, and u needs neither q, V nor T
+    {
+        const float Us = sg * U;
+        if (Us < -errU || Us > aa + errU + errA) return 0;
+    }
+#endif
     const float Us = sg * U, Vs = sg * V, Ts = sg * T;
     if (Us < -errU || Vs < -errV || Ts < -errT) return 0;
     if (Us + Vs > aa + errU + errV + errA) return 0;
@@ -286,7 +297,7 @@ __device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtFra
     }
     if (fp.hit_id) fp.hit_id[o] = b.tri >= 0 ? sh.id : RT_INVALID_REF;
     if (fp.dist) fp.dist[o] = b.tri >= 0 ? b.dist : -1.0;
-#ifndef RT_DIAG_TILECOST
+#if !defined(RT_DIAG_TILECOST) && !defined(RT_DIAG_WAVES)
     if (fp.hit_pos) {
         fp.hit_pos[3 * o] = b.tri >= 0 ? b.px : 0.0;
         fp.hit_pos[3 * o + 1] = b.tri >= 0 ? b.py : 0.0;

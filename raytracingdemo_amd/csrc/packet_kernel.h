@@ -66,6 +66,12 @@
 #define RT_DIAG_SPREAD 16
 #define RT_DIAG_SLOTS 64
 
+// Work stealing between the per-XCD tile queues (RT_TILE_SCHED 1); measured
+// slower (9528 vs 9850 Mrays/s) with no change in wave busy fraction, so off.
+#ifndef RT_STEAL
+#define RT_STEAL 0
+#endif
+
 // Packed (lo, hi) slab fma (measured: no gain over scalar fma); next-tile
 // prefetch (measured: slower, a reserved tile lengthens the tail).
 #ifndef RT_PK_SLAB
@@ -103,6 +109,8 @@
 #endif
 #if RT_PACKET_WPE > 0
 #define RT_PACKET_ATTR __attribute__((amdgpu_waves_per_eu(RT_PACKET_WPE)))
+#elif defined(RT_PACKET_SGPRS)
+#define RT_PACKET_ATTR __attribute__((amdgpu_num_sgpr(RT_PACKET_SGPRS)))
 #else
 #define RT_PACKET_ATTR
 #endif
@@ -736,7 +744,7 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
     }
     uint64_t tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     (void)tacc;
-#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE)
+#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE) || defined(RT_DIAG_WAVES)
     const uint64_t t_life = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
     uint32_t n_tiles = 0;
 #endif
@@ -745,6 +753,8 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
     // x, x + 8, x + 16, ...; every queue is drained by the blocks b = x mod 8.
     const uint32_t xq = blockIdx.x % RT_QUEUES;
     bool first = true;
+    uint32_t hop = 0;  // queues (after the own one) this wave found drained
+    (void)hop;
     // waves drained through queue xq: 4 per block b = xq (mod 8)
     const uint32_t nwx = 4u * ((gridDim.x + RT_QUEUES - 1 - xq) / RT_QUEUES);
     (void)first;
@@ -768,7 +778,19 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
             first = false;
             t = (int)(xq + RT_QUEUES * ((blockIdx.x / RT_QUEUES) * 4 + wv));
         } else if (lane == 0) {
-            t = (int)(xq + RT_QUEUES * (nwx + atomicAdd(kload(&A->aux.tile_ctr) + xq * RT_QUEUE_STRIDE, 1u)));
+            // own queue first; once it is drained, steal from the next
+            // queues in turn (a drained queue stays drained), so no XCD
+            // idles while another still has tiles
+            const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
+            const int all = ((W_ + 7) >> 3) * ((nrows + 7) >> 3) * kword(&A->fp.nframes);
+            RT_G uint32_t* const ctr = kload(&A->aux.tile_ctr);
+            for (;;) {
+                const uint32_t qx = (xq + hop) & (RT_QUEUES - 1);
+                const uint32_t nwq = 4u * ((gridDim.x + RT_QUEUES - 1 - qx) / RT_QUEUES);
+                t = (int)(qx + RT_QUEUES * (nwq + atomicAdd(ctr + qx * RT_QUEUE_STRIDE, 1u)));
+                if (!RT_STEAL || t < all || hop == RT_QUEUES - 1) break;
+                hop++;
+            }
         }
 #elif RT_TILE_SCHED == 3
         {
@@ -819,7 +841,7 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
 #endif
         RT_TACC(7, t_q0);
         if (tile >= tiles) break;
-#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE)
+#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE) || defined(RT_DIAG_WAVES)
         n_tiles++;
 #endif
         if (RT_TILE_PREFETCH) next = fetch();
@@ -862,7 +884,19 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
         }
 #endif
     }
-#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE)
+#ifdef RT_DIAG_WAVES
+    {   // per-wave start / end (10-ns ticks) and tile count into hit_pos[3 * wave + k]
+        // (diagnostic build: shade_store leaves hit_pos alone; tools/wave_life.py)
+        RT_G double* hp = kload(&A->fp.hit_pos);
+        const size_t wid = (size_t)blockIdx.x * 4 + wv;
+        if (hp && lane == 0) {
+            hp[3 * wid] = (double)t_life;
+            hp[3 * wid + 1] = (double)__builtin_amdgcn_s_memrealtime();
+            hp[3 * wid + 2] = (double)n_tiles;
+        }
+    }
+#endif
+#if defined(RT_DIAG_TIMING) || defined(RT_DIAG_LIFE) || defined(RT_DIAG_WAVES)
     RT_G unsigned long long* const diag = kload(&A->aux.diag);
     if (diag && lane == 0) {
 #ifdef RT_DIAG_TIMING

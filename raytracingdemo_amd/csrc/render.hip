@@ -372,7 +372,8 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
         const uint32_t k0 = sc.rkid_off[n], k1 = sc.rkid_off[n + 1];
         if (k0 == k1) {
             const uint32_t b = sc.rrange[2 * n], e = sc.rrange[2 * n + 1];
-            for (uint32_t k = b; k < e; k++) {
+            for (uint32_t kr = b; kr < e; kr++) {
+                const uint32_t k = sc.ref2walk[kr];  // triangle records are in walk (BVH) order
                 if (COUNT) n_tris++;
                 double t;
                 if (!mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, ray, t)) continue;

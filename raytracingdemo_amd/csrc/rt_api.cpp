@@ -161,6 +161,7 @@ void upload_one(rt_scene* s, int device) {
         {f.rkid_off.data(), f.rkid_off.size() * sizeof(uint32_t), 0},
         {f.rkid.data(), f.rkid.size() * sizeof(uint32_t), 0},
         {f.rrange.data(), f.rrange.size() * sizeof(uint32_t), 0},
+        {f.ref2walk.data(), f.ref2walk.size() * sizeof(uint32_t), 0},
     };
     size_t off = 0;
     for (auto& sc : secs) {
@@ -187,6 +188,7 @@ void upload_one(rt_scene* s, int device) {
     d.rkid_off = reinterpret_cast<const uint32_t*>(at(9));
     d.rkid = reinterpret_cast<const uint32_t*>(at(10));
     d.rrange = reinterpret_cast<const uint32_t*>(at(11));
+    d.ref2walk = reinterpret_cast<const uint32_t*>(at(12));
     d.root_ref = f.root_ref;
     std::memcpy(d.root_box, f.root_box, sizeof d.root_box);
     d.n_tris = (uint32_t)s->soup.n;
@@ -402,7 +404,15 @@ int rt_scene_create(const double* tri_v, uint64_t n, int algo, int k, int collap
         std::unique_ptr<rt_scene> s(new rt_scene);
         s->soup = rt::make_soup(tri_v, n);
         s->tree = rt::build_tree(s->soup, algo, k, collapse);
-        s->flat = rt::flatten(s->soup, s->tree, 0);
+        // the device walks a rebuilt SAH tree (walk_tree.cpp) unless
+        // RT_WALK=reference asks for the reference tree's own nodes
+        const char* wk = std::getenv("RT_WALK");
+        if (wk && wk[0] == 'r') {
+            s->flat = rt::flatten(s->soup, s->tree, 0);
+        } else {
+            const rt::WalkTree wt = rt::build_walk_tree(s->soup);
+            s->flat = rt::flatten(s->soup, s->tree, 0, &wt);
+        }
         s->literal_stack = literal_stack_bound(s.get());
         *out = s.release();
         return RT_OK;
@@ -627,9 +637,10 @@ int rt_scene_stats(const rt_scene* s, rt_scene_stats_t* o) {
     o->wide_nodes = f.n_wide;
     o->node_bytes = rt_node_bytes(f.width);
     o->stack_bound = f.stack_bound;
+    o->walk_tree = f.walk ? 1u : 0u;
     o->device_bytes = f.wide.size() + f.tri32.size() * 4 + f.tri64.size() * 8 + f.tri_id.size() * 12 +
                       f.rbox.size() * 8 + f.rparent.size() * 4 + s->soup.normal.size() * 8 +
-                      (f.rkid_off.size() + f.rkid.size() + f.rrange.size()) * 4;
+                      (f.rkid_off.size() + f.rkid.size() + f.rrange.size() + f.ref2walk.size()) * 4;
     return RT_OK;
 }
 

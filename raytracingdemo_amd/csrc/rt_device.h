@@ -54,7 +54,9 @@
 // Candidate lists handed from the traversal to the resolve kernel, per pixel:
 // RT_CAND_LDS entries kept in LDS during the walk plus overflow slots written
 // straight to HBM, RT_CAND_SLOTS in all ({triangle, t lower bound}, 8 B each).
+#ifndef RT_CAND_LDS
 #define RT_CAND_LDS 8
+#endif
 #define RT_CAND_SLOTS 32
 // tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
 #define RT_TRI32_PAD 4
@@ -88,7 +90,8 @@ struct RtDevScene {
     const RT_G double* normal;    // loader order, 3 per triangle
     const RT_G uint32_t* rkid_off;// real tree CSR (literal reference-order mode)
     const RT_G uint32_t* rkid;
-    const RT_G uint32_t* rrange;  // real node primitive range [begin, end)
+    const RT_G uint32_t* rrange;  // real node primitive range [begin, end) (reference order)
+    const RT_G uint32_t* ref2walk;// reference-order position -> BVH-order triangle index
     uint32_t root_ref;
     float root_box[6];
     uint32_t n_tris;

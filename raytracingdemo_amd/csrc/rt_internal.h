@@ -43,6 +43,21 @@ struct Tree {
 // StackBVH::build + partition fn + collapse (stack_bvh.hpp:26-608).
 Tree build_tree(const Soup& s, int algo, int k, int collapse);
 
+// Walk tree (walk_tree.cpp): the binary SAH tree the device traversal walks
+// after collapsing it into W-wide nodes.  Leaves are [first, first + count)
+// ranges of `order` (loader indices).
+struct WalkNode {
+    double mn[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+    int32_t left = -1, right = -1;  // inner node: both >= 0
+    uint32_t first = 0, count = 0;  // leaf
+};
+struct WalkTree {
+    std::vector<WalkNode> nodes;  // nodes[0] = root
+    std::vector<uint32_t> order;  // triangle (loader) index per walk position
+};
+WalkTree build_walk_tree(const Soup& s);
+std::vector<int32_t> collapse_children(const WalkTree& w, int32_t b, int W);
+
 // Device-format scene (wide fp32 nodes + fp64 leaf data), built from Tree.
 struct Flat {
     int width = 8;                        // W
@@ -57,11 +72,15 @@ struct Flat {
     std::vector<double> rbox;             // real nodes: 6 doubles
     std::vector<int32_t> rparent;         // real nodes: parent
     std::vector<uint32_t> rkid_off, rkid, rrange;  // real tree in CSR form
+    std::vector<uint32_t> ref2walk;       // reference-order position -> walk-order (BVH-order) index
+    bool walk = false;                    // wide nodes come from the walk tree (not the reference tree)
     uint32_t stack_bound = 0;
     uint32_t depth = 0, max_children = 0, max_leaf = 0;
     uint64_t real_inner = 0, real_leaves = 0;
 };
-Flat flatten(const Soup& s, const Tree& t, int width_hint);
+// walk: when non-null, the wide nodes and the per-triangle order come from
+// the walk tree (W = 8); the reference tree still supplies ranks and chains.
+Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk = nullptr);
 
 // Camera helpers (camera.hpp:20-38, main.cpp:325-329, camera_path.hpp:18-26)
 void pixel_constants(int W, int H, double& iw, double& ih, double& half, double& aspect);

@@ -1,0 +1,192 @@
+// Walk tree: the acceleration structure the gfx950 traversal actually walks.
+//
+// Results never depend on it.  The reference (src/stack_bvh.hpp:611-644)
+// reports, among the triangles whose fp64 Moller-Trumbore test passes and
+// whose every ancestor box in *its* tree passes the fp64 slab test, the
+// nearest one (first in its LIFO visit order on ties).  The device pipeline
+// finds every triangle the fp32 filters cannot rule out, whatever tree it
+// walks, and takes the ancestor chain (rbox/rparent) and the visit ranks
+// (tri_rank) from the reference's own tree.  So the walk tree
+// is free to be a better tree than the reference's.
+//
+// The reference's k-way "bsah" partition splits a node into up to k slabs
+// along one axis from 16 bins (stack_bvh.hpp:241-449): long thin children
+// that overlap a tile's rays far more than needed.  This builder makes a
+// binary SAH tree over all three axes (32 centroid bins, leaves of at most
+// kMaxLeaf triangles: one scalar-load chunk of the packet kernel), then
+// collapses it into W-wide nodes by repeatedly opening the child with the
+// largest surface area (the usual greedy wide-BVH collapse).
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <limits>
+
+#include "rt_internal.h"
+
+namespace rt {
+namespace {
+
+constexpr int kBins = 32;
+
+struct BBox {
+    double mn[3], mx[3];
+    BBox() {
+        for (int a = 0; a < 3; a++) {
+            mn[a] = std::numeric_limits<double>::infinity();
+            mx[a] = -std::numeric_limits<double>::infinity();
+        }
+    }
+    void grow(const BBox& o) {
+        for (int a = 0; a < 3; a++) {
+            mn[a] = std::min(mn[a], o.mn[a]);
+            mx[a] = std::max(mx[a], o.mx[a]);
+        }
+    }
+    void grow(const double p[3]) {
+        for (int a = 0; a < 3; a++) {
+            mn[a] = std::min(mn[a], p[a]);
+            mx[a] = std::max(mx[a], p[a]);
+        }
+    }
+    double area() const {
+        if (!(mx[0] >= mn[0])) return 0.0;
+        const double ex = mx[0] - mn[0], ey = mx[1] - mn[1], ez = mx[2] - mn[2];
+        return 2.0 * (ex * ey + ey * ez + ez * ex);
+    }
+};
+
+int max_leaf() {
+    static const int m = [] {
+        const char* e = std::getenv("RT_WALK_LEAF");
+        const int v = e ? std::atoi(e) : 4;
+        return v >= 1 && v <= 16 ? v : 4;
+    }();
+    return m;
+}
+
+}  // namespace
+
+WalkTree build_walk_tree(const Soup& s) {
+    WalkTree w;
+    const uint32_t n = (uint32_t)s.n;
+    w.order.resize(n);
+    for (uint32_t i = 0; i < n; i++) w.order[i] = i;
+    if (n == 0) return w;
+    const int LMAX = max_leaf();
+    std::vector<BBox> tb(n);
+    std::vector<double> cen(3 * (size_t)n);
+    for (uint32_t i = 0; i < n; i++) {
+        for (int a = 0; a < 3; a++) {
+            tb[i].mn[a] = s.lo[a][i];
+            tb[i].mx[a] = s.hi[a][i];
+            cen[3 * (size_t)i + a] = 0.5 * (s.lo[a][i] + s.hi[a][i]);
+        }
+    }
+    struct Job { int32_t node; uint32_t b, e; };
+    w.nodes.push_back(WalkNode{});
+    std::vector<Job> jobs{{0, 0, n}};
+    uint32_t* idx = w.order.data();
+    while (!jobs.empty()) {
+        const Job j = jobs.back();
+        jobs.pop_back();
+        BBox box, cb;
+        for (uint32_t i = j.b; i < j.e; i++) {
+            box.grow(tb[idx[i]]);
+            cb.grow(&cen[3 * (size_t)idx[i]]);
+        }
+        WalkNode& nd = w.nodes[j.node];
+        for (int a = 0; a < 3; a++) { nd.mn[a] = box.mn[a]; nd.mx[a] = box.mx[a]; }
+        const uint32_t cnt = j.e - j.b;
+        auto make_leaf = [&]() {
+            WalkNode& m = w.nodes[j.node];
+            m.first = j.b;
+            m.count = cnt;
+        };
+        if (cnt <= 1) { make_leaf(); continue; }
+        // binned SAH over the three axes (cost in units of one box / triangle test)
+        const double A = box.area();
+        double best = std::numeric_limits<double>::infinity();
+        int best_axis = -1, best_bin = 0;
+        for (int a = 0; a < 3; a++) {
+            const double lo = cb.mn[a], ext = cb.mx[a] - cb.mn[a];
+            if (!(ext > 0.0)) continue;
+            const double scale = kBins / ext;
+            BBox bb[kBins];
+            uint32_t bc[kBins] = {};
+            for (uint32_t i = j.b; i < j.e; i++) {
+                int k = (int)((cen[3 * (size_t)idx[i] + a] - lo) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                bc[k]++;
+                bb[k].grow(tb[idx[i]]);
+            }
+            double ra[kBins];
+            uint32_t rc[kBins];
+            BBox acc;
+            uint32_t c = 0;
+            for (int k = kBins - 1; k > 0; k--) {
+                acc.grow(bb[k]);
+                c += bc[k];
+                ra[k] = acc.area();
+                rc[k] = c;
+            }
+            BBox lacc;
+            uint32_t lc = 0;
+            for (int k = 1; k < kBins; k++) {
+                lacc.grow(bb[k - 1]);
+                lc += bc[k - 1];
+                if (lc == 0 || rc[k] == 0) continue;
+                const double cost = (lacc.area() * lc + ra[k] * rc[k]) / (A > 0 ? A : 1.0);
+                if (cost < best) { best = cost; best_axis = a; best_bin = k; }
+            }
+        }
+        // a leaf costs cnt triangle tests; an inner node one more box test
+        if (cnt <= (uint32_t)LMAX && (best_axis < 0 || (double)cnt <= 1.0 + best)) { make_leaf(); continue; }
+        uint32_t mid;
+        if (best_axis < 0) {
+            mid = j.b + cnt / 2;  // coincident centroids: split the range in half
+        } else {
+            const double lo = cb.mn[best_axis], scale = kBins / (cb.mx[best_axis] - cb.mn[best_axis]);
+            uint32_t* p = std::partition(idx + j.b, idx + j.e, [&](uint32_t t) {
+                int k = (int)((cen[3 * (size_t)t + best_axis] - lo) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                return k < best_bin;
+            });
+            mid = (uint32_t)(p - idx);
+            if (mid == j.b || mid == j.e) mid = j.b + cnt / 2;
+        }
+        const int32_t l = (int32_t)w.nodes.size();
+        w.nodes.push_back(WalkNode{});
+        w.nodes.push_back(WalkNode{});
+        w.nodes[j.node].left = l;
+        w.nodes[j.node].right = l + 1;
+        jobs.push_back({l + 1, mid, j.e});
+        jobs.push_back({l, j.b, mid});
+    }
+    return w;
+}
+
+// Children of binary node b for one W-wide node: open the inner child of
+// largest surface area until W children (or only leaves) remain.
+std::vector<int32_t> collapse_children(const WalkTree& w, int32_t b, int W) {
+    std::vector<int32_t> kids{w.nodes[b].left, w.nodes[b].right};
+    while ((int)kids.size() < W) {
+        int pick = -1;
+        double pa = -1.0;
+        for (int c = 0; c < (int)kids.size(); c++) {
+            const WalkNode& k = w.nodes[kids[c]];
+            if (k.left < 0) continue;
+            BBox bb;
+            for (int a = 0; a < 3; a++) { bb.mn[a] = k.mn[a]; bb.mx[a] = k.mx[a]; }
+            const double ar = bb.area();
+            if (ar > pa) { pa = ar; pick = c; }
+        }
+        if (pick < 0) break;
+        const WalkNode& k = w.nodes[kids[pick]];
+        const int32_t l = k.left, r = k.right;
+        kids[pick] = l;
+        kids.push_back(r);
+    }
+    return kids;
+}
+
+}  // namespace rt

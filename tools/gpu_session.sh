@@ -50,8 +50,8 @@ for s in $STEPS; do
                            "SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_TC_DATA_READ_REQ SQC_TC_STALL SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
                            "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" \
                            "SQC_DCACHE_MISSES_DUPLICATE SQC_DCACHE_REQ_READ_16 SQC_DCACHE_REQ_READ_8 SQC_DCACHE_REQ_READ_4 TCC_TAG_STALL_sum TCC_LATENCY_FIFO_FULL_sum"; do
-                   n=$((${n:-0}+1))
-                   run sq$n 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$n \
+                   pn=$((${pn:-0}+1))
+                   run sq$pn 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$pn \
                        -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu || exit 1
                done
                python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt ;;

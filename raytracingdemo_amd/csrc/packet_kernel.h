@@ -98,6 +98,19 @@
 #define RT_PRIO_STEPS 0
 #endif
 
+// Child refs of the scalar node path: 1 one vector load (lane c: child c),
+// 0 eight v_writelane from the scalar records (measured faster: 131 vs 134
+// us per 1080p frame; the any-mask s_addc chain gains 1.5%).
+#ifndef RT_REF_VLOAD
+#define RT_REF_VLOAD 0
+#endif
+
+// Octant dispatch of the child test: 1 bit-test tree, 0 switch (measured
+// equal: 12.16-12.31 vs 12.15-12.21 Grays/s over three runs each).
+#ifndef RT_OCT_TREE
+#define RT_OCT_TREE 0
+#endif
+
 // Node record fetch: 0 scalar loads (default), 1 uniform vector loads.
 #ifndef RT_NODE_FETCH
 #define RT_NODE_FETCH 0
@@ -156,12 +169,23 @@ __device__ __forceinline__ uint32_t any_bit(uint64_t m) {
     return r;
 }
 
-// Bit c set iff any lane of hm[c] is set (W x two SALU instructions).
+// Bit c set iff any lane of hm[c] is set.
+#ifndef RT_ANY_ADDC
+#define RT_ANY_ADDC 1
+#endif
 template <int W>
 __device__ __forceinline__ uint32_t any_mask(const uint64_t (&hm)[W]) {
     uint32_t m = 0;
+#if RT_ANY_ADDC
+    // two SALU per child: SCC = (mask != 0), then m = 2m + SCC (children
+    // from the last down, so child c lands in bit c)
+#pragma unroll
+    for (int c = W - 1; c >= 0; c--)
+        asm("s_cmp_lg_u64 %1, 0\n\ts_addc_u32 %0, %0, %0" : "+s"(m) : "s"(hm[c]) : "scc");
+#else
     [&]<int... C>(std::integer_sequence<int, C...>) { ((m |= any_bit<1u << C>(hm[C])), ...); }(
         std::make_integer_sequence<int, W>{});
+#endif
     return m;
 }
 
@@ -334,6 +358,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
     const f2 nox{-olx, -ohx}, noy{-oly, -ohy}, noz{-olz, -ohz};
 
     uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0, w_tris = 0;  // COUNT only
+    uint32_t w_narrow = 0, w_slots = 0;  // COUNT only: visits to nodes with <= 4 valid slots, valid slots visited
 #if RT_PREFETCH
     uint32_t pf_sink = 0, pf_val = 0, pf_val2 = 0;  // L2 prefetch loads (values unused)
 #endif
@@ -388,9 +413,16 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                         bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;
                         bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
                     }
+#if RT_REF_VLOAD
+                    // lane c (< W) loads child c's ref with one vector load
+                    // issued alongside the scalar box loads (no writelanes)
+                    refv = reinterpret_cast<const RT_G uint32_t*>(nodes + (size_t)cur * (32 * W))
+                        [8 * (lane & (W - 1)) + RT_CHILD_REF];
+#else
                     // built before any branch so the ref words load with the
                     // boxes, not in a second round trip
                     refv = lanes_of<W>(ch);
+#endif
                     meta = ch[0].pad;
                 }
 #else
@@ -419,6 +451,28 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                 // all lanes' rays share the tile's direction signs (nearly every
                 // tile): the near/far plane of each axis is known, no per-axis
                 // min/max; otherwise the general test
+#if RT_OCT_TREE
+                // binary dispatch on the octant bits (3 uniform branches)
+                if (oct > 7) {
+                    child_hits<W, -1>(bx, q, nox, noy, noz, tcull, hm);
+                } else if (oct & 4) {
+                    if (oct & 2) {
+                        if (oct & 1) child_hits<W, 7>(bx, q, nox, noy, noz, tcull, hm);
+                        else child_hits<W, 6>(bx, q, nox, noy, noz, tcull, hm);
+                    } else {
+                        if (oct & 1) child_hits<W, 5>(bx, q, nox, noy, noz, tcull, hm);
+                        else child_hits<W, 4>(bx, q, nox, noy, noz, tcull, hm);
+                    }
+                } else {
+                    if (oct & 2) {
+                        if (oct & 1) child_hits<W, 3>(bx, q, nox, noy, noz, tcull, hm);
+                        else child_hits<W, 2>(bx, q, nox, noy, noz, tcull, hm);
+                    } else {
+                        if (oct & 1) child_hits<W, 1>(bx, q, nox, noy, noz, tcull, hm);
+                        else child_hits<W, 0>(bx, q, nox, noy, noz, tcull, hm);
+                    }
+                }
+#else
                 switch (oct) {
                     case 0: child_hits<W, 0>(bx, q, nox, noy, noz, tcull, hm); break;
                     case 1: child_hits<W, 1>(bx, q, nox, noy, noz, tcull, hm); break;
@@ -429,6 +483,11 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                     case 6: child_hits<W, 6>(bx, q, nox, noy, noz, tcull, hm); break;
                     case 7: child_hits<W, 7>(bx, q, nox, noy, noz, tcull, hm); break;
                     default: child_hits<W, -1>(bx, q, nox, noy, noz, tcull, hm); break;
+                }
+#endif
+                if (COUNT) {
+                    w_narrow += (meta >> 2) <= 4u;
+                    w_slots += meta >> 2;
                 }
                 uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);
                 if (mask != 0) {
@@ -548,6 +607,8 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
         atomicAdd(&fp.counters[8], (unsigned long long)w_leaves);
         atomicAdd(&fp.counters[9], 1ull);
         atomicAdd(&fp.counters[12], (unsigned long long)w_tris);
+        atomicAdd(&fp.counters[13], (unsigned long long)w_narrow);
+        atomicAdd(&fp.counters[14], (unsigned long long)w_slots);
     }
 #ifdef RT_DIAG_TILECOST
     {   // wave-level visits of this tile into hit_pos[3 * tile + 1 / + 2]
@@ -593,24 +654,49 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
 // closer hit in its LIFO order (stack_bvh.hpp:633).  The winner's ancestor
 // chain is re-verified (the reference must see the triangle); a failure or
 // a candidate-list overflow sends the pixel to k_fixup.
+#ifndef RT_RESOLVE_SPEC
+#define RT_RESOLVE_SPEC 1
+#endif
+#ifndef RT_RESOLVE_WPE
+#define RT_RESOLVE_WPE 0
+#endif
+#if RT_RESOLVE_WPE > 0
+#define RT_RESOLVE_ATTR __attribute__((amdgpu_waves_per_eu(RT_RESOLVE_WPE)))
+#else
+#define RT_RESOLVE_ATTR
+#endif
 template <bool COUNT>
-__global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
+__global__ void __launch_bounds__(256) RT_RESOLVE_ATTR k_resolve(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
     __shared__ uint32_t wave_hits[4];
     // the traversal kernel is done with the tile queues: clear them for the
     // next launch (the packet pipeline needs no memset)
     if (blockIdx.x == 0 && threadIdx.x < RT_QUEUES) aux.tile_ctr[threadIdx.x * RT_QUEUE_STRIDE] = 0;
-    // blocks never straddle frames: frame f owns blocks [f * bpf, (f + 1) * bpf)
+    // One block = one 16x16 pixel tile.  Blocks are dealt to the 8 XCDs
+    // round-robin (block b on XCD b % 8), so block b = 8k + x takes logical
+    // tile x * T8 + k: each XCD resolves one horizontal band of the frame and
+    // the fp64 triangle records of neighbouring pixels stay in its L2.
+    // Blocks never straddle frames: frame f owns blocks [f * bpf, (f + 1) * bpf).
     const uint32_t fpix = (uint32_t)fp.W * (uint32_t)fp.nrows;
-    const uint32_t bpf = (fpix + 255u) / 256u;
+    const uint32_t tx = ((uint32_t)fp.W + 15u) >> 4, ty = ((uint32_t)fp.nrows + 15u) >> 4;
+    const uint32_t T8 = (tx * ty + 7u) >> 3;             // tiles per XCD band
+    const uint32_t bpf = 8u * T8;
     const int f = (int)(blockIdx.x / bpf);
     const uint32_t fb = blockIdx.x - (uint32_t)f * bpf;  // block within the frame
-    const size_t po = (size_t)fb * 256 + threadIdx.x;    // pixel within the frame
-    const bool active = po < fpix;
+    const uint32_t lt = (fb & 7u) * T8 + (fb >> 3);       // logical tile (raster order)
+    const int i = (int)((lt % tx) * 16u + (threadIdx.x & 15u));
+    const int r = (int)((lt / tx) * 16u + (threadIdx.x >> 4));
+    const bool active = lt < tx * ty && i < fp.W && r < fp.nrows;
+    const size_t po = active ? (size_t)r * fp.W + i : 0;  // pixel within the frame
     const size_t npix = (size_t)fpix * fp.nframes;       // candidate-list stride
     const size_t o = out_index(fp, f, po);               // pixel of the batch
-    const int i = (int)(po % (size_t)fp.W), r = (int)(po / (size_t)fp.W);
     const RtFrameCam& cam = fp.cam[f];
     const uint32_t cnt = active ? aux.cand_cnt[o] : 0u;
+    const RT_G uint2* const cl = reinterpret_cast<const RT_G uint2*>(aux.cand);
+#if RT_RESOLVE_SPEC
+    // entry 0 is loaded alongside the count (one dependent round trip less)
+    uint2 e0 = make_uint2(0u, 0u);
+    if (active) e0 = cl[o];
+#endif
     Best out;
     out.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
     out.rank = 0xFFFFFFFFu;
@@ -661,8 +747,12 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
                 for (int a = 0; a < 6; a++) lb[a] = B[a];
             }
         };
-        const RT_G uint2* const cl = reinterpret_cast<const RT_G uint2*>(aux.cand);
+#if RT_RESOLVE_SPEC
+        if (nlist > 0) consider(e0);
+        for (uint32_t c = 1; c < nlist; c++) consider(cl[(size_t)c * npix + o]);
+#else
         for (uint32_t c = 0; c < nlist; c++) consider(cl[(size_t)c * npix + o]);
+#endif
         if (cnt & kCandSpilled) {
             for (uint32_t c = RT_CAND_LDS; c < (uint32_t)RT_CAND_SLOTS; c++) {
                 const uint2 e = cl[(size_t)c * npix + o];

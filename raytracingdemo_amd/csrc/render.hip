@@ -440,7 +440,9 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     if (use_packet(sc.stack_bound)) {
         const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
         // k_resolve: frame f owns blocks [f * bpf, (f + 1) * bpf)
-        const dim3 rgrid((unsigned)(((uint64_t)fp.W * fp.nrows + 255) / 256 * (uint64_t)fp.nframes));
+        // k_resolve: one block per 16x16 tile, 8 XCD bands of T8 tiles per frame
+        const uint64_t rt8 = (((uint64_t)(fp.W + 15) / 16) * ((uint64_t)(fp.nrows + 15) / 16) + 7) / 8;
+        const dim3 rgrid((unsigned)(8 * rt8 * (uint64_t)fp.nframes));
         if (count) {
             hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true>), grid, blk, 0, s,
                                PacketArgs{sc, fp, aux});

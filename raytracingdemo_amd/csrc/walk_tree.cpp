@@ -64,6 +64,17 @@ int max_leaf() {
     return m;
 }
 
+// SAH cost of one inner-node visit relative to one triangle test (the packet
+// kernel's 8-child step and a triangle test cost about the same: DESIGN.md §7)
+double node_cost() {
+    static const double c = [] {
+        const char* e = std::getenv("RT_WALK_CT");
+        const double v = e ? std::atof(e) : 1.0;
+        return v > 0.0 && v < 100.0 ? v : 1.0;
+    }();
+    return c;
+}
+
 }  // namespace
 
 WalkTree build_walk_tree(const Soup& s) {
@@ -140,7 +151,7 @@ WalkTree build_walk_tree(const Soup& s) {
             }
         }
         // a leaf costs cnt triangle tests; an inner node one more box test
-        if (cnt <= (uint32_t)LMAX && (best_axis < 0 || (double)cnt <= 1.0 + best)) { make_leaf(); continue; }
+        if (cnt <= (uint32_t)LMAX && (best_axis < 0 || (double)cnt <= node_cost() + best)) { make_leaf(); continue; }
         uint32_t mid;
         if (best_axis < 0) {
             mid = j.b + cnt / 2;  // coincident centroids: split the range in half

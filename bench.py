@@ -89,18 +89,27 @@ def main():
 
     import raytracingdemo_amd as rt
     from raytracingdemo_amd.scenes import sponza_scene
-    from raytracingdemo_amd.shards import deinterleave, rows_per_rank, shard_rows
+    from raytracingdemo_amd.shards import gather_frames, rows_per_rank, shard_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    # RT_BENCH_REHEARSE=1: rehearse the N-rank path on ONE GPU (every rank on
+    # device 0, gloo over host copies instead of RCCL); numbers are not valid
+    rehearse = world > 1 and os.environ.get("RT_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    coll = (lambda t: t.cpu()) if rehearse else (lambda t: t)  # collective-side tensors
 
     tris, label = sponza_scene()
     scene = rt.Scene(tris, a.algo, a.k).upload([local])
@@ -120,8 +129,9 @@ def main():
     padded = my_rows != rows
     r_ids = torch.empty((F, my_rows, W), dtype=torch.int32, device=dev) if padded else ids
     r_rgb = torch.zeros((F, my_rows, W, 3), dtype=torch.uint8, device=dev) if padded else rgb
-    gather_ids = [torch.empty_like(ids) for _ in range(world)] if (world > 1 and rank == 0) else None
-    gather_rgb = [torch.empty_like(rgb) for _ in range(world)] if (world > 1 and rank == 0) else None
+    # rank 0's gather buffers, allocated once: [world, F, rows, W(, 3)]
+    gather_ids = coll(ids).new_empty((world,) + tuple(ids.shape)) if (world > 1 and rank == 0) else None
+    gather_rgb = coll(rgb).new_empty((world,) + tuple(rgb.shape)) if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev)
     mode = a.mode
 
@@ -136,11 +146,12 @@ def main():
             ids[:, :my_rows] = r_ids
             rgb[:, :my_rows] = r_rgb
         if world > 1:
-            dist.gather(ids, gather_ids, dst=0)
-            dist.gather(rgb, gather_rgb, dst=0)
-            if rank == 0:  # de-interleave: image row j = r*world + rank
-                return deinterleave(torch.stack(gather_rgb), H)
-        return rgb
+            # one RCCL gather per output to rank 0, which de-interleaves
+            # (image row j = r * world + rank) into full frames
+            full_ids = gather_frames(coll(ids), H, world, rank, out=gather_ids)
+            full_rgb = gather_frames(coll(rgb), H, world, rank, out=gather_rgb)
+            return full_ids, full_rgb
+        return ids, rgb
 
     # warm-up with kernel timing on, so the library's per-launch timing events
     # exist before the timed region (they are recycled, not re-created)
@@ -179,6 +190,19 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # multi-rank: the gathered, de-interleaved frames of the last step must
+    # equal a full-image render on rank 0 (outside the timed region)
+    verified = None
+    if world > 1:
+        g_ids, g_rgb = render_step()
+        if rank == 0:
+            f_ids = torch.empty((F, H, W), dtype=torch.int32, device=dev)
+            f_rgb = torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev)
+            scene.render_batch_device(local, cams, W, H, 0, 1, H, hit_id=f_ids.data_ptr(), rgb=f_rgb.data_ptr(),
+                                      stream=stream.cuda_stream, mode=mode)
+            torch.cuda.synchronize(dev)
+            verified = bool(torch.equal(g_ids.to(dev), f_ids) and torch.equal(g_rgb.to(dev), f_rgb))
+        dist.barrier()
     # per-kernel HIP-event times of the timed launches (library stream), and
     # in diagnostic builds the per-wave clock split
     ks = scene.frame_stats(local, reset=True)
@@ -186,6 +210,7 @@ def main():
     tiles_timed = a.steps * F * ((W + 7) // 8) * ((my_rows + 7) // 8)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = coll(t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -226,7 +251,9 @@ def main():
                                    f"{F}-frame camera orbit per step",
                        "width": W, "height": H, "spp": 1, "bvh": f"{a.algo}-{a.k}", "frames_per_step": F,
                        "triangles": int(st["triangles"]), "mode": mode,
-                       "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else "")},
+                       "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else ""),
+                       **({"gather_verified": verified} if world > 1 else {}),
+                       **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_trace_packet" if cs["wave_tiles"] else "k_trace_exact",

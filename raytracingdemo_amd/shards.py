@@ -30,3 +30,20 @@ def deinterleave(gathered, H: int):
     perm = (1, 2, 0) + tuple(range(3, nd))
     full = gathered.permute(*perm).reshape((F, rows * world) + rest)
     return full[:, :H]
+
+
+def gather_frames(shard, H: int, world: int, rank: int, dst: int = 0, out=None):
+    """Gather every rank's [F, rows, W, ...] shard to `dst` and de-interleave there.
+
+    The shards land in one [world, F, rows, W, ...] buffer (`out`, allocated
+    once by the caller, or here) through views of it, so the collective writes
+    straight into the layout `deinterleave` reads: one copy in all.  Returns
+    [F, H, W, ...] on `dst`, None elsewhere.
+    """
+    import torch.distributed as dist
+    if rank == dst:
+        buf = out if out is not None else shard.new_empty((world,) + tuple(shard.shape))
+        dist.gather(shard, list(buf.unbind(0)), dst=dst)
+        return deinterleave(buf, H)
+    dist.gather(shard, None, dst=dst)
+    return None

@@ -18,7 +18,7 @@ torch = pytest.importorskip("torch")
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
-from raytracingdemo_amd.shards import deinterleave, rows_per_rank, shard_rows  # noqa: E402
+from raytracingdemo_amd.shards import deinterleave, gather_frames, rows_per_rank, shard_rows  # noqa: E402
 
 
 def _free_port() -> int:
@@ -52,10 +52,9 @@ def _worker(rank: int, world: int, port: int, W: int, H: int, F: int, q):
         mine = list(shard_rows(rank, world, H))
         shard = torch.full((F, rows, W, 3), 255, dtype=torch.uint8)  # padding rows stay 255
         shard[:, : len(mine)] = torch.from_numpy(full[:, mine])
-        gathered = [torch.empty_like(shard) for _ in range(world)] if rank == 0 else None
-        dist.gather(shard, gathered, dst=0)
+        img = gather_frames(shard, H, world, rank)  # the bench's gather + de-interleave
         if rank == 0:
-            img = deinterleave(torch.stack(gathered), H).numpy()
+            img = img.numpy()
             q.put(("ok", bool(np.array_equal(img, full)), img.shape))
     except Exception as e:  # surface worker failures to the test
         q.put(("err", repr(e), None))

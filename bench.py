@@ -239,6 +239,17 @@ def main():
                 traffic = round(float(pm["hbm_bytes_per_launch"]))
         except (OSError, ValueError, KeyError):
             pass
+        # VALU issue utilisation of the same kernel (committed SQ PMC passes,
+        # tools/pmc_valu.py): the walk is issue-bound, not HBM-bound
+        valu = None
+        try:
+            pv = json.load(open(os.path.join(ROOT, "profiles", "pmc_valu.json")))
+            if pv.get("workload_key") == key:
+                valu = {"busy": pv["valu_busy"], "insts_per_launch": pv["valu_insts_per_launch"],
+                        "salu_insts_per_launch": pv["salu_insts_per_launch"],
+                        "wave_cycles_split": pv["wave_cycles_split"], "source": "profiles/pmc_valu.json"}
+        except (OSError, ValueError, KeyError):
+            pass
         cpu = None
         if world == 1 and not a.no_cpu:
             cpu = cpu_baseline(tris, a.algo, a.k, cams, W, H, a.cpu_seconds)
@@ -255,7 +266,7 @@ def main():
                        **({"gather_verified": verified} if world > 1 else {}),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "valu": valu,
                          "kernel": "k_trace_packet" if cs["wave_tiles"] else "k_trace_exact",
                          "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(alg_bytes_per_launch),

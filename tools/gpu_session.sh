@@ -52,9 +52,10 @@ for s in $STEPS; do
                            "SQC_DCACHE_MISSES_DUPLICATE SQC_DCACHE_REQ_READ_16 SQC_DCACHE_REQ_READ_8 SQC_DCACHE_REQ_READ_4 TCC_TAG_STALL_sum TCC_LATENCY_FIFO_FULL_sum"; do
                    pn=$((${pn:-0}+1))
                    run sq$pn 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$pn \
-                       -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu || exit 1
+                       -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu --key-out gpurun_out/pmc_key.txt || exit 1
                done
-               python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt ;;
+               python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt
+               python tools/pmc_valu.py gpurun_out/pmc_key.txt gpurun_out/pmc_valu.json gpurun_out/sq/sq*_counter_collection.csv ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""VALU issue utilisation of the traversal kernel from the rocprofv3 SQ passes
+of `tools/gpu_session.sh sq` (north_star asks for VALU-utilisation counters
+beside the HBM roofline).
+
+  busy = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)
+
+A wave64 VALU instruction occupies a SIMD-32 for 2 cycles (MI355X_MICROARCH.md,
+"Wave scheduling"); GRBM_GUI_ACTIVE is summed over the 8 XCDs.  The non-
+counting dispatch of one 12-frame launch is used.
+
+Usage: tools/pmc_valu.py KEY_FILE OUT_JSON SQ_CSV [SQ_CSV ...]
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def main():
+    key_file, out = sys.argv[1:3]
+    tot = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for path in sys.argv[3:]:
+        for r in csv.DictReader(open(path)):
+            n = r["Kernel_Name"]
+            if "k_trace_packet" not in n or "true>" in n:
+                continue
+            tot[r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[r["Counter_Name"]].add((path, r["Dispatch_Id"]))
+    per = {c: tot[c] / max(len(disp[c]), 1) for c in tot}  # per dispatch
+    cycles = per["GRBM_GUI_ACTIVE"] / 8.0
+    valu = per["SQ_INSTS_VALU"]
+    res = {
+        "workload_key": open(key_file).read().strip(),
+        "kernel": "k_trace_packet",
+        "valu_insts_per_launch": valu,
+        "salu_insts_per_launch": per.get("SQ_INSTS_SALU"),
+        "cycles_per_xcd": cycles,
+        "valu_busy": round(valu * 2.0 / (1024.0 * cycles), 4),
+        "wave_cycles_split": {k: round(per[k] / per["SQ_WAVE_CYCLES"], 4)
+                              for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                                        "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_ANY") if k in per},
+        "method": "rocprofv3 --pmc SQ passes (tools/gpu_session.sh sq); busy = SQ_INSTS_VALU x 2 / "
+                  "(1024 SIMDs x GRBM_GUI_ACTIVE/8)",
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -175,6 +175,20 @@ int rt_render_rows_device(rt_scene *s, int device, const rt_camera *cam, int mod
 int rt_render_batch_device(rt_scene *s, int device, const rt_camera *cams, int nframes, int mode, int row0,
                            int row_stride, int nrows, const rt_device_out *out, void *stream, uint32_t flags);
 
+/* rt_render_batch_device with spp samples per pixel (spp = n*n: 1, 4, 9 or
+ * 16), stratified: sample s of a pixel is shot through sub-pixel offset
+ * (((s % n) + 0.5) / n, ((s / n) + 0.5) / n) in place of the reference's
+ * pixel centre (0.5, 0.5) (camera.hpp:35-37; SURVEY.md §8(d) config c4 uses
+ * the 2x2 pattern).  Per-sample outputs (hit_id, dist, pos) of pose f, pixel
+ * o, sample s are at (f * width * nrows + o) * spp + s; the colour (rgb) of
+ * pixel o is shadeScreen's colour (main.cpp:356-377) summed over the samples
+ * in order from 0.0, divided by spp, then cast as Benchmark::saveScreen does
+ * (benchmark.hpp:105-114); hit_count[f] counts the samples that hit.  spp = 1
+ * is rt_render_batch_device exactly. */
+int rt_render_batch_spp_device(rt_scene *s, int device, const rt_camera *cams, int nframes, int spp, int mode,
+                               int row0, int row_stride, int nrows, const rt_device_out *out, void *stream,
+                               uint32_t flags);
+
 /* Read (and optionally reset) the per-device counters filled by
  * RT_FLAG_COUNT renders (synchronises the device). */
 int rt_frame_stats(rt_scene *s, int device, int reset, rt_frame_stats_t *out);

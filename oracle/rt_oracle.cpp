@@ -898,6 +898,69 @@ long long orc_render(const orc_bvh* h, const double cam_pos[3], const double cam
     return hits;
 }
 
+// Stratified multi-sample frame (build-defined extension, SURVEY.md §8(d)
+// config c4; include/rt.h rt_render_batch_spp_device): spp = n*n samples per
+// pixel at sub-pixel offsets (((s % n) + 0.5) / n, ((s / n) + 0.5) / n) in
+// place of camera.hpp:35-37's 0.5; per-sample outputs at
+// ((j-row0)*W + i)*spp + s; the pixel colour is the samples' shadeScreen
+// colours summed in sample order from 0.0, divided by spp, then cast.
+// Returns the number of samples that hit, or -1.
+long long orc_render_spp(const orc_bvh* h, const double cam_pos[3], const double cam_dir[3], int W, int H,
+                         int row0, int nrows, int spp, int threads, int32_t* hit_id, double* hit_pos,
+                         double* hit_dist, uint8_t* rgb) {
+    if (W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H) { g_err = "bad frame geometry"; return -1; }
+    int g = 1;
+    while ((g + 1) * (g + 1) <= spp) g++;
+    if (spp < 1 || g * g != spp) { g_err = "spp must be n*n"; return -1; }
+    const double fov = 90.0 * (std::numbers::pi / 180.0);
+    const double th = std::tan(fov * 0.5);
+    const double aspect = static_cast<double>(W) / H;
+    const double iw = 1.0 / W, ih = 1.0 / H;
+    const V3 cp{cam_pos[0], cam_pos[1], cam_pos[2]};
+    const V3 cd{cam_dir[0], cam_dir[1], cam_dir[2]};
+    V3 right, up;
+    basis(cd, right, up);
+    long long hits = 0;
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : hits)
+#endif
+    for (int i = 0; i < W; ++i) {
+        std::vector<int> st;
+        st.reserve(64);
+        TravStats ts;
+        for (int j = row0; j < row0 + nrows; ++j) {
+            const size_t o = (size_t)(j - row0) * W + i;
+            double acc[3] = {0.0, 0.0, 0.0};
+            for (int s = 0; s < spp; ++s) {
+                const double ox = ((double)(s % g) + 0.5) / (double)g, oy = ((double)(s / g) + 0.5) / (double)g;
+                const double px = (2.0 * (i + ox) * iw - 1.0) * th * aspect;
+                const double py = (1.0 - 2.0 * (j + oy) * ih) * th;
+                V3 d = add(add(cd, mul(up, py)), mul(right, px));
+                d = mul(d, 1.0 / length(d));
+                Ray r = make_ray(cp, d);
+                V3 pos;
+                double dist;
+                const int id = traverse(h->b, r, pos, dist, st, ts);
+                const size_t so = o * spp + s;
+                if (hit_id) hit_id[so] = id;
+                if (hit_pos) { hit_pos[so * 3] = pos.x; hit_pos[so * 3 + 1] = pos.y; hit_pos[so * 3 + 2] = pos.z; }
+                if (hit_dist) hit_dist[so] = id >= 0 ? dist : -1.0;
+                V3 nrm{0, 0, 0};
+                if (id >= 0) { nrm = h->b.tris[id].normal; hits++; }
+                double c[3];
+                shade(id >= 0, pos, nrm, cp, c);
+                acc[0] = acc[0] + c[0];
+                acc[1] = acc[1] + c[1];
+                acc[2] = acc[2] + c[2];
+            }
+            if (rgb)
+                for (int k = 0; k < 3; k++) rgb[o * 3 + k] = to_byte(acc[k] / (double)spp);
+        }
+    }
+    return hits;
+}
+
 int orc_max_threads() {
 #ifdef _OPENMP
     return omp_get_max_threads();

@@ -195,18 +195,21 @@ class Scene:
 
     def render_batch_device(self, device: int, cams, W: int, H: int, row0: int, row_stride: int, nrows: int,
                             hit_id=0, dist=0, hit_pos=0, rgb=0, hit_count=0, stream=0, mode: str = "exact",
-                            count: bool = False, timing: bool = False):
+                            count: bool = False, timing: bool = False, spp: int = 1):
         """Asynchronous shard render of several poses ``cams`` = [(pos, dir), ...]
-        (runTest's camera loop, src/main.cpp:234-281) into device pointers: frame
-        f's outputs start f * W * nrows pixels in, its hit counter is hit_count[f]."""
+        (runTest's camera loop, src/main.cpp:234-281) into device pointers: pose
+        f's outputs start f * W * nrows pixels in (per-sample outputs: times spp),
+        its hit counter is hit_count[f].  spp = n*n stratified samples per pixel
+        (include/rt.h rt_render_batch_spp_device)."""
         n = len(cams)
         arr = (N.rt_camera * max(n, 1))(*[_camera(p, d, W, H) for p, d in cams])
         o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
         m = N.RT_MODE_FP64 if mode in ("fp64", "literal") else N.RT_MODE_EXACT
-        N.check(N.lib().rt_render_batch_device(self._h, int(device), arr, n, m, int(row0), int(row_stride),
-                                               int(nrows), C.byref(o), C.c_void_p(stream or None),
-                                               (N.RT_FLAG_COUNT if count else 0) |
-                                               (N.RT_FLAG_TIMING if timing else 0)))
+        N.check(N.lib().rt_render_batch_spp_device(self._h, int(device), arr, n, int(spp), m, int(row0),
+                                                   int(row_stride), int(nrows), C.byref(o),
+                                                   C.c_void_p(stream or None),
+                                                   (N.RT_FLAG_COUNT if count else 0) |
+                                                   (N.RT_FLAG_TIMING if timing else 0)))
 
     def frame_stats(self, device: int = 0, reset: bool = True) -> dict:
         s = N.rt_frame_stats_t()

@@ -181,11 +181,14 @@ __device__ __forceinline__ int tri_classify(const float4 A, const float4 B, cons
 
 // Camera pixel caches (camera.hpp:35-37), evaluated per pixel in the same
 // operation order as the host's pixel_caches (no contraction): bit-identical.
-__device__ __forceinline__ double pixel_x(const RtFrameParams& fp, int x) {
-    return (2.0 * ((double)x + 0.5) * fp.cam_iw - 1.0) * fp.cam_half * fp.cam_aspect;
+// ox / oy: the sample's offset inside the pixel; the reference's pixel centre
+// is 0.5 (x + 0.5 exactly as camera.hpp:35-37), stratified samples use
+// (k + 0.5) / n.
+__device__ __forceinline__ double pixel_x(const RtFrameParams& fp, const RtFrameCam& cam, int x) {
+    return (2.0 * ((double)x + cam.ox) * fp.cam_iw - 1.0) * fp.cam_half * fp.cam_aspect;
 }
-__device__ __forceinline__ double pixel_y(const RtFrameParams& fp, int y) {
-    return (1.0 - 2.0 * ((double)y + 0.5) * fp.cam_ih) * fp.cam_half;
+__device__ __forceinline__ double pixel_y(const RtFrameParams& fp, const RtFrameCam& cam, int y) {
+    return (1.0 - 2.0 * ((double)y + cam.oy) * fp.cam_ih) * fp.cam_half;
 }
 
 // main.cpp:332-337: d = dir + up*py + right*px; d *= 1/|d|; Ray{pos, d}
@@ -193,7 +196,7 @@ __device__ __forceinline__ double pixel_y(const RtFrameParams& fp, int y) {
 // when it falls back to the chain walk (with_inv).
 template <bool INV = true>
 __device__ __forceinline__ Ray64 gen_ray(const RtFrameParams& fp, const RtFrameCam& cam, int i, int j) {
-    const double px = pixel_x(fp, i), py = pixel_y(fp, j);
+    const double px = pixel_x(fp, cam, i), py = pixel_y(fp, cam, j);
     double dx = (cam.dir[0] + cam.up[0] * py) + cam.right[0] * px;
     double dy = (cam.dir[1] + cam.up[1] * py) + cam.right[1] * px;
     double dz = (cam.dir[2] + cam.up[2] * py) + cam.right[2] * px;
@@ -262,48 +265,68 @@ __device__ __forceinline__ Shade shade_of(const RtDevScene& sc, int32_t tri) {
     }
     return s;
 }
-// Output slot of pixel o (row-major in the shard) of frame f of the launch.
+// Output slot of pixel o (row-major in the shard) of frame f of the launch
+// (spp = 1: frame = pose).
 __device__ __forceinline__ size_t out_index(const RtFrameParams& fp, int f, size_t o) {
     return (size_t)f * ((size_t)fp.W * (size_t)fp.nrows) + o;
 }
+// shadeScreen's colour of one sample before the byte cast (main.cpp:356-377):
+// (0.5 (n + 1)) * I per channel, 0 on a miss.
+__device__ __forceinline__ void shade_color(const RtFrameCam& cam, const Best& b, const Shade& sh, double c[3]) {
+    c[0] = c[1] = c[2] = 0.0;
+    if (b.tri < 0) return;
+    // the record holds the normal already normalised as shadeScreen does
+    // it (main.cpp:361; bvh_build.cpp flatten, same IEEE operations)
+    const double nx = sh.nx, ny = sh.ny, nz = sh.nz;
+    double lx = cam.pos[0] - b.px, ly = cam.pos[1] - b.py, lz = cam.pos[2] - b.pz;
+    // the light sits at the ray origin, so |light - p| is bit-for-bit the
+    // hit distance hit_dist returned ((o - p) = -(p - o) exactly, same
+    // sum order): reuse it instead of a second fp64 sqrt
+    const double dist = b.dist;
+    if (dist > 0.0) {
+        const double s = 1.0 / dist;
+        lx = lx * s; ly = ly * s; lz = lz * s;
+    }
+    const double diffuse = smax(0.0, nx * lx + ny * ly + nz * lz) * 1.35;
+    const double att = 1.0 / (1.0 + 0.05 * dist * dist);
+    const double I = sclamp((0.45 + diffuse * att) * 1.25, 0.0, 1.0);
+    c[0] = (0.5 * (nx + 1.0)) * I;
+    c[1] = (0.5 * (ny + 1.0)) * I;
+    c[2] = (0.5 * (nz + 1.0)) * I;
+}
+// Per-sample outputs (hit id, distance, position) at sample slot `so`.
+__device__ __forceinline__ void store_sample(const RtFrameParams& fp, size_t so, const Best& b, const Shade& sh) {
+    if (fp.hit_id) fp.hit_id[so] = b.tri >= 0 ? sh.id : RT_INVALID_REF;
+    if (fp.dist) fp.dist[so] = b.tri >= 0 ? b.dist : -1.0;
+#if !defined(RT_DIAG_TILECOST) && !defined(RT_DIAG_WAVES)
+    if (fp.hit_pos) {
+        fp.hit_pos[3 * so] = b.tri >= 0 ? b.px : 0.0;
+        fp.hit_pos[3 * so + 1] = b.tri >= 0 ? b.py : 0.0;
+        fp.hit_pos[3 * so + 2] = b.tri >= 0 ? b.pz : 0.0;
+    }
+#endif
+}
+// Pixel colour as PPM bytes (benchmark.hpp:105-114 truncating cast) from the
+// sum of its samples' colours (summed in sample order from 0.0): the mean
+// c / spp; for spp = 1 that is the reference's c * 255 bit for bit.
+__device__ __forceinline__ void store_rgb(const RtFrameParams& fp, size_t po, const double c[3]) {
+    if (!fp.rgb) return;
+    const double n = (double)fp.spp;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const double m = fp.spp == 1 ? c[k] : c[k] / n;  // (c / 1 == c: skip the division)
+        fp.rgb[3 * po + k] = (uint8_t)sclamp(m * 255.0, 0.0, 255.0);
+    }
+}
+// spp = 1 store of one pixel of frame f: per-sample outputs, colour and (one
+// atomic per wave) the frame's hit count.
 __device__ __forceinline__ void shade_store(const RtFrameParams& fp, const RtFrameCam& cam, int f, size_t o,
                                             const Best& b, const Shade& sh, bool count_hit = true) {
     o = out_index(fp, f, o);
-    uint8_t c0 = 0, c1 = 0, c2 = 0;
-    if (b.tri >= 0 && fp.rgb) {
-        // the record holds the normal already normalised as shadeScreen does
-        // it (main.cpp:361; bvh_build.cpp flatten, same IEEE operations)
-        const double nx = sh.nx, ny = sh.ny, nz = sh.nz;
-        double lx = cam.pos[0] - b.px, ly = cam.pos[1] - b.py, lz = cam.pos[2] - b.pz;
-        // the light sits at the ray origin, so |light - p| is bit-for-bit the
-        // hit distance hit_dist returned ((o - p) = -(p - o) exactly, same
-        // sum order): reuse it instead of a second fp64 sqrt
-        const double dist = b.dist;
-        if (dist > 0.0) {
-            const double s = 1.0 / dist;
-            lx = lx * s; ly = ly * s; lz = lz * s;
-        }
-        const double diffuse = smax(0.0, nx * lx + ny * ly + nz * lz) * 1.35;
-        const double att = 1.0 / (1.0 + 0.05 * dist * dist);
-        const double I = sclamp((0.45 + diffuse * att) * 1.25, 0.0, 1.0);
-        c0 = (uint8_t)sclamp((0.5 * (nx + 1.0)) * I * 255.0, 0.0, 255.0);
-        c1 = (uint8_t)sclamp((0.5 * (ny + 1.0)) * I * 255.0, 0.0, 255.0);
-        c2 = (uint8_t)sclamp((0.5 * (nz + 1.0)) * I * 255.0, 0.0, 255.0);
-    }
-    if (fp.rgb) {
-        fp.rgb[3 * o] = c0;
-        fp.rgb[3 * o + 1] = c1;
-        fp.rgb[3 * o + 2] = c2;
-    }
-    if (fp.hit_id) fp.hit_id[o] = b.tri >= 0 ? sh.id : RT_INVALID_REF;
-    if (fp.dist) fp.dist[o] = b.tri >= 0 ? b.dist : -1.0;
-#if !defined(RT_DIAG_TILECOST) && !defined(RT_DIAG_WAVES)
-    if (fp.hit_pos) {
-        fp.hit_pos[3 * o] = b.tri >= 0 ? b.px : 0.0;
-        fp.hit_pos[3 * o + 1] = b.tri >= 0 ? b.py : 0.0;
-        fp.hit_pos[3 * o + 2] = b.tri >= 0 ? b.pz : 0.0;
-    }
-#endif
+    double c[3];
+    shade_color(cam, b, sh, c);
+    store_rgb(fp, o, c);
+    store_sample(fp, o, b, sh);
     if (count_hit && fp.hit_count) {  // one atomic per wave (all active lanes reach this)
         const uint64_t hits = __ballot(b.tri >= 0);
         const uint64_t act = __ballot(1);

@@ -665,30 +665,15 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
 #else
 #define RT_RESOLVE_ATTR
 #endif
+// Exact resolve of one sample (frame f of the launch, pixel (i, r), batch
+// pixel index o of the candidate lists): the winner, its shading inputs, and
+// whether the pixel must be redone (1: a dropped candidate could win, 2: the
+// reference cannot see the winner).
 template <bool COUNT>
-__global__ void __launch_bounds__(256) RT_RESOLVE_ATTR k_resolve(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
-    __shared__ uint32_t wave_hits[4];
-    // the traversal kernel is done with the tile queues: clear them for the
-    // next launch (the packet pipeline needs no memset)
-    if (blockIdx.x == 0 && threadIdx.x < RT_QUEUES) aux.tile_ctr[threadIdx.x * RT_QUEUE_STRIDE] = 0;
-    // One block = one 16x16 pixel tile.  Blocks are dealt to the 8 XCDs
-    // round-robin (block b on XCD b % 8), so block b = 8k + x takes logical
-    // tile x * T8 + k: each XCD resolves one horizontal band of the frame and
-    // the fp64 triangle records of neighbouring pixels stay in its L2.
-    // Blocks never straddle frames: frame f owns blocks [f * bpf, (f + 1) * bpf).
-    const uint32_t fpix = (uint32_t)fp.W * (uint32_t)fp.nrows;
-    const uint32_t tx = ((uint32_t)fp.W + 15u) >> 4, ty = ((uint32_t)fp.nrows + 15u) >> 4;
-    const uint32_t T8 = (tx * ty + 7u) >> 3;             // tiles per XCD band
-    const uint32_t bpf = 8u * T8;
-    const int f = (int)(blockIdx.x / bpf);
-    const uint32_t fb = blockIdx.x - (uint32_t)f * bpf;  // block within the frame
-    const uint32_t lt = (fb & 7u) * T8 + (fb >> 3);       // logical tile (raster order)
-    const int i = (int)((lt % tx) * 16u + (threadIdx.x & 15u));
-    const int r = (int)((lt / tx) * 16u + (threadIdx.x >> 4));
-    const bool active = lt < tx * ty && i < fp.W && r < fp.nrows;
-    const size_t po = active ? (size_t)r * fp.W + i : 0;  // pixel within the frame
-    const size_t npix = (size_t)fpix * fp.nframes;       // candidate-list stride
-    const size_t o = out_index(fp, f, po);               // pixel of the batch
+__device__ __forceinline__ void resolve_sample(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux,
+                                               int f, int i, int r, size_t o, size_t npix, bool active, Best& out,
+                                               Shade& sh, uint32_t& redo, uint32_t& n_tris, uint32_t& n_chain,
+                                               uint32_t& n_chain_nodes) {
     const RtFrameCam& cam = fp.cam[f];
     const uint32_t cnt = active ? aux.cand_cnt[o] : 0u;
     const RT_G uint2* const cl = reinterpret_cast<const RT_G uint2*>(aux.cand);
@@ -697,14 +682,13 @@ __global__ void __launch_bounds__(256) RT_RESOLVE_ATTR k_resolve(RtDevScene sc, 
     uint2 e0 = make_uint2(0u, 0u);
     if (active) e0 = cl[o];
 #endif
-    Best out;
     out.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
     out.rank = 0xFFFFFFFFu;
     out.tri = -1;
     out.px = out.py = out.pz = 0.0;
-    uint32_t redo = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0;
+    sh = Shade{0.0, 0.0, 0.0, RT_INVALID_REF};
+    redo = 0;
     const uint32_t nlist = cnt & kCandCount;
-    Shade sh{0.0, 0.0, 0.0, RT_INVALID_REF};
     if (cnt != 0) {
         const Ray64 ray = gen_ray<false>(fp, cam, i, fp.row0 + r * fp.row_stride);
         double best_t = 0.0;
@@ -778,32 +762,90 @@ __global__ void __launch_bounds__(256) RT_RESOLVE_ATTR k_resolve(RtDevScene sc, 
                 redo = 2;
         }
     }
-    if (active) {
-        if (redo) {
-            const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-            aux.redo[slot] = (uint32_t)o | (redo == 2u ? kRedoPass1 : 0u);
-        } else {
-            shade_store(fp, cam, f, po, out, sh, false);
+}
+
+// One pixel per lane over all spp samples of its pose; one block per 16x16
+// tile of one pose.  MULTI = false: spp == 1, the straight-line reference
+// path (no sample loop, 76 instead of 105 VGPRs).
+template <bool COUNT, bool MULTI>
+__global__ void __launch_bounds__(256) RT_RESOLVE_ATTR k_resolve(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
+    __shared__ uint32_t wave_hits[4];
+    // the traversal kernel is done with the tile queues: clear them for the
+    // next launch (the packet pipeline needs no memset)
+    if (blockIdx.x == 0 && threadIdx.x < RT_QUEUES) aux.tile_ctr[threadIdx.x * RT_QUEUE_STRIDE] = 0;
+    // One block = one 16x16 pixel tile.  Blocks are dealt to the 8 XCDs
+    // round-robin (block b on XCD b % 8), so block b = 8k + x takes logical
+    // tile x * T8 + k: each XCD resolves one horizontal band of the pose.
+    // Blocks never straddle poses: pose p owns blocks [p * bpf, (p + 1) * bpf).
+    const uint32_t fpix = (uint32_t)fp.W * (uint32_t)fp.nrows;
+    const uint32_t tx = ((uint32_t)fp.W + 15u) >> 4, ty = ((uint32_t)fp.nrows + 15u) >> 4;
+    const uint32_t T8 = (tx * ty + 7u) >> 3;             // tiles per XCD band
+    const uint32_t bpf = 8u * T8;
+    const int p = (int)(blockIdx.x / bpf);
+    const uint32_t fb = blockIdx.x - (uint32_t)p * bpf;  // block within the pose
+    const uint32_t lt = (fb & 7u) * T8 + (fb >> 3);       // logical tile (raster order)
+    const int i = (int)((lt % tx) * 16u + (threadIdx.x & 15u));
+    const int r = (int)((lt / tx) * 16u + (threadIdx.x >> 4));
+    const bool active = lt < tx * ty && i < fp.W && r < fp.nrows;
+    const size_t po = active ? (size_t)r * fp.W + i : 0;  // pixel within the frame
+    const size_t npix = (size_t)fpix * fp.nframes;       // candidate-list stride
+    const size_t pix = out_index(fp, p, po);             // pixel of the pose outputs
+    uint32_t redo_any = 0, hits = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_redo[3] = {0, 0, 0};
+    double acc[3] = {0.0, 0.0, 0.0};
+    const int spp = MULTI ? fp.spp : 1;
+    for (int k = 0; k < spp; k++) {
+        const int f = p * spp + k;
+        Best out;
+        Shade sh;
+        uint32_t redo;
+        resolve_sample<COUNT>(sc, fp, aux, f, i, r, out_index(fp, f, po), npix, active, out, sh, redo, n_tris,
+                              n_chain, n_chain_nodes);
+        if (COUNT) n_redo[redo]++;
+        redo_any = redo_any > redo ? redo_any : redo;
+        if (active && !redo) {
+            store_sample(fp, pix * (size_t)spp + k, out, sh);
+            if (MULTI) {
+                double c[3];
+                shade_color(fp.cam[f], out, sh, c);
+                acc[0] = acc[0] + c[0];
+                acc[1] = acc[1] + c[1];
+                acc[2] = acc[2] + c[2];
+            } else {
+                shade_color(fp.cam[f], out, sh, acc);  // the sample's colour is the pixel's
+            }
+            hits += out.tri >= 0;
         }
     }
-    // hit count: block sums spread over RT_HIT_SLOTS counters (k_fixup adds
-    // them up) instead of same-address device atomics, which serialise
-    const uint64_t hits = __ballot(active && !redo && out.tri >= 0);
-    if ((threadIdx.x & 63) == 0) wave_hits[threadIdx.x >> 6] = (uint32_t)__builtin_popcountll(hits);
+    if (active) {
+        if (redo_any) {
+            // k_fixup redoes every sample of the pixel with the exact per-lane path
+            const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
+            aux.redo[slot] = (uint32_t)pix | (redo_any == 2u && !MULTI ? kRedoPass1 : 0u);
+            hits = 0;
+        } else {
+            store_rgb(fp, pix, acc);
+        }
+    }
+    // hit count (samples hit): block sums spread over RT_HIT_SLOTS counters
+    // per pose (k_fixup adds them up) instead of same-address device atomics
+    uint32_t wsum = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) wsum += (uint32_t)__builtin_popcountll(__ballot((hits >> b) & 1u)) << b;
+    if ((threadIdx.x & 63) == 0) wave_hits[threadIdx.x >> 6] = wsum;
     __syncthreads();
     if (threadIdx.x == 0 && fp.hit_count) {
         const uint32_t sum = wave_hits[0] + wave_hits[1] + wave_hits[2] + wave_hits[3];
-        if (sum) atomicAdd(aux.tile_ctr + RT_HIT_BASE + (f * RT_HIT_SLOTS + fb % RT_HIT_SLOTS) * RT_QUEUE_STRIDE, sum);
+        if (sum) atomicAdd(aux.tile_ctr + RT_HIT_BASE + (p * RT_HIT_SLOTS + fb % RT_HIT_SLOTS) * RT_QUEUE_STRIDE, sum);
     }
     if (!active) return;
     if (COUNT && fp.counters) {
-        atomicAdd(&fp.counters[0], 1ull);
+        atomicAdd(&fp.counters[0], (unsigned long long)spp);
         atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
         atomicAdd(&fp.counters[3], (unsigned long long)n_chain);
-        if (!redo && out.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
+        if (hits) atomicAdd(&fp.counters[4], (unsigned long long)hits);
         atomicAdd(&fp.counters[5], (unsigned long long)n_chain_nodes);
-        if (redo == 1) atomicAdd(&fp.counters[10], 1ull);
-        if (redo == 2) atomicAdd(&fp.counters[11], 1ull);
+        if (n_redo[1]) atomicAdd(&fp.counters[10], (unsigned long long)n_redo[1]);
+        if (n_redo[2]) atomicAdd(&fp.counters[11], (unsigned long long)n_redo[2]);
     }
 }
 

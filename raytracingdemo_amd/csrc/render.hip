@@ -102,7 +102,7 @@ struct Win {
 // Fast exact kernel (persistent).
 // --------------------------------------------------------------------------
 template <int W, int S, bool COUNT>
-__device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
+__device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
                                             LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
     constexpr int G = W < 4 ? W : 4;  // children tested per load group
     const int j = fp.row0 + r * fp.row_stride;
@@ -258,8 +258,6 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
         const Ray64 ray = gen_ray(fp, cam, opaque(i), j);
         (void)hit_dist(ray, best.t, out.px, out.py, out.pz);
     }
-    const size_t o = (size_t)r * fp.W + i;
-    shade_store(fp, cam, f, sc, o, out);
     if (COUNT && fp.counters) {
         if (!fixup) atomicAdd(&fp.counters[0], 1ull);  // a fixed-up ray was counted by the packet kernel
         atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
@@ -269,6 +267,40 @@ __device__ __forceinline__ void trace_exact(const RtDevScene& sc, const RtFrameP
         atomicAdd(&fp.counters[5], (unsigned long long)n_chain_nodes);
         atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
     }
+    return out;
+}
+
+// Adds each active lane's v (0..31) to *p with one atomic per wave.
+__device__ __forceinline__ void wave_add(RT_G unsigned long long* p, uint32_t v) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) sum += (uint32_t)__builtin_popcountll(__ballot((v >> b) & 1u)) << b;
+    const uint64_t act = __ballot(1);
+    if (p && sum != 0 && (int)(threadIdx.x & 63) == __builtin_ctzll(act)) atomicAdd(p, (unsigned long long)sum);
+}
+
+// All spp samples of pixel (i, r) of pose p with the per-lane exact kernel:
+// per-sample outputs, the averaged colour and the pose's hit count.
+template <int W, int S, bool COUNT>
+__device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameParams& fp, int p, int i, int r,
+                                            LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
+    const size_t po = out_index(fp, p, (size_t)r * fp.W + i);
+    double acc[3] = {0.0, 0.0, 0.0};
+    uint32_t hits = 0;
+    for (int k = 0; k < fp.spp; k++) {
+        const int f = p * fp.spp + k;
+        const Best b = trace_exact<W, S, COUNT>(sc, fp, f, i, r, st, pass0, fixup);
+        const Shade sh = shade_of(sc, b.tri);
+        store_sample(fp, po * (size_t)fp.spp + k, b, sh);
+        double c[3];
+        shade_color(fp.cam[f], b, sh, c);
+        acc[0] = acc[0] + c[0];
+        acc[1] = acc[1] + c[1];
+        acc[2] = acc[2] + c[2];
+        hits += b.tri >= 0;
+    }
+    store_rgb(fp, po, acc);
+    wave_add(fp.hit_count ? fp.hit_count + p : nullptr, hits);
 }
 
 #include "packet_kernel.h"
@@ -286,12 +318,13 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
         // fold k_resolve's per-frame hit-count partials into the caller's counters
         if (tid < RT_MAX_BATCH) frame_sum[tid] = 0;
         __syncthreads();
-        for (int k = tid; k < fp.nframes * RT_HIT_SLOTS; k += 256) {
+        const int poses = fp.nframes / fp.spp;
+        for (int k = tid; k < poses * RT_HIT_SLOTS; k += 256) {
             const uint32_t v = aux.tile_ctr[RT_HIT_BASE + k * RT_QUEUE_STRIDE];
             if (v) atomicAdd(&frame_sum[k / RT_HIT_SLOTS], (unsigned long long)v);
         }
         __syncthreads();
-        if (tid < fp.nframes && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
+        if (tid < poses && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
     }
     const uint32_t n = *(volatile uint32_t*)(aux.tile_ctr + RT_REDO_COUNT);
     if (n == 0) return;
@@ -301,13 +334,14 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
     st.tid = tid;
     st.top = 0;
     const uint32_t npix = (uint32_t)fp.W * (uint32_t)fp.nrows;
+    // (grid-stride over the redo list; every thread reaches the exit test)
     for (uint32_t e = blockIdx.x * 256u + (uint32_t)tid; e < n; e += gridDim.x * 256u) {
         const uint32_t v = aux.redo[e];
-        const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: frame * npix + pixel
-        const int f = (int)(ob / npix);
-        const uint32_t o = ob - (uint32_t)f * npix;
+        const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: pose * npix + pixel
+        const int p = (int)(ob / npix);
+        const uint32_t o = ob - (uint32_t)p * npix;
         const int i = (int)(o % (uint32_t)fp.W), r = (int)(o / (uint32_t)fp.W);
-        trace_exact<W, S, COUNT>(sc, fp, f, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
+        trace_pixel<W, S, COUNT>(sc, fp, p, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
     }
 }
 
@@ -332,7 +366,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace_exact(RtDevScene sc, RtFram
         if (tile >= tiles) break;
         const int i = (tile % tiles_x) * 8 + (lane & 7);
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
-        if (i < fp.W && r < fp.nrows) trace_exact<W, S, COUNT>(sc, fp, 0, i, r, st);
+        if (i < fp.W && r < fp.nrows) trace_pixel<W, S, COUNT>(sc, fp, 0, i, r, st);
     }
 }
 
@@ -351,11 +385,8 @@ __device__ __forceinline__ bool lane_pixel(const RtFrameParams& fp, int& i, int&
 }
 
 template <int SMAX, bool COUNT>
-__global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFrameParams fp) {
-    int i, r;
-    if (!lane_pixel(fp, i, r)) return;
-    const int j = fp.row0 + r * fp.row_stride;
-    const Ray64 ray = gen_ray(fp, fp.cam[0], i, j);
+__device__ __forceinline__ Best trace_literal(const RtDevScene& sc, const Ray64& ray, uint32_t& n_nodes,
+                                              uint32_t& n_tris) {
     Best best;
     best.dist = 1.7976931348623157e308;
     best.rank = 0;
@@ -364,7 +395,6 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
     uint32_t st[SMAX];
     int sp = 0;
     st[sp++] = 0;
-    uint32_t n_nodes = 0, n_tris = 0;
     while (sp > 0) {
         const uint32_t n = st[--sp];
         if (COUNT) n_nodes++;
@@ -391,13 +421,37 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
         for (uint32_t k = k0; k < k1; k++)
             if (sp < SMAX) st[sp++] = sc.rkid[k];
     }
-    const size_t o = (size_t)r * fp.W + i;
-    shade_store(fp, fp.cam[0], 0, sc, o, best);
+    return best;
+}
+
+// One pose (spp samples per pixel) per launch.
+template <int SMAX, bool COUNT>
+__global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFrameParams fp) {
+    int i, r;
+    if (!lane_pixel(fp, i, r)) return;
+    const int j = fp.row0 + r * fp.row_stride;
+    const size_t po = (size_t)r * fp.W + i;
+    uint32_t n_nodes = 0, n_tris = 0, hits = 0;
+    double acc[3] = {0.0, 0.0, 0.0};
+    for (int k = 0; k < fp.spp; k++) {
+        const Ray64 ray = gen_ray(fp, fp.cam[k], i, j);
+        const Best best = trace_literal<SMAX, COUNT>(sc, ray, n_nodes, n_tris);
+        const Shade sh = shade_of(sc, best.tri);
+        store_sample(fp, po * (size_t)fp.spp + k, best, sh);
+        double c[3];
+        shade_color(fp.cam[k], best, sh, c);
+        acc[0] = acc[0] + c[0];
+        acc[1] = acc[1] + c[1];
+        acc[2] = acc[2] + c[2];
+        hits += best.tri >= 0;
+    }
+    store_rgb(fp, po, acc);
+    wave_add(fp.hit_count, hits);
     if (COUNT && fp.counters) {
-        atomicAdd(&fp.counters[0], 1ull);
+        atomicAdd(&fp.counters[0], (unsigned long long)fp.spp);
         atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
         atomicAdd(&fp.counters[2], (unsigned long long)n_tris);
-        if (best.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
+        if (hits) atomicAdd(&fp.counters[4], (unsigned long long)hits);
     }
 }
 
@@ -416,17 +470,19 @@ bool use_packet(uint32_t stack_bound) {
     return !lane_forced && stack_bound <= (uint32_t)kPacketStack;
 }
 
-// Frame f of a batch as a one-frame launch (kernels that run per frame).
-RtFrameParams single_frame(const RtFrameParams& fp, int f) {
+// Pose p of a batch (its spp sample frames) as a one-pose launch (kernels
+// that run per pose).
+RtFrameParams single_pose(const RtFrameParams& fp, int p) {
     RtFrameParams o = fp;
-    const size_t off = (size_t)f * (size_t)fp.W * (size_t)fp.nrows;
-    o.nframes = 1;
-    o.cam[0] = fp.cam[f];
-    if (o.hit_id) o.hit_id += off;
-    if (o.dist) o.dist += off;
-    if (o.hit_pos) o.hit_pos += 3 * off;
+    const size_t off = (size_t)p * (size_t)fp.W * (size_t)fp.nrows;  // pixels before pose p
+    const size_t soff = off * (size_t)fp.spp;                         // samples before pose p
+    o.nframes = fp.spp;
+    for (int k = 0; k < fp.spp; k++) o.cam[k] = fp.cam[p * fp.spp + k];
+    if (o.hit_id) o.hit_id += soff;
+    if (o.dist) o.dist += soff;
+    if (o.hit_pos) o.hit_pos += 3 * soff;
     if (o.rgb) o.rgb += 3 * off;
-    if (o.hit_count) o.hit_count += f;
+    if (o.hit_count) o.hit_count += p;
     return o;
 }
 
@@ -440,27 +496,29 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     if (use_packet(sc.stack_bound)) {
         const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
         // k_resolve: frame f owns blocks [f * bpf, (f + 1) * bpf)
-        // k_resolve: one block per 16x16 tile, 8 XCD bands of T8 tiles per frame
+        // k_resolve: one block per 16x16 tile, 8 XCD bands of T8 tiles per pose
         const uint64_t rt8 = (((uint64_t)(fp.W + 15) / 16) * ((uint64_t)(fp.nrows + 15) / 16) + 7) / 8;
-        const dim3 rgrid((unsigned)(8 * rt8 * (uint64_t)fp.nframes));
+        const dim3 rgrid((unsigned)(8 * rt8 * (uint64_t)(fp.nframes / fp.spp)));
         if (count) {
             hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true>), grid, blk, 0, s,
                                PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
-            hipLaunchKernelGGL((k_resolve<true>), rgrid, blk, 0, s, sc, fp, aux);
+            if (fp.spp == 1) hipLaunchKernelGGL((k_resolve<true, false>), rgrid, blk, 0, s, sc, fp, aux);
+            else hipLaunchKernelGGL((k_resolve<true, true>), rgrid, blk, 0, s, sc, fp, aux);
             hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, blk, 0, s, sc, fp, aux);
         } else {
             hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false>), grid, blk, 0, s,
                                PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
-            hipLaunchKernelGGL((k_resolve<false>), rgrid, blk, 0, s, sc, fp, aux);
+            if (fp.spp == 1) hipLaunchKernelGGL((k_resolve<false, false>), rgrid, blk, 0, s, sc, fp, aux);
+            else hipLaunchKernelGGL((k_resolve<false, true>), rgrid, blk, 0, s, sc, fp, aux);
             hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, blk, 0, s, sc, fp, aux);
         }
     } else {
         // per-lane kernel (trees deeper than the packet stack): one launch
         // per frame of the batch, each on a zeroed work queue
-        for (int f = 0; f < fp.nframes; f++) {
-            const RtFrameParams f1 = single_frame(fp, f);
+        for (int f = 0; f < fp.nframes / fp.spp; f++) {
+            const RtFrameParams f1 = single_pose(fp, f);
             if (f > 0) {
                 hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);
                 if (e != hipSuccess) return e;
@@ -518,7 +576,8 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
                         hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after) {
     *fresh_after = fresh;
     if (fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0) return hipSuccess;
-    if (fp.nframes > RT_MAX_BATCH || (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.nframes >= (1ull << 31))
+    if (fp.nframes > RT_MAX_BATCH || fp.spp < 1 || fp.nframes % fp.spp != 0 ||
+        (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.nframes >= (1ull << 31))
         return hipErrorInvalidValue;
     if (mode == 1) {
         const long tiles = (long)((fp.W + 7) / 8) * (long)((fp.nrows + 7) / 8);
@@ -526,8 +585,8 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
         if (literal_stack > 1024) return hipErrorInvalidValue;
         if (ev) (void)hipEventRecord(ev[0], s);
         hipError_t e = hipSuccess;
-        for (int f = 0; f < fp.nframes && e == hipSuccess; f++) {
-            const RtFrameParams f1 = single_frame(fp, f);
+        for (int f = 0; f < fp.nframes / fp.spp && e == hipSuccess; f++) {
+            const RtFrameParams f1 = single_pose(fp, f);
             e = literal_stack <= 64    ? launch_literal_s<64>(sc, f1, count, grid, s)
                 : literal_stack <= 256 ? launch_literal_s<256>(sc, f1, count, grid, s)
                                        : launch_literal_s<1024>(sc, f1, count, grid, s);

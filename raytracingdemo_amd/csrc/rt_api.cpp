@@ -252,6 +252,13 @@ void check_camera(const rt_scene* s, const rt_camera* c) {
 // World-space margin added to every fp32 slab plane: 2^-19 * (|o|_max +
 // |coordinate|_max) dominates the fp32 rounding of the origin, the reciprocal
 // and the fma (each <= 2^-24 relative) by >= 8x (DESIGN.md "exactness").
+// n of an n x n stratified pattern (spp = n * n, checked by the caller)
+int spp_grid(int spp) {
+    int g = 1;
+    while ((g + 1) * (g + 1) <= spp) g++;
+    return g;
+}
+
 float frame_pad(const rt_scene* s, const rt_camera* c) {
     double om = std::max({std::fabs(c->pos[0]), std::fabs(c->pos[1]), std::fabs(c->pos[2])});
     double p = std::ldexp(om + s->flat.coord_max + 1e-30, -19);
@@ -260,19 +267,30 @@ float frame_pad(const rt_scene* s, const rt_camera* c) {
     return f;
 }
 
-// Launch parameters for frames c[0..n-1] (n <= RT_MAX_BATCH) of one image
-// geometry: per-pose camera basis (main.cpp:325-329) and slab margin.
-RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row0, int row_stride, int nrows) {
+// Launch parameters for poses c[0..n-1] (n * spp <= RT_MAX_BATCH) of one
+// image geometry: per-pose camera basis (main.cpp:325-329) and slab margin,
+// and per sample frame its stratified sub-pixel offset: sample s of an
+// n x n pattern sits at ((s % n) + 0.5) / n, ((s / n) + 0.5) / n (spp = 1:
+// the reference's pixel centre 0.5, camera.hpp:35-37).
+RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row0, int row_stride, int nrows,
+                           int spp = 1) {
     RtFrameParams fp{};
-    fp.nframes = n;
-    for (int f = 0; f < n; f++) {
-        RtFrameCam& k = fp.cam[f];
-        k.pad = frame_pad(s, &c[f]);
+    fp.nframes = n * spp;
+    fp.spp = spp;
+    const int g = spp_grid(spp);
+    for (int p = 0; p < n; p++) {
+        RtFrameCam k{};
+        k.pad = frame_pad(s, &c[p]);
         for (int a = 0; a < 3; a++) {
-            k.pos[a] = c[f].pos[a];
-            k.dir[a] = c[f].dir[a];
+            k.pos[a] = c[p].pos[a];
+            k.dir[a] = c[p].dir[a];
         }
-        rt::camera_basis(c[f].dir, k.right, k.up);
+        rt::camera_basis(c[p].dir, k.right, k.up);
+        for (int q = 0; q < spp; q++) {
+            k.ox = ((double)(q % g) + 0.5) / (double)g;
+            k.oy = ((double)(q / g) + 0.5) / (double)g;
+            fp.cam[p * spp + q] = k;
+        }
     }
     rt::pixel_constants(c->width, c->height, fp.cam_iw, fp.cam_ih, fp.cam_half, fp.cam_aspect);
     fp.W = c->width;
@@ -283,12 +301,13 @@ RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row
     return fp;
 }
 
-// Frames per launch of a batch: RT_MAX_BATCH, or RT_BATCH (1..RT_MAX_BATCH) for A/B runs.
+// Sample frames per launch of a batch: 12 (36-frame orbits split evenly), or
+// RT_BATCH (1..RT_MAX_BATCH) for A/B runs.
 int batch_frames() {
     static const int b = [] {
         const char* e = std::getenv("RT_BATCH");
-        const int v = e ? std::atoi(e) : RT_MAX_BATCH;
-        return v >= 1 && v <= RT_MAX_BATCH ? v : RT_MAX_BATCH;
+        const int v = e ? std::atoi(e) : 12;
+        return v >= 1 && v <= RT_MAX_BATCH ? v : 12;
     }();
     return b;
 }
@@ -441,10 +460,13 @@ int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {
     }
 }
 
-int rt_render_batch_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int mode, int row0,
-                           int row_stride, int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
+int rt_render_batch_spp_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int spp, int mode,
+                               int row0, int row_stride, int nrows, const rt_device_out* out, void* stream,
+                               uint32_t flags) {
     if (!s || !out || (nframes > 0 && !cams)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     if (nframes < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative frame count");
+    if (spp < 1 || spp > RT_MAX_BATCH || spp_grid(spp) * spp_grid(spp) != spp)
+        return fail(RT_ERR_INVALID_ARGUMENT, "spp must be n*n samples (1, 4, 9 or 16)");
     if (mode != RT_MODE_EXACT && mode != RT_MODE_FP64) return fail(RT_ERR_INVALID_ARGUMENT, "bad mode");
     try {
         for (int f = 0; f < nframes; f++) {
@@ -464,20 +486,22 @@ int rt_render_batch_device(rt_scene* s, int device, const rt_camera* cams, int n
         DevGuard g(device);
         hipStream_t st = (hipStream_t)stream;
         const uint64_t fpix = (uint64_t)cam->width * (uint64_t)nrows;  // pixels per frame
-        // frames per launch: the batch limit, and batch pixels < 2^31 (redo-list entries)
-        int per = batch_frames();
-        while (per > 1 && fpix * (uint64_t)per >= (1ull << 31)) per--;
+        // poses per launch: the batch's sample-frame limit, and batch pixels
+        // < 2^31 (redo-list entries)
+        int per = std::max(1, batch_frames() / spp);
+        while (per > 1 && fpix * (uint64_t)(per * spp) >= (1ull << 31)) per--;
+        if (fpix * (uint64_t)spp >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "image too large for spp");
         // serialise on the replica's stream: the caller's stream waits for it
         std::lock_guard<std::mutex> lk(s->mu);
-        ensure_redo(*r, fpix * (uint64_t)std::min(per, nframes));
+        ensure_redo(*r, fpix * (uint64_t)(std::min(per, nframes) * spp));
         order_on(*r, st);
         for (int f0 = 0; f0 < nframes; f0 += per) {
             const int n = std::min(per, nframes - f0);
-            RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows);
-            const uint64_t off = (uint64_t)f0 * fpix;
-            fp.hit_id = out->hit_id ? out->hit_id + off : nullptr;
-            fp.dist = out->dist ? out->dist + off : nullptr;
-            fp.hit_pos = out->pos ? out->pos + 3 * off : nullptr;
+            RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows, spp);
+            const uint64_t off = (uint64_t)f0 * fpix, soff = off * (uint64_t)spp;
+            fp.hit_id = out->hit_id ? out->hit_id + soff : nullptr;
+            fp.dist = out->dist ? out->dist + soff : nullptr;
+            fp.hit_pos = out->pos ? out->pos + 3 * soff : nullptr;
             fp.rgb = out->rgb ? out->rgb + 3 * off : nullptr;
             fp.hit_count = out->hit_count ? out->hit_count + f0 : nullptr;
             fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
@@ -496,6 +520,11 @@ int rt_render_batch_device(rt_scene* s, int device, const rt_camera* cams, int n
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
     }
+}
+
+int rt_render_batch_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int mode, int row0,
+                           int row_stride, int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
+    return rt_render_batch_spp_device(s, device, cams, nframes, 1, mode, row0, row_stride, nrows, out, stream, flags);
 }
 
 int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mode, int row0, int row_stride,

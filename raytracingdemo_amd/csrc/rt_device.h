@@ -49,7 +49,7 @@
 // RT_MAX_BATCH frames (camera poses) of the same geometry, so the persistent
 // traversal kernel's ramp-up and tail, and the launch gaps, are paid once per
 // batch instead of once per frame.
-#define RT_MAX_BATCH 12
+#define RT_MAX_BATCH 16
 #define RT_QUEUE_WORDS (RT_HIT_BASE + RT_MAX_BATCH * RT_HIT_SLOTS * RT_QUEUE_STRIDE)
 // Candidate lists handed from the traversal to the resolve kernel, per pixel:
 // RT_CAND_LDS entries kept in LDS during the walk plus overflow slots written
@@ -119,19 +119,25 @@ struct RtLaunchAux {
 // direction and the basis main.cpp:325-329 derives from it).
 struct RtFrameCam {
     double pos[3], dir[3], right[3], up[3];
+    double ox, oy;                 // sub-pixel sample offset (0.5, 0.5 = the reference's pixel centre)
     float pad;                     // world-space slab margin of the fp32 traversal (per pose)
     uint32_t reserved;
 };
 
-// One launch: `nframes` frames (poses cam[0..nframes-1]) of the same image
-// geometry and row shard.  Frame f's outputs start f * W * nrows pixels into
-// every output buffer; its hit counter is hit_count[f].
+// One launch: `nframes` frames (cam[0..nframes-1]) of the same image
+// geometry and row shard.  With spp samples per pixel a pose is spp
+// consecutive frames (sample s of pose p = frame p * spp + s, its own
+// sub-pixel offset); outputs are per pose: per-sample values (hit_id, dist,
+// hit_pos) of pose p, pixel o, sample s at (p * W * nrows + o) * spp + s, the
+// averaged colour (rgb) at p * W * nrows + o, the hit counter (samples hit)
+// at hit_count[p].  spp = 1 is the reference's one ray per pixel centre.
 struct RtFrameParams {
     double cam_iw, cam_ih;        // 1/W, 1/H            (camera.hpp:33-34)
     double cam_half, cam_aspect;  // tan(fov/2), W/H      (camera.hpp:29-30)
     int32_t W, H;
     int32_t row0, row_stride, nrows;
-    int32_t nframes;              // 1..RT_MAX_BATCH
+    int32_t nframes;              // 1..RT_MAX_BATCH, a multiple of spp
+    int32_t spp;                  // samples per pixel (n x n stratified), >= 1
     RT_G uint32_t* hit_id;
     RT_G double* dist;
     RT_G double* hit_pos;

@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--algo", default="bsah")
     p.add_argument("--k", type=int, default=8)
     p.add_argument("--mode", default="exact", choices=["exact", "fp64"])
+    p.add_argument("--spp", type=int, default=1, help="stratified samples per pixel (n*n; config c4: 4); "
+                                                      "the headline metric is 1")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -121,13 +123,14 @@ def main():
 
     rows = rows_per_rank(H, world)             # rows per rank (padded)
     my_rows = len(shard_rows(rank, world, H))
-    ids = torch.empty((F, rows, W), dtype=torch.int32, device=dev)
+    S = a.spp
+    ids = torch.empty((F, rows, W, S), dtype=torch.int32, device=dev)
     rgb = torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev)
     cnt = torch.zeros((F,), dtype=torch.int64, device=dev)
     # the library writes frame f at f * W * my_rows: a short shard renders
     # into contiguous buffers and is copied into the padded gather layout
     padded = my_rows != rows
-    r_ids = torch.empty((F, my_rows, W), dtype=torch.int32, device=dev) if padded else ids
+    r_ids = torch.empty((F, my_rows, W, S), dtype=torch.int32, device=dev) if padded else ids
     r_rgb = torch.zeros((F, my_rows, W, 3), dtype=torch.uint8, device=dev) if padded else rgb
     # rank 0's gather buffers, allocated once: [world, F, rows, W(, 3)]
     gather_ids = coll(ids).new_empty((world,) + tuple(ids.shape)) if (world > 1 and rank == 0) else None
@@ -141,7 +144,7 @@ def main():
         cnt.zero_()
         scene.render_batch_device(local, cams, W, H, rank, world, my_rows, hit_id=r_ids.data_ptr(),
                                   rgb=r_rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
-                                  mode=mode, timing=timing, count=count)
+                                  mode=mode, timing=timing, count=count, spp=S)
         if padded:
             ids[:, :my_rows] = r_ids
             rgb[:, :my_rows] = r_rgb
@@ -196,10 +199,10 @@ def main():
     if world > 1:
         g_ids, g_rgb = render_step()
         if rank == 0:
-            f_ids = torch.empty((F, H, W), dtype=torch.int32, device=dev)
+            f_ids = torch.empty((F, H, W, S), dtype=torch.int32, device=dev)
             f_rgb = torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev)
             scene.render_batch_device(local, cams, W, H, 0, 1, H, hit_id=f_ids.data_ptr(), rgb=f_rgb.data_ptr(),
-                                      stream=stream.cuda_stream, mode=mode)
+                                      stream=stream.cuda_stream, mode=mode, spp=S)
             torch.cuda.synchronize(dev)
             verified = bool(torch.equal(g_ids.to(dev), f_ids) and torch.equal(g_rgb.to(dev), f_rgb))
         dist.barrier()
@@ -207,14 +210,14 @@ def main():
     # in diagnostic builds the per-wave clock split
     ks = scene.frame_stats(local, reset=True)
     diag = ks["diag_cycles"]
-    tiles_timed = a.steps * F * ((W + 7) // 8) * ((my_rows + 7) // 8)
+    tiles_timed = a.steps * F * S * ((W + 7) // 8) * ((my_rows + 7) // 8)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         t = coll(t)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_rays = a.steps * F * W * H
+    total_rays = a.steps * F * W * H * S
     value = total_rays / elapsed / 1e6
     launches_timed = max(ks["timed_launches"], 1)
     frames_timed = a.steps * F
@@ -228,7 +231,7 @@ def main():
     achieved = alg_bytes_per_launch / avg_kernel_s / 1e9
 
     if rank == 0:
-        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}|fpl{frames_per_launch:g}"
+        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}|fpl{frames_per_launch:g}" + (f"|spp{S}" if S > 1 else "")
         if a.key_out:
             with open(a.key_out, "w") as fh:
                 fh.write(key + "\n")
@@ -254,13 +257,13 @@ def main():
         if world == 1 and not a.no_cpu:
             cpu = cpu_baseline(tris, a.algo, a.k, cams, W, H, a.cpu_seconds)
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC if S == 1 else METRIC.replace("1spp", f"{S}spp"), "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32 traversal + f64 exact resolve",
             "data": f"synthetic: {label}",
-            "config": {"workload": f"{label}, {W}x{H}x1spp primary rays, {a.algo}-{a.k} (BVH{a.k}) k-way, "
+            "config": {"workload": f"{label}, {W}x{H}x{S}spp primary rays, {a.algo}-{a.k} (BVH{a.k}) k-way, "
                                    f"{F}-frame camera orbit per step",
-                       "width": W, "height": H, "spp": 1, "bvh": f"{a.algo}-{a.k}", "frames_per_step": F,
+                       "width": W, "height": H, "spp": S, "bvh": f"{a.algo}-{a.k}", "frames_per_step": F,
                        "triangles": int(st["triangles"]), "mode": mode,
                        "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else ""),
                        **({"gather_verified": verified} if world > 1 else {}),

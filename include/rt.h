@@ -189,6 +189,20 @@ int rt_render_batch_spp_device(rt_scene *s, int device, const rt_camera *cams, i
                                int row0, int row_stride, int nrows, const rt_device_out *out, void *stream,
                                uint32_t flags);
 
+/* Diffuse path tracing of one pose (BASELINE config
+ * c5 "16 spp + 4-bounce secondary rays").  The reference has no secondary
+ * rays: the path model is build-defined and every segment is
+ * traced with the reference's closest-hit semantics (stack_bvh.hpp:611-644).
+ * Per pixel (i, j) and sample s: hash-seeded sub-pixel offset (frame, pixel,
+ * sample), 1 + bounces segments, cosine-weighted bounces, radiance
+ * sum_k 0.5^k * shadeScreen colour of vertex k (light at the camera); the
+ * pixel colour is the mean over samples cast as saveScreen does.  Outputs:
+ * rgb per pixel; hit_id / dist / pos of the primary segment per sample at
+ * (row * width + i) * spp + s; hit_count += samples whose primary ray hit.
+ * Row shard as rt_render_rows_device; asynchronous on `stream`. */
+int rt_render_paths_device(rt_scene *s, int device, const rt_camera *cam, int frame, int spp, int bounces, int row0,
+                           int row_stride, int nrows, const rt_device_out *out, void *stream, uint32_t flags);
+
 /* Read (and optionally reset) the per-device counters filled by
  * RT_FLAG_COUNT renders (synchronises the device). */
 int rt_frame_stats(rt_scene *s, int device, int reset, rt_frame_stats_t *out);

@@ -117,6 +117,9 @@ class Oracle(_Lib):
         L.orc_render_spp.argtypes = [C.c_void_p, _dp, _dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                      _i32p, _dp, _dp, _u8p]
         L.orc_render_spp.restype = C.c_longlong
+        L.orc_render_paths.argtypes = [C.c_void_p, _dp, _dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_int, _i32p, _dp, _dp, _u8p]
+        L.orc_render_paths.restype = C.c_longlong
         L.orc_max_threads.restype = C.c_int
 
     def bvh(self, tris: np.ndarray, algorithm: str, k: int):
@@ -190,6 +193,26 @@ class OracleBVH:
         hits = self.lib.lib.orc_render_spp(self.h, _ptr(p, _dp), _ptr(d, _dp), W, H, row0, nrows, int(spp),
                                            threads or self.lib.max_threads(), _ptr(out["id"], _i32p),
                                            _ptr(out["pos"], _dp), _ptr(out["dist"], _dp), _ptr(out["rgb"], _u8p))
+        if hits < 0:
+            raise RuntimeError(self.lib.err())
+        out["hits"] = int(hits)
+        return out
+
+
+    def render_paths(self, cam_pos, cam_dir, W: int, H: int, frame: int, spp: int, bounces: int, row0: int = 0,
+                     nrows: int | None = None, threads: int = 0):
+        """Diffuse paths (orc_render_paths): rgb per pixel, primary id / pos /
+        dist per sample."""
+        nrows = H - row0 if nrows is None else nrows
+        n = W * nrows
+        out = {"id": np.empty((n, spp), np.int32), "pos": np.empty((n, spp, 3)), "dist": np.empty((n, spp)),
+               "rgb": np.empty((n, 3), np.uint8)}
+        p = np.ascontiguousarray(cam_pos, dtype=np.float64)
+        d = np.ascontiguousarray(cam_dir, dtype=np.float64)
+        hits = self.lib.lib.orc_render_paths(self.h, _ptr(p, _dp), _ptr(d, _dp), W, H, row0, nrows, int(frame),
+                                             int(spp), int(bounces), threads or self.lib.max_threads(),
+                                             _ptr(out["id"], _i32p), _ptr(out["pos"], _dp), _ptr(out["dist"], _dp),
+                                             _ptr(out["rgb"], _u8p))
         if hits < 0:
             raise RuntimeError(self.lib.err())
         out["hits"] = int(hits)

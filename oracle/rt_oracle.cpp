@@ -961,6 +961,144 @@ long long orc_render_spp(const orc_bvh* h, const double cam_pos[3], const double
     return hits;
 }
 
+// ---------------------------------------------------------------- paths
+// Diffuse path tracing (build-defined extension, SURVEY.md §8(f) item 3 /
+// config c5; GPU: raytracingdemo_amd/csrc/path_kernel.h).
+// Every segment is traverse() above, the reference's closest hit.  All fp64
+// expressions in the GPU's operation order (this TU: -ffp-contract=off).
+}  // extern "C"
+namespace {
+inline uint32_t h32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+inline uint32_t path_seed(uint32_t frame, uint32_t px, uint32_t s) { return h32(h32(h32(0x5EEDu + frame) + px) + s); }
+inline double path_u(uint32_t seed, uint32_t n) { return (double)(h32(seed + n * 0x9E3779B9u) >> 8) * 0x1p-24; }
+// sin / cos of 2 pi f by octant + Taylor polynomials (no libm: same bits as the GPU)
+void spec_sincos(double f, double& sn, double& cs) {
+    const double f8 = f * 8.0;
+    const int k = (int)f8;
+    const double x = (f8 - (double)k) * 0x1.921fb54442d18p-1;
+    const double x2 = x * x;
+    const double S[8] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
+                         -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49};
+    const double Cc[9] = {-0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10,
+                          0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29,
+                          -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45, -0x1.6827863b97d97p-53};
+    double ps = x2 * S[7];
+    for (int q = 6; q >= 0; q--) ps = x2 * (S[q] + ps);
+    const double sx = x * (1.0 + ps);
+    double pc = x2 * Cc[8];
+    for (int q = 7; q >= 0; q--) pc = x2 * (Cc[q] + pc);
+    const double cx = 1.0 + pc;
+    const double r = 0x1.6a09e667f3bcdp-1;
+    static const double SA[8] = {0.0, r, 1.0, r, 0.0, -r, -1.0, -r};
+    static const double CA[8] = {1.0, r, 0.0, -r, -1.0, -r, 0.0, r};
+    sn = SA[k] * cx + CA[k] * sx;
+    cs = CA[k] * cx - SA[k] * sx;
+}
+// cosine-weighted bounce about n facing against din (Duff et al. 2017 basis),
+// normalised by division as Vector3::normalize
+V3 bounce_dir(V3 n, const V3& din, double u1, double u2) {
+    if (n.x * din.x + n.y * din.y + n.z * din.z > 0.0) n = {-n.x, -n.y, -n.z};
+    const double sign = n.z >= 0.0 ? 1.0 : -1.0;
+    const double a = -1.0 / (sign + n.z);
+    const double b = n.x * n.y * a;
+    const V3 t{1.0 + sign * n.x * n.x * a, sign * b, -sign * n.x};
+    const V3 bt{b, sign + n.y * n.y * a, -n.y};
+    const double rr = std::sqrt(u1);
+    double sphi, cphi;
+    spec_sincos(u2, sphi, cphi);
+    const double x = rr * cphi, y = rr * sphi, z = std::sqrt(1.0 - u1);
+    V3 e{(t.x * x + bt.x * y) + n.x * z, (t.y * x + bt.y * y) + n.y * z, (t.z * x + bt.z * y) + n.z * z};
+    const double len = std::sqrt(e.x * e.x + e.y * e.y + e.z * e.z);
+    if (len > 0.0) e = {e.x / len, e.y / len, e.z / len};
+    return e;
+}
+}  // namespace
+extern "C" {
+
+// One pose: spp paths per pixel of 1 + bounces segments; rgb per pixel,
+// primary-segment id / pos / dist per sample at ((j-row0)*W + i)*spp + s.
+// Returns the number of samples whose primary ray hit, or -1.
+long long orc_render_paths(const orc_bvh* h, const double cam_pos[3], const double cam_dir[3], int W, int H,
+                           int row0, int nrows, int frame, int spp, int bounces, int threads, int32_t* hit_id,
+                           double* hit_pos, double* hit_dist, uint8_t* rgb) {
+    if (W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H || spp < 1 || bounces < 0) {
+        g_err = "bad path geometry";
+        return -1;
+    }
+    const double fov = 90.0 * (std::numbers::pi / 180.0);
+    const double th = std::tan(fov * 0.5);
+    const double aspect = static_cast<double>(W) / H;
+    const double iw = 1.0 / W, ih = 1.0 / H;
+    const V3 cp{cam_pos[0], cam_pos[1], cam_pos[2]};
+    const V3 cd{cam_dir[0], cam_dir[1], cam_dir[2]};
+    V3 right, up;
+    basis(cd, right, up);
+    long long hits = 0;
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : hits)
+#endif
+    for (int i = 0; i < W; ++i) {
+        std::vector<int> st;
+        st.reserve(64);
+        TravStats ts;
+        for (int j = row0; j < row0 + nrows; ++j) {
+            const size_t o = (size_t)(j - row0) * W + i;
+            double acc[3] = {0.0, 0.0, 0.0};
+            for (int s = 0; s < spp; ++s) {
+                const uint32_t seed = path_seed((uint32_t)frame, (uint32_t)j * (uint32_t)W + (uint32_t)i, (uint32_t)s);
+                const double ox = path_u(seed, 0), oy = path_u(seed, 1);
+                const double px = (2.0 * (i + ox) * iw - 1.0) * th * aspect;
+                const double py = (1.0 - 2.0 * (j + oy) * ih) * th;
+                V3 d = add(add(cd, mul(up, py)), mul(right, px));
+                d = mul(d, 1.0 / length(d));
+                Ray r = make_ray(cp, d);
+                double L[3] = {0.0, 0.0, 0.0};
+                double w = 1.0;
+                for (int b = 0; b <= bounces; ++b) {
+                    V3 pos{0, 0, 0};
+                    double dist;
+                    const int id = traverse(h->b, r, pos, dist, st, ts);
+                    if (b == 0) {
+                        const size_t so = o * spp + s;
+                        if (hit_id) hit_id[so] = id;
+                        if (hit_pos) { hit_pos[so * 3] = pos.x; hit_pos[so * 3 + 1] = pos.y; hit_pos[so * 3 + 2] = pos.z; }
+                        if (hit_dist) hit_dist[so] = id >= 0 ? dist : -1.0;
+                        if (id >= 0) hits++;
+                    }
+                    if (id < 0) break;
+                    const V3 nrm = h->b.tris[id].normal;
+                    double c[3];
+                    shade(true, pos, nrm, cp, c);
+                    L[0] = L[0] + w * c[0];
+                    L[1] = L[1] + w * c[1];
+                    L[2] = L[2] + w * c[2];
+                    w = w * 0.5;
+                    if (b == bounces) break;
+                    V3 N = nrm;  // the unit normal shade() uses (normalised once more)
+                    const double nl = length(N);
+                    if (nl > 0.0) N = mul(N, 1.0 / nl);
+                    const V3 nd = bounce_dir(N, r.d, path_u(seed, 2u + 2u * (uint32_t)b), path_u(seed, 3u + 2u * (uint32_t)b));
+                    r = make_ray(pos, nd);
+                }
+                acc[0] = acc[0] + L[0];
+                acc[1] = acc[1] + L[1];
+                acc[2] = acc[2] + L[2];
+            }
+            if (rgb)
+                for (int k = 0; k < 3; k++) rgb[o * 3 + k] = to_byte(spp == 1 ? acc[k] : acc[k] / (double)spp);
+        }
+    }
+    return hits;
+}
+
 int orc_max_threads() {
 #ifdef _OPENMP
     return omp_get_max_threads();

@@ -32,7 +32,7 @@ RT_MISS = 0xFFFFFFFF
 # Every symbol include/rt.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "rt_load_obj", "rt_free", "rt_scene_center", "rt_camera_path", "rt_scene_create", "rt_scene_upload",
-    "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
+    "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_render_paths_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
     "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
 ]
 
@@ -127,6 +127,8 @@ def lib() -> C.CDLL:
     L.rt_render_batch_spp_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                              C.c_int, C.c_int, C.c_int, C.POINTER(rt_device_out), C.c_void_p,
                                              C.c_uint32]
+    L.rt_render_paths_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_int, C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
     L.rt_frame_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(rt_frame_stats_t)]
     L.rt_scene_stats.argtypes = [C.c_void_p, C.POINTER(rt_scene_stats_t)]
     L.rt_diag_raw.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]

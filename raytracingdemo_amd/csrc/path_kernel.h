@@ -1,0 +1,206 @@
+// Diffuse path tracing of primary + secondary rays (SURVEY.md §8(f) item 3,
+// BASELINE config c5: "16 spp + 4-bounce secondary rays").  Included by
+// render.hip after trace_core (uses Ray64, Win, LaneStack, trace_core).
+//
+// The reference has no secondary rays, so the path model is build-defined
+//  and restated operation for operation by the oracle
+// (oracle/rt_oracle.cpp orc_render_paths); every *segment* is traced with
+// the reference's own closest-hit semantics (stack_bvh.hpp:611-644) by the
+// exact per-lane traversal, so a path's vertices are the reference's hits.
+//
+//   sample s of pixel (i, j), frame F:   seed = h(h(h(0x5EED + F) + j*W + i) + s)
+//   draw n:                              u_n = (h(seed + n * 0x9E3779B9) >> 8) * 2^-24
+//   primary ray:                         camera.hpp:35-37 with offsets (u_0, u_1)
+//                                        in place of the pixel centre 0.5
+//   vertex k (k = 0 .. bounces):         c_k = shadeScreen's colour at the hit
+//                                        (light at the camera, main.cpp:356-377)
+//   radiance:                            L = sum_k 0.5^k c_k   (until a miss)
+//   bounce k -> k+1:                     cosine-weighted direction about the
+//                                        hit normal facing the ray, draws
+//                                        u_{2+2k}, u_{3+2k}
+//   pixel colour:                        (sum_s L_s) / spp, cast as saveScreen
+//
+// Every fp64 expression keeps the oracle's operation order (-ffp-contract=off);
+// sin/cos come from the fixed polynomial below, not from a libm, so the CPU
+// and the GPU compute the same bits.
+#pragma once
+
+// lowbias32 integer hash
+__device__ __forceinline__ uint32_t h32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t path_seed(uint32_t frame, uint32_t px, uint32_t s) {
+    return h32(h32(h32(0x5EEDu + frame) + px) + s);
+}
+__device__ __forceinline__ double path_u(uint32_t seed, uint32_t n) {
+    return (double)(h32(seed + n * 0x9E3779B9u) >> 8) * 0x1p-24;
+}
+
+// sin and cos of 2 pi f, f in [0, 1): octant k = floor(8 f), x = (8 f - k) pi/4
+// in [0, pi/4) (8 f is exact), Taylor polynomials to x^17 / x^18 (truncation
+// below 2^-60 there), then the octant's rotation.
+__device__ __forceinline__ void spec_sincos(double f, double& sn, double& cs) {
+    const double f8 = f * 8.0;
+    const int k = (int)f8;
+    const double x = (f8 - (double)k) * 0x1.921fb54442d18p-1;  // pi / 4
+    const double x2 = x * x;
+    const double sx = x * (1.0 + x2 * (-0x1.5555555555555p-3 + x2 * (0x1.1111111111111p-7 + x2 * (-0x1.a01a01a01a01ap-13 + x2 * (0x1.71de3a556c734p-19 + x2 * (-0x1.ae64567f544e4p-26 + x2 * (0x1.6124613a86d09p-33 + x2 * (-0x1.ae7f3e733b81fp-41 + x2 * 0x1.952c77030ad4ap-49))))))));
+    const double cx = 1.0 + x2 * (-0x1.0000000000000p-1 + x2 * (0x1.5555555555555p-5 + x2 * (-0x1.6c16c16c16c17p-10 + x2 * (0x1.a01a01a01a01ap-16 + x2 * (-0x1.27e4fb7789f5cp-22 + x2 * (0x1.1eed8eff8d898p-29 + x2 * (-0x1.93974a8c07c9dp-37 + x2 * (0x1.ae7f3e733b81fp-45 + x2 * -0x1.6827863b97d97p-53))))))));
+    const double r = 0x1.6a09e667f3bcdp-1;  // sqrt(2) / 2
+    // the octant's sin / cos (selects, no indexed table: it would live in scratch)
+    const double sa = (k == 1 || k == 3) ? r : (k == 5 || k == 7) ? -r : k == 2 ? 1.0 : k == 6 ? -1.0 : 0.0;
+    const double ca = (k == 1 || k == 7) ? r : (k == 3 || k == 5) ? -r : k == 0 ? 1.0 : k == 4 ? -1.0 : 0.0;
+    sn = sa * cx + ca * sx;
+    cs = ca * cx - sa * sx;
+}
+
+// Cosine-weighted direction about n (flipped to face against din), from the
+// orthonormal basis of Duff et al. (2017); normalised by division by the
+// length as Vector3::normalize (vector3.hpp:91-95).
+__device__ __forceinline__ void bounce_dir(double nx, double ny, double nz, double dx, double dy, double dz,
+                                           double u1, double u2, double& ox, double& oy, double& oz) {
+    if (nx * dx + ny * dy + nz * dz > 0.0) {
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
+    const double sign = nz >= 0.0 ? 1.0 : -1.0;
+    const double a = -1.0 / (sign + nz);
+    const double b = nx * ny * a;
+    const double tx = 1.0 + sign * nx * nx * a, ty = sign * b, tz = -sign * nx;
+    const double bx = b, by = sign + ny * ny * a, bz = -ny;
+    const double rr = __builtin_sqrt(u1);
+    double sphi, cphi;
+    spec_sincos(u2, sphi, cphi);
+    const double x = rr * cphi, y = rr * sphi, z = __builtin_sqrt(1.0 - u1);
+    double ex = (tx * x + bx * y) + nx * z;
+    double ey = (ty * x + by * y) + ny * z;
+    double ez = (tz * x + bz * y) + nz * z;
+    const double len = __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+    if (len > 0.0) {
+        ex = ex / len;
+        ey = ey / len;
+        ez = ez / len;
+    }
+    ox = ex;
+    oy = ey;
+    oz = ez;
+}
+
+// shadeScreen's colour of a vertex at p with unit normal n, light at the
+// camera (main.cpp:356-377; the primary vertex gives shade_color's value).
+__device__ __forceinline__ void shade_at(const RtFrameCam& cam, double px, double py, double pz, double nx, double ny,
+                                         double nz, double c[3]) {
+    double lx = cam.pos[0] - px, ly = cam.pos[1] - py, lz = cam.pos[2] - pz;
+    const double dist = __builtin_sqrt(lx * lx + ly * ly + lz * lz);
+    if (dist > 0.0) {
+        const double s = 1.0 / dist;
+        lx = lx * s;
+        ly = ly * s;
+        lz = lz * s;
+    }
+    const double diffuse = smax(0.0, nx * lx + ny * ly + nz * lz) * 1.35;
+    const double att = 1.0 / (1.0 + 0.05 * dist * dist);
+    const double I = sclamp((0.45 + diffuse * att) * 1.25, 0.0, 1.0);
+    c[0] = (0.5 * (nx + 1.0)) * I;
+    c[1] = (0.5 * (ny + 1.0)) * I;
+    c[2] = (0.5 * (nz + 1.0)) * I;
+}
+
+// World-space slab margin valid for a ray from o (frame_pad's bound,
+// rt_api.cpp: 2^-19 (|o|max + |coordinate|max), rounded up to fp32).
+__device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
+    const double om = __builtin_fmax(__builtin_fmax(__builtin_fabs(r.ox), __builtin_fabs(r.oy)), __builtin_fabs(r.oz));
+    return round_up_f(__builtin_ldexp(om + sc.coord_max + 1e-30, -19));
+}
+
+__device__ __forceinline__ Ray64 make_ray64(double ox, double oy, double oz, double dx, double dy, double dz) {
+    Ray64 r;
+    r.ox = ox;
+    r.oy = oy;
+    r.oz = oz;
+    r.dx = dx;
+    r.dy = dy;
+    r.dz = dz;
+    return with_inv(r);  // ray.hpp:13-19: +inf for a zero component
+}
+
+// Persistent waves over 8x8 pixel tiles of one pose; every lane traces all
+// spp paths of its pixel (segments in order), so the pixel's sum is formed in
+// sample order.  frame: the hash's frame number.
+template <int W, int S>
+__global__ void __launch_bounds__(256) k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
+                                               int bounces) {
+    __shared__ uint2 lds[S][256];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int tiles_x = (fp.W + 7) >> 3;
+    const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
+    LaneStack<S> st;
+    st.lds = lds;
+    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
+    st.tid = tid;
+    st.top = 0;
+    const RtFrameCam& cam = fp.cam[0];
+    for (;;) {
+        int tile = 0;
+        if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);
+        tile = __shfl(tile, 0);
+        if (tile >= tiles) break;
+        const int i = (tile % tiles_x) * 8 + (lane & 7);
+        const int r = (tile / tiles_x) * 8 + (lane >> 3);
+        uint32_t hits = 0;
+        if (i < fp.W && r < fp.nrows) {
+            const int j = fp.row0 + r * fp.row_stride;
+            const size_t pix = (size_t)r * fp.W + i;
+            double acc[3] = {0.0, 0.0, 0.0};
+            for (int s = 0; s < fp.spp; s++) {
+                const uint32_t seed = path_seed(frame, (uint32_t)j * (uint32_t)fp.W + (uint32_t)i, (uint32_t)s);
+                // primary ray through (i + u0, j + u1): gen_ray with the sample's offsets
+                RtFrameCam c1 = cam;
+                c1.ox = path_u(seed, 0);
+                c1.oy = path_u(seed, 1);
+                Ray64 ray = gen_ray(fp, c1, i, j);
+                double L[3] = {0.0, 0.0, 0.0};
+                double w = 1.0;
+                for (int b = 0; b <= bounces; b++) {
+                    LaneCounts lc;
+                    const Win win = trace_core<W, S, false>(sc, [&]() { return ray; }, ray_pad(sc, ray), st, 0, lc);
+                    Best hb;
+                    hb.dist = win.dist;
+                    hb.rank = win.rank;
+                    hb.tri = win.tri;
+                    hb.px = hb.py = hb.pz = 0.0;
+                    if (win.tri >= 0) (void)hit_dist(ray, win.t, hb.px, hb.py, hb.pz);
+                    const Shade sh = shade_of(sc, win.tri);
+                    if (b == 0) {  // the primary segment's per-sample outputs
+                        store_sample(fp, pix * (size_t)fp.spp + s, hb, sh);
+                        hits += win.tri >= 0;
+                    }
+                    if (win.tri < 0) break;
+                    double c[3];
+                    shade_at(cam, hb.px, hb.py, hb.pz, sh.nx, sh.ny, sh.nz, c);
+                    L[0] = L[0] + w * c[0];
+                    L[1] = L[1] + w * c[1];
+                    L[2] = L[2] + w * c[2];
+                    w = w * 0.5;
+                    if (b == bounces) break;
+                    double nx, ny, nz;
+                    bounce_dir(sh.nx, sh.ny, sh.nz, ray.dx, ray.dy, ray.dz, path_u(seed, 2u + 2u * (uint32_t)b),
+                               path_u(seed, 3u + 2u * (uint32_t)b), nx, ny, nz);
+                    ray = make_ray64(hb.px, hb.py, hb.pz, nx, ny, nz);
+                }
+                acc[0] = acc[0] + L[0];
+                acc[1] = acc[1] + L[1];
+                acc[2] = acc[2] + L[2];
+            }
+            store_rgb(fp, pix, acc);
+        }
+        wave_add(fp.hit_count, hits);
+    }
+}

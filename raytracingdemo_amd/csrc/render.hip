@@ -101,17 +101,24 @@ struct Win {
 // --------------------------------------------------------------------------
 // Fast exact kernel (persistent).
 // --------------------------------------------------------------------------
-template <int W, int S, bool COUNT>
-__device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
-                                            LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
+// Per-lane traversal counters (COUNT builds).
+struct LaneCounts {
+    uint32_t nodes = 0, tris = 0, chain = 0, chain_nodes = 0, pre = 0;
+};
+
+// The exact per-lane traversal of one ray, the reference's closest-hit
+// semantics (stack_bvh.hpp:611-644) over the walk tree: ray_of() returns the
+// fp64 ray (with reciprocals) — rebuilt on demand rather than held in
+// registers — and pad is a slab margin valid for it (frame_pad's bound).
+template <int W, int S, bool COUNT, class RayFn>
+__device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S>& st,
+                                          int pass0, LaneCounts& lc) {
     constexpr int G = W < 4 ? W : 4;  // children tested per load group
-    const int j = fp.row0 + r * fp.row_stride;
-    const RtFrameCam& cam = fp.cam[f];
     Ray32 q;
     double tslack;
     {
-        const Ray64 ray = gen_ray(fp, cam, i, j);
-        q = make_ray32(ray, cam.pad);
+        const Ray64 ray = ray_of();
+        q = make_ray32(ray, pad);
         // dist = |fl(o + d t) - o| differs from t by <= 2^-52 |o| + 2^-50 t:
         // covered by tslack + the 2^-20 relative margin of tcull
         tslack = 0x1p-40 * ((double)q.co + 1.0);
@@ -121,7 +128,11 @@ __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameP
     const bool sx = q.ix < 0.f, sy = q.iy < 0.f, sz = q.iz < 0.f;
 
     Win best;
-    uint32_t n_nodes = 0, n_tris = 0, n_chain = 0, n_chain_nodes = 0, n_pre = 0;
+    uint32_t& n_nodes = lc.nodes;
+    uint32_t& n_tris = lc.tris;
+    uint32_t& n_chain = lc.chain;
+    uint32_t& n_chain_nodes = lc.chain_nodes;
+    uint32_t& n_pre = lc.pre;
     // pass 0: traverse with the ancestor re-verification deferred to the
     //         winner (one check per ray, usually the margin test alone);
     // pass 1: only if that winner is invisible to the reference — traverse
@@ -203,7 +214,7 @@ __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameP
                     if (COUNT) n_pre++;
                     if (!tri_prefilter(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull)) continue;
                     if (COUNT) n_tris++;
-                    const Ray64 ray = gen_ray(fp, cam, opaque(i), j);
+                    const Ray64 ray = ray_of();
                     const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)k;
                     double t;
                     if (!mt64(T, ray, t)) continue;
@@ -239,7 +250,7 @@ __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameP
         }
         if (pass == 1 || best.tri < 0) break;
         // deferred re-verification of the winner's reference ancestor chain
-        const Ray64 ray = gen_ray(fp, cam, opaque(i), j);
+        const Ray64 ray = ray_of();
         double hx, hy, hz;
         (void)hit_dist(ray, best.t, hx, hy, hz);
         const uint32_t leaf =
@@ -249,13 +260,27 @@ __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameP
         if (chain_ok(sc, leaf, ray, n_chain_nodes)) break;
     }
 
+    return best;
+}
+
+// Exact per-lane traversal of the primary ray of pixel (i, r) of frame f.
+template <int W, int S, bool COUNT>
+__device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
+                                            LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
+    const int j = fp.row0 + r * fp.row_stride;
+    const RtFrameCam& cam = fp.cam[f];
+    auto ray_of = [&]() { return gen_ray(fp, cam, opaque(i), j); };
+    LaneCounts lc;
+    const Win best = trace_core<W, S, COUNT>(sc, ray_of, cam.pad, st, pass0, lc);
+    const uint32_t n_nodes = lc.nodes, n_tris = lc.tris, n_chain = lc.chain, n_chain_nodes = lc.chain_nodes,
+                   n_pre = lc.pre;
     Best out;
     out.dist = best.dist;
     out.rank = best.rank;
     out.tri = best.tri;
     out.px = out.py = out.pz = 0.0;
     if (best.tri >= 0) {
-        const Ray64 ray = gen_ray(fp, cam, opaque(i), j);
+        const Ray64 ray = ray_of();
         (void)hit_dist(ray, best.t, out.px, out.py, out.pz);
     }
     if (COUNT && fp.counters) {
@@ -304,6 +329,7 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
 }
 
 #include "packet_kernel.h"
+#include "path_kernel.h"
 
 // Finishes the pixels the packet kernel handed over (redo list, count in
 // tile_ctr[RT_REDO_COUNT]) with the per-lane exact kernel: from pass 0 after a candidate
@@ -614,6 +640,29 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
         case 16: return launch_exact<16>(sc, fp, aux, count, s, ev);
         default: return hipErrorInvalidValue;
     }
+}
+
+// Diffuse path tracing of one pose (path_kernel.h): spp paths per pixel of
+// 1 + bounces segments each, on a zeroed work queue; leaves it dirty.
+hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
+                        int bounces, hipStream_t s, const hipEvent_t* ev) {
+    if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
+    if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.tile_ctr || !aux.spill || aux.grid <= 0 ||
+        aux.spill_cap + kLdsStack < sc.stack_bound)
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const dim3 grid((unsigned)aux.grid), blk(256);
+    if (ev) (void)hipEventRecord(ev[0], s);
+    switch (sc.width) {
+        case 2: hipLaunchKernelGGL((k_paths<2, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 4: hipLaunchKernelGGL((k_paths<4, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 8: hipLaunchKernelGGL((k_paths<8, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 16: hipLaunchKernelGGL((k_paths<16, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        default: return hipErrorInvalidValue;
+    }
+    if (ev) (void)hipEventRecord(ev[1], s);
+    return hipGetLastError();
 }
 
 }  // namespace rt

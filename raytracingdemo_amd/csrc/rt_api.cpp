@@ -20,6 +20,8 @@ namespace rt {
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
                         hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after);
 int exact_blocks_per_cu(int width, uint32_t stack_bound);
+hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
+                        int bounces, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
 int exact_lds_stack();
 }
@@ -195,6 +197,7 @@ void upload_one(rt_scene* s, int device) {
     d.node_bytes = rt_node_bytes(f.width);
     d.width = f.width;
     d.stack_bound = f.stack_bound;
+    d.coord_max = f.coord_max;
     HIP_TRY(hipMalloc(&r.d_counters, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(r.d_counters, 0, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
@@ -525,6 +528,51 @@ int rt_render_batch_spp_device(rt_scene* s, int device, const rt_camera* cams, i
 int rt_render_batch_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int mode, int row0,
                            int row_stride, int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
     return rt_render_batch_spp_device(s, device, cams, nframes, 1, mode, row0, row_stride, nrows, out, stream, flags);
+}
+
+int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int frame, int spp, int bounces, int row0,
+                           int row_stride, int nrows, const rt_device_out* out, void* stream, uint32_t flags) {
+    if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (spp < 1 || spp > 4096) return fail(RT_ERR_INVALID_ARGUMENT, "spp must be 1..4096");
+    if (bounces < 0 || bounces > 64) return fail(RT_ERR_INVALID_ARGUMENT, "bounces must be 0..64");
+    try {
+        check_camera(s, cam);
+        if (row0 < 0 || row_stride < 1 || nrows < 0 || (nrows > 0 && row0 + (int64_t)(nrows - 1) * row_stride >= cam->height))
+            return fail(RT_ERR_INVALID_ARGUMENT, "row shard outside the image");
+        if ((uint64_t)cam->width * (uint64_t)nrows * (uint64_t)spp >= (1ull << 31))
+            return fail(RT_ERR_INVALID_ARGUMENT, "image too large for spp");
+        Replica* r;
+        {
+            std::lock_guard<std::mutex> lk(s->mu);
+            r = &replica_for(s, device);
+        }
+        DevGuard g(device);
+        hipStream_t st = (hipStream_t)stream;
+        RtFrameParams fp = frame_params(s, cam, 1, row0, row_stride, nrows);
+        fp.spp = spp;  // samples per pixel of the paths (one frame: offsets come from the hash)
+        fp.hit_id = out->hit_id;
+        fp.dist = out->dist;
+        fp.hit_pos = out->pos;
+        fp.rgb = out->rgb;
+        fp.hit_count = out->hit_count;
+        std::lock_guard<std::mutex> lk(s->mu);
+        const hipEvent_t* tev = nullptr;
+        if (flags & RT_FLAG_TIMING) {
+            if (r->tev_used == r->tev.size()) {
+                std::array<hipEvent_t, 2> a{};
+                for (auto& e : a) HIP_TRY(hipEventCreate(&e));
+                r->tev.push_back(a);
+            }
+            tev = r->tev[r->tev_used++].data();
+        }
+        order_on(*r, st);
+        const hipError_t e = rt::launch_paths(r->dev, fp, aux_of(*r), (uint32_t)frame, bounces, st, tev);
+        r->fresh = false;  // the work queue is left dirty: the next packet launch clears it
+        HIP_TRY(e);
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
 }
 
 int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mode, int row0, int row_stride,

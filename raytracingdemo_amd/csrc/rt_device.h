@@ -98,6 +98,7 @@ struct RtDevScene {
     uint32_t node_bytes;
     int32_t width;
     uint32_t stack_bound;
+    double coord_max;             // max |coordinate| of the scene (slab margins of arbitrary rays)
 };
 
 // Per-launch resources of the persistent exact kernel.

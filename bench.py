@@ -43,20 +43,28 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--frames", type=int, default=36, help="camera-path frames per step (runTest: 36)")
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--frames", type=int, default=None, help="camera-path frames per step (runTest: 36; paths: 1)")
+    p.add_argument("--width", type=int, default=None, help="default 1920 (paths: 3840)")
+    p.add_argument("--height", type=int, default=None, help="default 1080 (paths: 2160)")
+    p.add_argument("--paths", action="store_true",
+                   help="config c5: diffuse path tracing (secondary rays), 16 spp x (1 + 4 bounces) by default")
+    p.add_argument("--bounces", type=int, default=4, help="paths: secondary bounces per sample")
     p.add_argument("--algo", default="bsah")
     p.add_argument("--k", type=int, default=8)
     p.add_argument("--mode", default="exact", choices=["exact", "fp64"])
-    p.add_argument("--spp", type=int, default=1, help="stratified samples per pixel (n*n; config c4: 4); "
-                                                      "the headline metric is 1")
+    p.add_argument("--spp", type=int, default=None, help="samples per pixel: stratified n*n for primary rays "
+                                                         "(config c4: 4; headline: 1), paths default 16")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="committed rocprofv3 PMC summary supplying roofline.traffic")
     p.add_argument("--key-out", default="", help="write this run's workload key (for tools/pmc_traffic.py)")
-    return p.parse_args()
+    a = p.parse_args()
+    a.frames = a.frames if a.frames is not None else (1 if a.paths else 36)
+    a.width = a.width if a.width is not None else (3840 if a.paths else 1920)
+    a.height = a.height if a.height is not None else (2160 if a.paths else 1080)
+    a.spp = a.spp if a.spp is not None else (16 if a.paths else 1)
+    return a
 
 
 def cpu_baseline(tris, algo, k, cams, W, H, target_s):
@@ -82,6 +90,109 @@ def cpu_baseline(tris, algo, k, cams, W, H, target_s):
     return {"value": round(rays / spent / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": kind,
             "sample": f"{frames} full {W}x{H} frames of the same camera orbit ({rays} rays, {spent:.1f} s), "
                       f"same scene and {algo}-{k} tree, reference traversal semantics (no culling)"}
+
+
+def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
+    """Config c5: diffuse path tracing of primary + secondary rays (rt_render_paths_device).
+    A step is one pose of the orbit (step k: frame k % 36), every rank tracing its
+    interleaved rows, then one RCCL gather of the colours to rank 0, which
+    de-interleaves.  value = W*H*spp*(1 + bounces) / time (SURVEY.md §8(d)'s
+    nominal c5 ray count); segments actually traced are reported beside it."""
+    import torch
+    import torch.distributed as dist
+
+    import raytracingdemo_amd as rt
+    from raytracingdemo_amd.shards import gather_frames, rows_per_rank, shard_rows
+
+    W, H, S, B, F = a.width, a.height, a.spp, a.bounces, a.frames
+    path = rt.CameraPath(rt.scene_center(tris), 36)
+    rows = rows_per_rank(H, world)
+    my_rows = len(shard_rows(rank, world, H))
+    rgb = torch.zeros((1, rows, W, 3), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros((1,), dtype=torch.int64, device=dev)
+    gather_rgb = coll(rgb).new_empty((world,) + tuple(rgb.shape)) if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step(k, timing=False, count=False):
+        pos, d = path.circular_path(k % 36)
+        for f in range(F):
+            scene.render_paths_device(local, pos, d, W, H, rank, world, my_rows, frame=k % 36, spp=S, bounces=B,
+                                      rgb=rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
+                                      timing=timing, count=count)
+        if world > 1:
+            return gather_frames(coll(rgb), H, world, rank, out=gather_rgb)
+        return rgb
+
+    for w in range(a.warmup):
+        step(w, timing=True)
+    torch.cuda.synchronize(dev)
+    scene.frame_stats(local, reset=True)
+    step(0, count=True)  # counting pass: segments traced (outside timing)
+    torch.cuda.synchronize(dev)
+    cs = scene.frame_stats(local, reset=True)
+    segs_per_pose = cs["rays"] / F
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(k, timing=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ks = scene.frame_stats(local, reset=True)
+    if world > 1:
+        t = coll(torch.tensor([elapsed], dtype=torch.float64, device=dev))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        sg = coll(torch.tensor([segs_per_pose], dtype=torch.float64, device=dev))
+        dist.all_reduce(sg, op=dist.ReduceOp.SUM)
+        segs_per_pose = float(sg.item())
+    nominal = a.steps * F * W * H * S * (1 + B)
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu:
+            cpu = paths_cpu_baseline(tris, a, path, W, H, S, B)
+        line = {
+            "metric": f"Mrays/sec (primary + {B} diffuse bounces, {S}spp) on Sponza {W}x{H}",
+            "value": round(nominal / elapsed / 1e6, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32 traversal + f64 exact hits",
+            "data": f"synthetic: {label}",
+            "config": {"workload": f"{label}, {W}x{H}x{S}spp, 1 + {B} bounce segments per sample, diffuse paths, "
+                                   f"{a.algo}-{a.k} reference tree, SAH walk tree, {F} pose(s) per step",
+                       "width": W, "height": H, "spp": S, "bounces": B, "frames_per_step": F,
+                       "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else ""),
+                       **({"rehearsal_not_a_measurement": True} if rehearse else {})},
+            "segments_traced_per_s_M": round(segs_per_pose * a.steps * F / elapsed / 1e6, 2),
+            "segments_per_sample": round(segs_per_pose / (W * H * S), 3),
+            "kernel_ms_avg": round(ks["trace_ms"] / max(ks["timed_launches"], 1), 3),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def paths_cpu_baseline(tris, a, path, W, H, S, B):
+    """The oracle's path tracer (the reference has none: kind "port") on host
+    cores over whole rows of the same pose until ~cpu_seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    threads = int(os.environ.get("RT_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    b = pyoracle.Oracle().bvh(tris, a.algo, a.k)
+    pos, d = path.circular_path(0)
+    rows, spent, j = 0, 0.0, 0
+    while spent < a.cpu_seconds and rows < H:
+        n = max(1, threads // 4)
+        t0 = time.perf_counter()
+        b.render_paths(pos, d, W, H, 0, S, B, row0=j, nrows=min(n, H - j), threads=threads)
+        spent += time.perf_counter() - t0
+        rows += min(n, H - j)
+        j = (j + 97 * n) % (H - n)
+    return {"value": round(rows * W * S * (1 + B) / spent / 1e6, 4), "unit": "Mrays/s", "cores": threads,
+            "kind": "port", "sample": f"{rows} rows of {W} px x {S} spp x (1 + {B}) segments, pose 0 ({spent:.1f} s)"}
 
 
 def main():
@@ -115,6 +226,8 @@ def main():
 
     tris, label = sponza_scene()
     scene = rt.Scene(tris, a.algo, a.k).upload([local])
+    if a.paths:
+        return run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse)
     st = scene.stats()
     W, H, F = a.width, a.height, a.frames
     center = rt.scene_center(tris)

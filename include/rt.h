@@ -199,7 +199,9 @@ int rt_render_batch_spp_device(rt_scene *s, int device, const rt_camera *cams, i
  * pixel colour is the mean over samples cast as saveScreen does.  Outputs:
  * rgb per pixel; hit_id / dist / pos of the primary segment per sample at
  * (row * width + i) * spp + s; hit_count += samples whose primary ray hit.
- * Row shard as rt_render_rows_device; asynchronous on `stream`. */
+ * Row shard as rt_render_rows_device; asynchronous on `stream`.  flags:
+ * RT_FLAG_COUNT adds the ray segments traced to rt_frame_stats' rays,
+ * RT_FLAG_TIMING times the kernel (trace_ms). */
 int rt_render_paths_device(rt_scene *s, int device, const rt_camera *cam, int frame, int spp, int bounces, int row0,
                            int row_stride, int nrows, const rt_device_out *out, void *stream, uint32_t flags);
 

@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256) k_paths(RtDevScene sc, RtFrameParams fp, 
         if (tile >= tiles) break;
         const int i = (tile % tiles_x) * 8 + (lane & 7);
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
-        uint32_t hits = 0;
+        uint32_t hits = 0, segs = 0;  // segs: ray segments traced (RT_FLAG_COUNT)
         if (i < fp.W && r < fp.nrows) {
             const int j = fp.row0 + r * fp.row_stride;
             const size_t pix = (size_t)r * fp.W + i;
@@ -171,6 +171,7 @@ __global__ void __launch_bounds__(256) k_paths(RtDevScene sc, RtFrameParams fp, 
                 for (int b = 0; b <= bounces; b++) {
                     LaneCounts lc;
                     const Win win = trace_core<W, S, false>(sc, [&]() { return ray; }, ray_pad(sc, ray), st, 0, lc);
+                    segs++;
                     Best hb;
                     hb.dist = win.dist;
                     hb.rank = win.rank;
@@ -201,6 +202,7 @@ __global__ void __launch_bounds__(256) k_paths(RtDevScene sc, RtFrameParams fp, 
             }
             store_rgb(fp, pix, acc);
         }
-        wave_add(fp.hit_count, hits);
+        wave_add<13>(fp.hit_count, hits);
+        if (fp.counters) wave_add<20>(fp.counters, segs);
     }
 }

@@ -295,11 +295,12 @@ __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameP
     return out;
 }
 
-// Adds each active lane's v (0..31) to *p with one atomic per wave.
+// Adds each active lane's v (< 2^BITS) to *p with one atomic per wave.
+template <int BITS = 5>
 __device__ __forceinline__ void wave_add(RT_G unsigned long long* p, uint32_t v) {
     uint32_t sum = 0;
 #pragma unroll
-    for (int b = 0; b < 5; b++) sum += (uint32_t)__builtin_popcountll(__ballot((v >> b) & 1u)) << b;
+    for (int b = 0; b < BITS; b++) sum += (uint32_t)__builtin_popcountll(__ballot((v >> b) & 1u)) << b;
     const uint64_t act = __ballot(1);
     if (p && sum != 0 && (int)(threadIdx.x & 63) == __builtin_ctzll(act)) atomicAdd(p, (unsigned long long)sum);
 }

@@ -550,6 +550,7 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
         hipStream_t st = (hipStream_t)stream;
         RtFrameParams fp = frame_params(s, cam, 1, row0, row_stride, nrows);
         fp.spp = spp;  // samples per pixel of the paths (one frame: offsets come from the hash)
+        fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;  // [0] += ray segments traced
         fp.hit_id = out->hit_id;
         fp.dist = out->dist;
         fp.hit_pos = out->pos;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Wide-node fill of the traversal (diagnostic): fraction of wave node visits
 to nodes with <= 4 valid child slots and mean valid slots per visit, from the
-counting kernel's raw counters (rt_diag_raw words 13, 14)."""
+counting kernel's raw counters (rt_diag_raw words 7, 8, 13-15)."""
 import ctypes as C
 import os
 import sys
@@ -28,8 +28,9 @@ def main():
     torch.cuda.synchronize()
     raw = np.zeros(16, np.uint64)
     N.check(N.lib().rt_diag_raw(s.handle, 0, raw.ctypes.data, 16))
-    nodes, narrow, slots = int(raw[7]), int(raw[13]), int(raw[14])
-    print(f"wave node visits {nodes}: <=4 valid slots {narrow / nodes:.3f}, mean valid slots {slots / nodes:.2f}")
+    nodes, empty_pop, popcull, empty = int(raw[7]), int(raw[13]), int(raw[14]), int(raw[15])
+    print(f"wave node visits {nodes}: popped and empty {empty_pop / nodes:.3f}, pops culled {popcull}, "
+          f"no child entered {empty / nodes:.3f}; leaf visits {int(raw[8])}")
 
 
 if __name__ == "__main__":

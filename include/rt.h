@@ -135,6 +135,14 @@ typedef struct {
 int rt_load_obj(const char *path, double scale, double **tris, uint64_t *n_tris);
 void rt_free(void *p);
 
+/* rt_load_obj through a binary scene cache: the
+ * loader's output is kept in cache_dir under the FNV-1a digest of the OBJ
+ * bytes and the scale; a valid entry is returned as is (bit-identical to
+ * rt_load_obj), anything else is parsed and the entry (re)written.
+ * *from_cache (may be NULL) = 1 on a cache hit. */
+int rt_load_obj_cached(const char *path, double scale, const char *cache_dir, double **tris, uint64_t *n_tris,
+                       int *from_cache);
+
 /* runTest's scene centre (main.cpp:118-122). */
 int rt_scene_center(const double *tri_v, uint64_t n_tris, double center[3]);
 

@@ -18,6 +18,7 @@ librtmi355x.so; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -54,6 +55,26 @@ def load_obj(path: str, scale: float = 1.0) -> np.ndarray:
         if n.value == 0:
             return np.zeros((0, 9))
         return np.ctypeslib.as_array(buf, shape=(n.value * 9,)).copy().reshape(-1, 9)
+    finally:
+        L.rt_free(buf)
+
+
+def load_obj_cached(path: str, scale: float = 1.0, cache_dir: str = "") -> tuple[np.ndarray, bool]:
+    """load_obj through the binary scene cache (include/rt.h rt_load_obj_cached):
+    (triangles, True if the cache entry was used).  cache_dir defaults to
+    $RT_SCENE_CACHE or ~/.cache/rtmi355x."""
+    cache_dir = cache_dir or os.environ.get("RT_SCENE_CACHE") or os.path.expanduser("~/.cache/rtmi355x")
+    os.makedirs(cache_dir, exist_ok=True)
+    L = N.lib()
+    buf = C.POINTER(C.c_double)()
+    n = C.c_uint64()
+    hit = C.c_int(0)
+    N.check(L.rt_load_obj_cached(str(path).encode(), float(scale), cache_dir.encode(), C.byref(buf), C.byref(n),
+                                 C.byref(hit)))
+    try:
+        if n.value == 0:
+            return np.zeros((0, 9)), bool(hit.value)
+        return np.ctypeslib.as_array(buf, shape=(n.value * 9,)).copy().reshape(-1, 9), bool(hit.value)
     finally:
         L.rt_free(buf)
 

@@ -31,7 +31,7 @@ RT_MISS = 0xFFFFFFFF
 
 # Every symbol include/rt.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "rt_load_obj", "rt_free", "rt_scene_center", "rt_camera_path", "rt_scene_create", "rt_scene_upload",
+    "rt_load_obj", "rt_load_obj_cached", "rt_free", "rt_scene_center", "rt_camera_path", "rt_scene_create", "rt_scene_upload",
     "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_render_paths_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
     "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
 ]
@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
     L.rt_abi_version.restype = C.c_int
     L.rt_load_obj.argtypes = [C.c_char_p, C.c_double, C.POINTER(dp), u64p]
     L.rt_free.argtypes = [C.c_void_p]
+    L.rt_load_obj_cached.argtypes = [C.c_char_p, C.c_double, C.c_char_p, C.POINTER(dp), u64p, C.POINTER(C.c_int)]
     L.rt_scene_center.argtypes = [C.c_void_p, C.c_uint64, dp]
     L.rt_camera_path.argtypes = [dp, C.c_int, C.c_int, dp, dp]
     L.rt_scene_create.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]

@@ -404,6 +404,24 @@ int rt_load_obj(const char* path, double scale, double** tris, uint64_t* n_tris)
     }
 }
 
+int rt_load_obj_cached(const char* path, double scale, const char* cache_dir, double** tris, uint64_t* n_tris,
+                       int* from_cache) {
+    if (!path || !cache_dir || !tris || !n_tris) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    try {
+        bool hit = false;
+        std::vector<double> v = rt::load_obj_cached(path, scale, cache_dir, &hit);
+        double* buf = (double*)std::malloc(std::max<size_t>(v.size(), 1) * sizeof(double));
+        if (!buf) return fail(RT_ERR_RUNTIME, "out of memory");
+        if (!v.empty()) std::memcpy(buf, v.data(), v.size() * sizeof(double));
+        *tris = buf;
+        *n_tris = v.size() / 9;
+        if (from_cache) *from_cache = hit ? 1 : 0;
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
 int rt_scene_center(const double* tri_v, uint64_t n, double center[3]) {
     if (!tri_v || !center || n == 0) return fail(RT_ERR_INVALID_ARGUMENT, "empty scene");
     rt::scene_center(tri_v, n, center);

@@ -91,5 +91,8 @@ void scene_center(const double* tri_v, uint64_t n, double out[3]);
 
 // OBJ ingestion with objl semantics (lib/OBJ_Loader.h:431-1003).
 std::vector<double> load_obj(const std::string& path, double scale);
+// The same through the binary scene cache in cache_dir (scene_cache.cpp);
+// *hit: the entry was valid and used.
+std::vector<double> load_obj_cached(const std::string& path, double scale, const std::string& cache_dir, bool* hit);
 
 }  // namespace rt

@@ -119,22 +119,19 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
     return round_up_f(__builtin_ldexp(om + sc.coord_max + 1e-30, -19));
 }
 
-__device__ __forceinline__ Ray64 make_ray64(double ox, double oy, double oz, double dx, double dy, double dz) {
-    Ray64 r;
-    r.ox = ox;
-    r.oy = oy;
-    r.oz = oz;
-    r.dx = dx;
-    r.dy = dy;
-    r.dz = dz;
-    return with_inv(r);  // ray.hpp:13-19: +inf for a zero component
-}
-
 // Persistent waves over 8x8 pixel tiles of one pose; every lane traces all
 // spp paths of its pixel (segments in order), so the pixel's sum is formed in
 // sample order.  frame: the hash's frame number.
+#ifndef RT_PATHS_WPE
+#define RT_PATHS_WPE 4  // 128 VGPRs (a few spills): +13% over the compiler's 161 (3 waves/SIMD)
+#endif
+#if RT_PATHS_WPE > 0
+#define RT_PATHS_ATTR __attribute__((amdgpu_waves_per_eu(RT_PATHS_WPE)))
+#else
+#define RT_PATHS_ATTR
+#endif
 template <int W, int S>
-__global__ void __launch_bounds__(256) k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
+__global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
                                                int bounces) {
     __shared__ uint2 lds[S][256];
     const int tid = threadIdx.x;
@@ -165,19 +162,22 @@ __global__ void __launch_bounds__(256) k_paths(RtDevScene sc, RtFrameParams fp, 
                 RtFrameCam c1 = cam;
                 c1.ox = path_u(seed, 0);
                 c1.oy = path_u(seed, 1);
-                Ray64 ray = gen_ray(fp, c1, i, j);
+                // the segment's ray without reciprocals (6 doubles live across the
+                // walk); ray_of() adds them where the traversal needs them
+                Ray64 ray = gen_ray<false>(fp, c1, i, j);
                 double L[3] = {0.0, 0.0, 0.0};
                 double w = 1.0;
                 for (int b = 0; b <= bounces; b++) {
                     LaneCounts lc;
-                    const Win win = trace_core<W, S, false>(sc, [&]() { return ray; }, ray_pad(sc, ray), st, 0, lc);
+                    const Win win =
+                        trace_core<W, S, false>(sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, 0, lc);
                     segs++;
                     Best hb;
                     hb.dist = win.dist;
                     hb.rank = win.rank;
                     hb.tri = win.tri;
                     hb.px = hb.py = hb.pz = 0.0;
-                    if (win.tri >= 0) (void)hit_dist(ray, win.t, hb.px, hb.py, hb.pz);
+                    if (win.tri >= 0) (void)hit_dist(ray, win.t, hb.px, hb.py, hb.pz);  // (uses o, d only)
                     const Shade sh = shade_of(sc, win.tri);
                     if (b == 0) {  // the primary segment's per-sample outputs
                         store_sample(fp, pix * (size_t)fp.spp + s, hb, sh);
@@ -194,7 +194,12 @@ __global__ void __launch_bounds__(256) k_paths(RtDevScene sc, RtFrameParams fp, 
                     double nx, ny, nz;
                     bounce_dir(sh.nx, sh.ny, sh.nz, ray.dx, ray.dy, ray.dz, path_u(seed, 2u + 2u * (uint32_t)b),
                                path_u(seed, 3u + 2u * (uint32_t)b), nx, ny, nz);
-                    ray = make_ray64(hb.px, hb.py, hb.pz, nx, ny, nz);
+                    ray.ox = hb.px;
+                    ray.oy = hb.py;
+                    ray.oz = hb.pz;
+                    ray.dx = nx;
+                    ray.dy = ny;
+                    ray.dz = nz;
                 }
                 acc[0] = acc[0] + L[0];
                 acc[1] = acc[1] + L[1];

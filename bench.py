@@ -6,8 +6,9 @@ a CPU baseline (the reference's own traversal, compiled, all host cores used).
 A *step* is one pass of the reference's camera orbit (runTest's 36-frame path,
 src/main.cpp:234-281): every frame is ray generation + traversal + exact
 resolve + shading on the GPU, rows interleaved over the N GPUs (row j on rank
-j mod N), followed by one RCCL gather of the step's shards to rank 0 and the
-de-interleave there.  Total work per step is fixed (strong scaling).
+j mod N), followed by one RCCL gather of the step's framebuffers (rgb) and hit
+counts to rank 0 and the de-interleave there, on a side stream that overlaps
+the next step's render.  Total work per step is fixed (strong scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -202,7 +203,7 @@ def main():
 
     import raytracingdemo_amd as rt
     from raytracingdemo_amd.scenes import sponza_scene
-    from raytracingdemo_amd.shards import gather_frames, rows_per_rank, shard_rows
+    from raytracingdemo_amd.shards import deinterleave_into, gather_frames, rows_per_rank, shard_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -237,48 +238,86 @@ def main():
     rows = rows_per_rank(H, world)             # rows per rank (padded)
     my_rows = len(shard_rows(rank, world, H))
     S = a.spp
-    ids = torch.empty((F, rows, W, S), dtype=torch.int32, device=dev)
-    rgb = torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev)
-    cnt = torch.zeros((F,), dtype=torch.int64, device=dev)
+    # Two buffer sets: step k renders into set k % 2 while set (k - 1) % 2 is
+    # still being gathered (the gather of step k overlaps the render of step
+    # k + 1; the render of step k + 2 waits for the gather of step k).
+    NB = 2 if world > 1 else 1
+    ids = [torch.empty((F, rows, W, S), dtype=torch.int32, device=dev) for _ in range(NB)]
+    rgb = [torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
+    cnt = [torch.zeros((F,), dtype=torch.int64, device=dev) for _ in range(NB)]
     # the library writes frame f at f * W * my_rows: a short shard renders
     # into contiguous buffers and is copied into the padded gather layout
     padded = my_rows != rows
-    r_ids = torch.empty((F, my_rows, W, S), dtype=torch.int32, device=dev) if padded else ids
-    r_rgb = torch.zeros((F, my_rows, W, 3), dtype=torch.uint8, device=dev) if padded else rgb
-    # rank 0's gather buffers, allocated once: [world, F, rows, W(, 3)]
-    gather_ids = coll(ids).new_empty((world,) + tuple(ids.shape)) if (world > 1 and rank == 0) else None
-    gather_rgb = coll(rgb).new_empty((world,) + tuple(rgb.shape)) if (world > 1 and rank == 0) else None
+    r_ids = [torch.empty((F, my_rows, W, S), dtype=torch.int32, device=dev) for _ in range(NB)] if padded else ids
+    r_rgb = [torch.zeros((F, my_rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)] if padded else rgb
+    # rank 0's gather buffers, allocated once: [world, F, rows, W, 3], and the
+    # de-interleaved frames [F, H, W, 3] (the step's framebuffers) and counts
+    root = world > 1 and rank == 0
+    gather_rgb = [coll(rgb[0]).new_empty((world,) + tuple(rgb[0].shape)) for _ in range(NB)] if root else None
+    gather_cnt = [coll(cnt[0]).new_empty((world, F)) for _ in range(NB)] if root else None
+    frames = [torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)] if root else None
     stream = torch.cuda.current_stream(dev)
+    post = torch.cuda.Stream(dev) if world > 1 else None  # gather + de-interleave
+    shipped = [None] * NB                                 # event: set b's gather and copy done
     mode = a.mode
 
-    def render_step(timing=False, count=False):
+    def render(b, timing=False, count=False):
         # the whole camera orbit in one batched call (the library launches up
         # to 12 frames per traversal / resolve / fix-up launch)
-        cnt.zero_()
-        scene.render_batch_device(local, cams, W, H, rank, world, my_rows, hit_id=r_ids.data_ptr(),
-                                  rgb=r_rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
+        if shipped[b] is not None:
+            stream.wait_event(shipped[b])  # set b's previous gather has read it
+        cnt[b].zero_()
+        scene.render_batch_device(local, cams, W, H, rank, world, my_rows, hit_id=r_ids[b].data_ptr(),
+                                  rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(), stream=stream.cuda_stream,
                                   mode=mode, timing=timing, count=count, spp=S)
         if padded:
-            ids[:, :my_rows] = r_ids
-            rgb[:, :my_rows] = r_rgb
-        if world > 1:
-            # one RCCL gather per output to rank 0, which de-interleaves
-            # (image row j = r * world + rank) into full frames
-            full_ids = gather_frames(coll(ids), H, world, rank, out=gather_ids)
-            full_rgb = gather_frames(coll(rgb), H, world, rank, out=gather_rgb)
-            return full_ids, full_rgb
-        return ids, rgb
+            ids[b][:, :my_rows] = r_ids[b]
+            rgb[b][:, :my_rows] = r_rgb[b]
+
+    def ship(b):
+        # the step's framebuffers (rgb) and per-frame hit counts
+        # to rank 0 with RCCL, issued on a side stream after the render, and
+        # de-interleaved there (image row j = r * world + rank) into frames[b]
+        if world == 1:
+            return
+        if rehearse:  # gloo over host copies: synchronous
+            dist.gather(coll(cnt[b]), list(gather_cnt[b].unbind(0)) if root else None, dst=0)
+            full = gather_frames(coll(rgb[b]), H, world, rank, out=gather_rgb[b] if root else None)
+            if root:
+                frames[b].copy_(full)
+            return
+        post.wait_stream(stream)
+        with torch.cuda.stream(post):
+            w1 = dist.gather(cnt[b], list(gather_cnt[b].unbind(0)) if root else None, dst=0, async_op=True)
+            w2 = dist.gather(rgb[b], list(gather_rgb[b].unbind(0)) if root else None, dst=0, async_op=True)
+            w1.wait()
+            w2.wait()
+            if root:
+                deinterleave_into(gather_rgb[b], H, frames[b])
+            ev = torch.cuda.Event()
+            ev.record(post)
+        shipped[b] = ev
+
+    def render_step(k, timing=False, count=False):
+        b = k % NB
+        render(b, timing=timing, count=count)
+        ship(b)
+
+    def drain():
+        if post is not None:
+            stream.wait_stream(post)
 
     # warm-up with kernel timing on, so the library's per-launch timing events
     # exist before the timed region (they are recycled, not re-created)
     ktiming = not os.environ.get("RT_BENCH_NO_KTIMING")
-    for _ in range(a.warmup):
-        render_step(timing=ktiming)
+    for k in range(a.warmup):
+        render_step(k, timing=ktiming)
+    drain()
     torch.cuda.synchronize(dev)
     scene.frame_stats(local, reset=True)
 
     # counting pass for algorithmic bytes (outside the timed region)
-    render_step(count=True)
+    render(0, count=True)
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
     nb = st["node_bytes"]
@@ -300,24 +339,30 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        render_step(timing=ktiming)
+    for k in range(a.steps):
+        render_step(k, timing=ktiming)
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # multi-rank: the gathered, de-interleaved frames of the last step must
-    # equal a full-image render on rank 0 (outside the timed region)
+    # multi-rank (outside the timed region): the last step's gathered,
+    # de-interleaved frames and hit counts, and a gather of the last step's
+    # hit ids, must equal a full-image render on rank 0
     verified = None
     if world > 1:
-        g_ids, g_rgb = render_step()
+        bl = (a.steps - 1) % NB
+        g_ids = gather_frames(coll(ids[bl]), H, world, rank)
+        torch.cuda.synchronize(dev)
         if rank == 0:
             f_ids = torch.empty((F, H, W, S), dtype=torch.int32, device=dev)
             f_rgb = torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev)
+            f_cnt = torch.zeros((F,), dtype=torch.int64, device=dev)
             scene.render_batch_device(local, cams, W, H, 0, 1, H, hit_id=f_ids.data_ptr(), rgb=f_rgb.data_ptr(),
-                                      stream=stream.cuda_stream, mode=mode, spp=S)
+                                      hit_count=f_cnt.data_ptr(), stream=stream.cuda_stream, mode=mode, spp=S)
             torch.cuda.synchronize(dev)
-            verified = bool(torch.equal(g_ids.to(dev), f_ids) and torch.equal(g_rgb.to(dev), f_rgb))
+            verified = bool(torch.equal(g_ids.to(dev), f_ids) and torch.equal(frames[bl], f_rgb) and
+                            torch.equal(gather_cnt[bl].to(dev).sum(0), f_cnt))
         dist.barrier()
     # per-kernel HIP-event times of the timed launches (library stream), and
     # in diagnostic builds the per-wave clock split
@@ -378,7 +423,8 @@ def main():
                                    f"{F}-frame camera orbit per step",
                        "width": W, "height": H, "spp": S, "bvh": f"{a.algo}-{a.k}", "frames_per_step": F,
                        "triangles": int(st["triangles"]), "mode": mode,
-                       "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else ""),
+                       "parallelism": f"image rows interleaved x{world}" +
+                                      (" + RCCL gather of rgb (overlapped)" if world > 1 else ""),
                        **({"gather_verified": verified} if world > 1 else {}),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

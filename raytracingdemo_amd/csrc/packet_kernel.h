@@ -128,6 +128,15 @@
 #define RT_NODE_FETCH 0
 #endif
 
+// Child test of the walk: 0 every lane slab-tests its own ray against each
+// of the W children (records through scalar loads), 1 group interval test:
+// lane l tests child l % W against the interval of the rays of lane group
+// l / W (W lanes), all W x 64/W pairs in one pass (records through one
+// vector load per lane; see group_hits).
+#ifndef RT_GROUP_TEST
+#define RT_GROUP_TEST 0
+#endif
+
 // Occupancy target of the packet kernel (waves per SIMD); 0 = compiler's choice.
 #ifndef RT_PACKET_WPE
 #define RT_PACKET_WPE 0
@@ -341,6 +350,75 @@ __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32&
     }
 }
 
+// Lane-group reductions over groups of G consecutive lanes (G <= 32, a
+// power of 2): ds_swizzle in xor mode (and_mask 0x1F, xor_mask s).
+template <int S>
+__device__ __forceinline__ float swz_xor(float v) {
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (S << 10) | 0x1F));
+}
+template <int G>
+__device__ __forceinline__ float group_min(float v) {
+    if constexpr (G > 1) v = fminf(v, swz_xor<1>(v));
+    if constexpr (G > 2) v = fminf(v, swz_xor<2>(v));
+    if constexpr (G > 4) v = fminf(v, swz_xor<4>(v));
+    if constexpr (G > 8) v = fminf(v, swz_xor<8>(v));
+    static_assert(G <= 16, "groups of up to 16 lanes");
+    return v;
+}
+template <int G>
+__device__ __forceinline__ float group_max(float v) {
+    if constexpr (G > 1) v = fmaxf(v, swz_xor<1>(v));
+    if constexpr (G > 2) v = fmaxf(v, swz_xor<2>(v));
+    if constexpr (G > 4) v = fmaxf(v, swz_xor<4>(v));
+    if constexpr (G > 8) v = fmaxf(v, swz_xor<8>(v));
+    return v;
+}
+
+// Ray interval of a lane group (RT_GROUP_TEST): the group's rays share the
+// origin o (primary rays: the camera position, kernels_common.h gen_ray) and
+// their fp32 reciprocals lie in [i0, i1] per axis.  al / ah = o + 2 pad and
+// o - 2 pad: the lo / hi plane offsets, padded twice as far as the per-lane
+// test's (o + pad, o - pad).
+struct GroupIv {
+    float ix0, ix1, iy0, iy1, iz0, iz1;  // per lane (its group's interval)
+    float alx, ahx, aly, ahy, alz, ahz;  // uniform
+};
+
+// Group interval test of child (lane % W) for ray group (lane / W).  For one
+// axis and a plane at offset d = p - a from the origin, t = d * i is linear
+// in the reciprocal i, so over i in [i0, i1] it lies between d * i0 and
+// d * i1 whatever the signs (a group whose rays straddle the axis plane has
+// i0 < 0 < i1 and simply gets a wide interval).  A ray's near value
+// min(t_lo, t_hi) is therefore >= the least of the four products and its far
+// value <= the greatest, so the test below passes whenever any ray of the
+// group passes the per-lane test: a superset, never a miss.  Rounding: the
+// fp32 errors here are below 2^-23 (|p| + |o|) |i| <= pad |i| / 16 (pad =
+// 2^-19 (|o|max + |coord|max), rt_api.cpp frame_pad), and the extra pad of
+// the offsets moves every bound by pad |i|, so the computed test contains the
+// per-lane computed test (which contains the fp64 reference test).
+__device__ __forceinline__ bool group_hits(const float4 ra, const float2 rb, const GroupIv& g, float tg) {
+    const float dlx = ra.x - g.alx, dhx = ra.y - g.ahx;
+    const float dly = ra.z - g.aly, dhy = ra.w - g.ahy;
+    const float dlz = rb.x - g.alz, dhz = rb.y - g.ahz;
+    const float ax = dlx * g.ix0, bx = dlx * g.ix1, cx = dhx * g.ix0, ex = dhx * g.ix1;
+    const float ay = dly * g.iy0, by = dly * g.iy1, cy = dhy * g.iy0, ey = dhy * g.iy1;
+    const float az = dlz * g.iz0, bz = dlz * g.iz1, cz = dhz * g.iz0, ez = dhz * g.iz1;
+    const float nx = fminf(fminf(ax, bx), fminf(cx, ex)), fx = fmaxf(fmaxf(ax, bx), fmaxf(cx, ex));
+    const float ny = fminf(fminf(ay, by), fminf(cy, ey)), fy = fmaxf(fmaxf(ay, by), fmaxf(cy, ey));
+    const float nz = fminf(fminf(az, bz), fminf(cz, ez)), fz = fmaxf(fmaxf(az, bz), fmaxf(cz, ez));
+    const float t0 = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+    const float t1 = fminf(fminf(fx, fy), fminf(fz, tg));
+    return t0 <= t1;
+}
+
+// Bit c set iff some group's bit c of the ballot is set (groups of W lanes).
+template <int W>
+__device__ __forceinline__ uint32_t fold_groups(uint64_t m) {
+#pragma unroll
+    for (int s = 32; s >= W; s >>= 1) m |= m >> s;
+    return (uint32_t)m & ((1u << W) - 1u);
+}
+
 template <int W, int SP, int K, bool COUNT>
 __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool valid, uint32_t* __restrict__ wstack,
                                              uint2* __restrict__ cand, uint64_t* tacc, float4* __restrict__ wbox4,
@@ -374,6 +452,27 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
     const float oly = (q.oy + pd) * q.iy, ohy = (q.oy - pd) * q.iy;
     const float olz = (q.oz + pd) * q.iz, ohz = (q.oz - pd) * q.iz;
     const f2 nox{-olx, -ohx}, noy{-oly, -ohy}, noz{-olz, -ohz};
+#if RT_GROUP_TEST
+    (void)oct;
+    (void)nox;
+    (void)noy;
+    (void)noz;
+    // the lane group's ray interval (lanes outside the image do not widen it;
+    // a group with none has an empty interval and tg = -1: it passes no test)
+    GroupIv g;
+    g.ix0 = group_min<W>(valid ? q.ix : 3e38f);
+    g.ix1 = group_max<W>(valid ? q.ix : -3e38f);
+    g.iy0 = group_min<W>(valid ? q.iy : 3e38f);
+    g.iy1 = group_max<W>(valid ? q.iy : -3e38f);
+    g.iz0 = group_min<W>(valid ? q.iz : 3e38f);
+    g.iz1 = group_max<W>(valid ? q.iz : -3e38f);
+    g.alx = __builtin_bit_cast(float, uni(__float_as_uint(q.ox + 2.f * pd)));
+    g.ahx = __builtin_bit_cast(float, uni(__float_as_uint(q.ox - 2.f * pd)));
+    g.aly = __builtin_bit_cast(float, uni(__float_as_uint(q.oy + 2.f * pd)));
+    g.ahy = __builtin_bit_cast(float, uni(__float_as_uint(q.oy - 2.f * pd)));
+    g.alz = __builtin_bit_cast(float, uni(__float_as_uint(q.oz + 2.f * pd)));
+    g.ahz = __builtin_bit_cast(float, uni(__float_as_uint(q.oz - 2.f * pd)));
+#endif
 
     uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0, w_tris = 0;  // COUNT only
     uint32_t w_empty = 0;                // COUNT only: node steps where no lane enters any child
@@ -384,6 +483,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
     uint32_t pf_sink = 0, pf_val = 0, pf_val2 = 0;  // L2 prefetch loads (values unused)
 #endif
     float tcull = valid ? __builtin_huge_valf() : -1.f;
+#if RT_GROUP_TEST
+    float tg = group_max<W>(tcull);  // the group's largest culling distance
+#endif
     int nc = 0;         // candidates in the lane's list
     int nsp = 0;        // candidates in the pixel's HBM overflow slots
     float drop = __builtin_huge_valf();  // smallest t lower bound of a dropped candidate
@@ -418,13 +520,32 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                     w_nodes++;
                     n_nodes += valid;
                 }
+#if !RT_GROUP_TEST
                 float bx[W][6];  // child boxes {lx, hx, ly, hy, lz, hz}
+#endif
                 uint32_t refv;   // lane c: child c's ref
 #if RT_POP_CULL
                 float4 cb4;      // lane c: child c's {lx, hx, ly, hy}
                 float2 cb2;      //         and {lz, hz}
 #endif
                 uint32_t meta;   // slot 0's pad: sort axis | valid slots << 2 (bvh_build.cpp set_meta)
+#if RT_GROUP_TEST
+                uint32_t mask;
+                {
+                    // lane l loads child l % W's record (the W records of the
+                    // node, 256 B for W = 8, one request per lane group)
+                    const RT_G float4* cv =
+                        reinterpret_cast<const RT_G float4*>(nodes + (size_t)cur * (32 * W)) + 2 * (lane & (W - 1));
+                    const float4 ra = cv[0];
+                    const float4 rb = cv[1];
+                    refv = __float_as_uint(rb.z);
+                    meta = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(rb.w), 0);
+                    RT_TACC(0, t_n0);
+                    mask = fold_groups<W>(__ballot(group_hits(ra, make_float2(rb.x, rb.y), g, tg))) &
+                           ((1u << (meta >> 2)) - 1u);
+                }
+                RT_TSTAMP(t_n1);
+#else
 #if RT_NODE_FETCH == 0
                 {
                     // scalar path: all W records are loaded before any branch
@@ -522,6 +643,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                 }
 #endif
                 uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);
+#endif  // RT_GROUP_TEST
                 if (COUNT) {
                     w_empty += mask == 0;
                     w_empty_pop += mask == 0 && popped;
@@ -620,6 +742,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                         }
                     }
                 }
+#if RT_GROUP_TEST
+                tg = group_max<W>(tcull);
+#endif
                 RT_TACC(2, t_l0);
             }
         }

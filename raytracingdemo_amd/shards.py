@@ -32,6 +32,19 @@ def deinterleave(gathered, H: int):
     return full[:, :H]
 
 
+def deinterleave_into(gathered, H: int, out):
+    """deinterleave() written into `out` ([F, H, W, ...]) with one copy kernel
+    (no temporary when the shards have no padding rows)."""
+    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+    rest = tuple(gathered.shape[3:])
+    if rows * world == H:
+        perm = (1, 2, 0) + tuple(range(3, gathered.dim()))
+        out.view((F, rows, world) + rest).copy_(gathered.permute(*perm))
+    else:
+        out.copy_(deinterleave(gathered, H))
+    return out
+
+
 def gather_frames(shard, H: int, world: int, rank: int, dst: int = 0, out=None):
     """Gather every rank's [F, rows, W, ...] shard to `dst` and de-interleave there.
 

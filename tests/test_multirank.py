@@ -18,7 +18,7 @@ torch = pytest.importorskip("torch")
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
-from raytracingdemo_amd.shards import deinterleave, gather_frames, rows_per_rank, shard_rows  # noqa: E402
+from raytracingdemo_amd.shards import deinterleave, deinterleave_into, gather_frames, rows_per_rank, shard_rows  # noqa: E402
 
 
 def _free_port() -> int:
@@ -90,3 +90,12 @@ def test_deinterleave_single_process():
             idx = list(shard_rows(r, world, H))
             sh[r, :, : len(idx)] = full[:, idx]
         assert torch.equal(deinterleave(sh, H), full)
+        # the bench's single-copy form (padded and unpadded shards)
+        out = torch.empty_like(full)
+        assert torch.equal(deinterleave_into(sh, H, out), full)
+    H = 12  # rows * world == H: the strided-view copy
+    full = torch.arange(F * H * W * 3, dtype=torch.int32).reshape(F, H, W, 3)
+    for world in (1, 2, 3, 4, 6, 12):
+        rows = rows_per_rank(H, world)
+        sh = torch.stack([full[:, list(shard_rows(r, world, H))] for r in range(world)])
+        assert torch.equal(deinterleave_into(sh, H, torch.empty_like(full)), full)

@@ -1,5 +1,6 @@
-set -e
-b() { timeout -k 10 300 python bench.py --no-cpu --paths --steps 2 --warmup 1 2>&1 | grep -v amdgpu.ids | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1', d['value'], d['segments_traced_per_s_M'], d['kernel_ms_avg'])"; }
-V=$PWD/raytracingdemo_amd/variants
-b base
-for v in p4 p5; do RT_LIB=$V/librtmi355x_$v.so b $v; done
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python bench.py --no-cpu --steps 5 > gpurun_out/b1.log 2>&1 && tail -1 gpurun_out/b1.log | cut -c1-400 &&
+RT_BENCH_REHEARSE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu > gpurun_out/r2.log 2>&1 && tail -1 gpurun_out/r2.log | cut -c1-900 &&
+RT_BENCH_REHEARSE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 3 --steps 3 --warmup 1 --no-cpu > gpurun_out/r3.log 2>&1 && tail -1 gpurun_out/r3.log | cut -c1-900

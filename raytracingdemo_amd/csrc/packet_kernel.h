@@ -332,9 +332,17 @@ __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32&
     asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
 #pragma unroll
     for (int c = 0; c < W; c++) {
+#if RT_PK_SLAB
+        // (lo, hi) plane pairs in one v_pk_fma_f32 each
+        const f2 tx = __builtin_elementwise_fma(f2{bx[c][0], bx[c][1]}, f2{ix, ix}, nox);
+        const f2 ty = __builtin_elementwise_fma(f2{bx[c][2], bx[c][3]}, f2{iy, iy}, noy);
+        const f2 tz = __builtin_elementwise_fma(f2{bx[c][4], bx[c][5]}, f2{iz, iz}, noz);
+        const float tlx = tx.x, thx = tx.y, tly = ty.x, thy = ty.y, tlz = tz.x, thz = tz.y;
+#else
         const float tlx = __builtin_fmaf(bx[c][0], ix, nox.x), thx = __builtin_fmaf(bx[c][1], ix, nox.y);
         const float tly = __builtin_fmaf(bx[c][2], iy, noy.x), thy = __builtin_fmaf(bx[c][3], iy, noy.y);
         const float tlz = __builtin_fmaf(bx[c][4], iz, noz.x), thz = __builtin_fmaf(bx[c][5], iz, noz.y);
+#endif
         float t0, t1;
         if constexpr (OCT < 0) {
             t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));

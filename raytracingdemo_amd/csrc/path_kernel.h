@@ -130,10 +130,21 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
 #else
 #define RT_PATHS_ATTR
 #endif
+// Segments through trace_deferred (fp64 after the walk, RT_PATHS_K LDS
+// candidates per lane) or trace_core (fp64 inside the walk): 1 / 0.
+#ifndef RT_PATHS_DEFER
+#define RT_PATHS_DEFER 1
+#endif
+#ifndef RT_PATHS_K
+#define RT_PATHS_K 4
+#endif
 template <int W, int S>
 __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
                                                int bounces) {
     __shared__ uint2 lds[S][256];
+#if RT_PATHS_DEFER
+    __shared__ uint2 pcand[RT_PATHS_K][256];
+#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int tiles_x = (fp.W + 7) >> 3;
@@ -169,8 +180,13 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                 double w = 1.0;
                 for (int b = 0; b <= bounces; b++) {
                     LaneCounts lc;
+#if RT_PATHS_DEFER
+                    const Win win = trace_deferred<W, S, RT_PATHS_K, false>(sc, [&]() { return with_inv(ray); },
+                                                                            ray_pad(sc, ray), st, pcand, lc);
+#else
                     const Win win =
                         trace_core<W, S, false>(sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, 0, lc);
+#endif
                     segs++;
                     Best hb;
                     hb.dist = win.dist;

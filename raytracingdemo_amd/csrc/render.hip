@@ -263,6 +263,175 @@ __device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, 
     return best;
 }
 
+// The per-lane traversal with the fp64 work deferred (K candidates per lane,
+// cand[c][tid] in LDS): the walk is fp32 only — tri_classify sorts each leaf
+// triangle into reject / borderline / certain (a certain hit's upper bound
+// tightens the culling distance at once) and appends the survivors — and the
+// exact fp64 Moller-Trumbore of the survivors runs after the walk, when the
+// wave's lanes do it together instead of one divergent lane at a time inside
+// the loop.  The winner is the (distance, visit rank) minimum and its
+// reference ancestor chain is re-verified, as in k_resolve.
+// A lane whose list overflows (after compaction against the culling
+// distance), or whose winner the reference cannot see, falls back to
+// trace_core (pass 0 / pass 1): the same answer, the slow way.
+template <int W, int S, int K, bool COUNT, class RayFn>
+__device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S>& st,
+                                              uint2 (*cand)[256], LaneCounts& lc) {
+    constexpr int G = W < 4 ? W : 4;  // children tested per load group
+    const int tid = st.tid;
+    Ray32 q;
+    float tsl;  // distance slack (trace_core's tslack), fp32 rounded up
+    {
+        const Ray64 ray = ray_of();
+        q = make_ray32(ray, pad);
+        tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
+    }
+    const bool sx = q.ix < 0.f, sy = q.iy < 0.f, sz = q.iz < 0.f;
+    float tcull = __builtin_huge_valf();
+    int nc = 0;
+    bool over = false;
+    st.top = 0;
+    uint32_t cur = sc.root_ref;
+    {
+        const float* b = sc.root_box;
+        const float tx0 = __builtin_fmaf(q.ix >= 0.f ? b[0] : b[1], q.ix, -q.onx);
+        const float tx1 = __builtin_fmaf(q.ix >= 0.f ? b[1] : b[0], q.ix, -q.ofx);
+        const float ty0 = __builtin_fmaf(q.iy >= 0.f ? b[2] : b[3], q.iy, -q.ony);
+        const float ty1 = __builtin_fmaf(q.iy >= 0.f ? b[3] : b[2], q.iy, -q.ofy);
+        const float tz0 = __builtin_fmaf(q.iz >= 0.f ? b[4] : b[5], q.iz, -q.onz);
+        const float tz1 = __builtin_fmaf(q.iz >= 0.f ? b[5] : b[4], q.iz, -q.ofz);
+        const float tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, 0.f));
+        const float tf = fminf(fminf(tx1, ty1), tz1);
+        if (!(tn <= tf)) cur = RT_INVALID_REF;
+    }
+    while (cur != RT_INVALID_REF) {
+        if (!(cur & RT_LEAF_BIT)) {
+            if (COUNT) lc.nodes++;
+            const float4* nb = reinterpret_cast<const float4*>(sc.nodes + (size_t)cur * sc.node_bytes);
+            float tn[W];
+            uint32_t rb[W];
+            uint32_t mask = 0;
+#pragma unroll
+            for (int g = 0; g < W; g += G) {
+                float4 lo[G], hi[G];  // {lx,hx,ly,hy}, {lz,hz,ref,pad}
+#pragma unroll
+                for (int c = 0; c < G; c++) {
+                    lo[c] = nb[2 * (g + c)];
+                    hi[c] = nb[2 * (g + c) + 1];
+                }
+#pragma unroll
+                for (int c = 0; c < G; c++) {
+                    const float a0 = __builtin_fmaf(sx ? lo[c].y : lo[c].x, q.ix, -q.onx);
+                    const float a1 = __builtin_fmaf(sx ? lo[c].x : lo[c].y, q.ix, -q.ofx);
+                    const float b0 = __builtin_fmaf(sy ? lo[c].w : lo[c].z, q.iy, -q.ony);
+                    const float b1 = __builtin_fmaf(sy ? lo[c].z : lo[c].w, q.iy, -q.ofy);
+                    const float c0 = __builtin_fmaf(sz ? hi[c].y : hi[c].x, q.iz, -q.onz);
+                    const float c1 = __builtin_fmaf(sz ? hi[c].x : hi[c].y, q.iz, -q.ofz);
+                    const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
+                    const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
+                    const uint32_t ref = __float_as_uint(hi[c].z);
+                    tn[g + c] = t0;
+                    rb[g + c] = ref;
+                    if (t0 <= t1 && ref != RT_INVALID_REF) mask |= 1u << (g + c);
+                }
+            }
+            if (mask) {
+                // push all hit children but the nearest, farthest first
+                while (__builtin_popcount(mask) > 1) {
+                    float far_t = -1.f;
+                    int far_c = 0;
+#pragma unroll
+                    for (int c = 0; c < W; c++)
+                        if (((mask >> c) & 1u) && tn[c] > far_t) { far_t = tn[c]; far_c = c; }
+                    st.push(rb[far_c], far_t);
+                    mask &= ~(1u << far_c);
+                }
+                cur = rb[__builtin_ctz(mask)];
+                continue;
+            }
+        } else {
+            const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+            const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+            for (uint32_t k = first; k < first + cnt; k++) {
+                const float4* R = reinterpret_cast<const float4*>(sc.tri32 + 12 * (size_t)k);
+                if (COUNT) lc.pre++;
+                float tl, tu;
+                const int cls = tri_classify(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull, tl, tu);
+                if (cls == 0) continue;
+                // dist of a certain hit <= (tu + slack)(1 + 2^-20)
+                if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
+                if (nc == K) {
+                    int m = 0;
+                    for (int c = 0; c < K; c++) {
+                        const uint2 e = cand[c][tid];
+                        if (__uint_as_float(e.y) <= tcull) cand[m++][tid] = e;
+                    }
+                    nc = m;
+                }
+                if (nc < K) {
+                    cand[nc][tid] = make_uint2(k, __float_as_uint(tl));
+                    nc++;
+                } else {
+                    over = true;
+                }
+            }
+        }
+        // pop the next subtree still in front of the culling distance
+        cur = RT_INVALID_REF;
+        while (st.top > 0) {
+            const uint2 e = st.pop();
+            if (__uint_as_float(e.y) <= tcull) {
+                cur = e.x;
+                break;
+            }
+        }
+    }
+    if (over) return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 0, lc);
+    // exact resolve of the survivors (k_resolve's selection)
+    Win best;
+    best.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
+    best.t = 0.0;
+    best.rank = 0xFFFFFFFFu;
+    best.tri = -1;
+    if (nc == 0) return best;
+    const Ray64 ray = ray_of();
+    for (int c = 0; c < nc; c++) {
+        const uint2 e = cand[c][tid];
+        if (__uint_as_float(e.y) > tcull) continue;  // cannot beat a certain hit
+        if (COUNT) lc.tris++;
+        const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)e.x;
+        double t;
+        if (!mt64(T, ray, t)) continue;
+        double hx, hy, hz;
+        const double d = hit_dist(ray, t, hx, hy, hz);
+        bool take = d < best.dist;
+        if (!take && d == best.dist) {  // tie: the reference keeps the earlier visit
+            if (best.rank == 0xFFFFFFFFu) best.rank = sc.tri_rank[best.tri];
+            const uint32_t rank = sc.tri_rank[e.x];
+            take = rank < best.rank;
+            if (take) best.rank = rank;
+        } else if (take) {
+            best.rank = 0xFFFFFFFFu;  // visit ranks are loaded on a tie only
+        }
+        if (take) {
+            best.dist = d;
+            best.t = t;
+            best.tri = (int32_t)e.x;
+        }
+    }
+    if (best.tri < 0) return best;
+    if (best.rank == 0xFFFFFFFFu) best.rank = sc.tri_rank[best.tri];
+    // the reference must see the winner: re-verify its ancestor chain
+    double hx, hy, hz;
+    (void)hit_dist(ray, best.t, hx, hy, hz);
+    const uint32_t leaf =
+        reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + RT_T64_IDLEAF)->y;
+    if (COUNT) lc.chain++;
+    if (chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz)) return best;
+    if (chain_ok(sc, leaf, ray, lc.chain_nodes)) return best;
+    return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 1, lc);
+}
+
 // Exact per-lane traversal of the primary ray of pixel (i, r) of frame f.
 template <int W, int S, bool COUNT>
 __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,

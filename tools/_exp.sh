@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py --no-cpu --steps 5 > gpurun_out/b1.log 2>&1 && tail -1 gpurun_out/b1.log | cut -c1-400 &&
-RT_BENCH_REHEARSE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu > gpurun_out/r2.log 2>&1 && tail -1 gpurun_out/r2.log | cut -c1-900 &&
-RT_BENCH_REHEARSE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 3 --steps 3 --warmup 1 --no-cpu > gpurun_out/r3.log 2>&1 && tail -1 gpurun_out/r3.log | cut -c1-900
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "paths" -p no:cacheprovider --timeout 300 > gpurun_out/tpaths.log 2>&1; rc=$?; tail -3 gpurun_out/tpaths.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/pd.log 2>&1 && tail -1 gpurun_out/pd.log | cut -c1-250 &&
+RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_nodefer.so timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/pn.log 2>&1 && tail -1 gpurun_out/pn.log | cut -c1-250

@@ -652,6 +652,10 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
 }
 
 constexpr int kLdsStack = 16;      // per-lane kernel: LDS ring entries per lane (8 B each)
+#ifndef RT_PATHS_STACK
+#define RT_PATHS_STACK 16
+#endif
+constexpr int kPathStack = RT_PATHS_STACK;  // path kernel: LDS ring entries per lane
 constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (4 B each)
 constexpr int kCandidates = RT_CAND_LDS;  // packet kernel: LDS candidate list entries per lane (8 B each)
 constexpr int kFixupGrid = 256;    // k_fixup blocks (the redo list is short)
@@ -758,7 +762,7 @@ int exact_blocks_per_cu(int width, uint32_t stack_bound) {
     return n < 8 ? n : 8;
 }
 
-int exact_lds_stack() { return kLdsStack; }
+int exact_lds_stack() { return kLdsStack < kPathStack ? kLdsStack : kPathStack; }  // the smaller ring: spill sizing
 int packet_candidates() { return RT_CAND_SLOTS; }  // HBM slots per pixel (LDS list + overflow)
 
 // Host entry: validates the launch geometry against what the kernels assume
@@ -818,17 +822,17 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
                         int bounces, hipStream_t s, const hipEvent_t* ev) {
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
     if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.tile_ctr || !aux.spill || aux.grid <= 0 ||
-        aux.spill_cap + kLdsStack < sc.stack_bound)
+        aux.spill_cap + kPathStack < sc.stack_bound)
         return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const dim3 grid((unsigned)aux.grid), blk(256);
     if (ev) (void)hipEventRecord(ev[0], s);
     switch (sc.width) {
-        case 2: hipLaunchKernelGGL((k_paths<2, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
-        case 4: hipLaunchKernelGGL((k_paths<4, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
-        case 8: hipLaunchKernelGGL((k_paths<8, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
-        case 16: hipLaunchKernelGGL((k_paths<16, kLdsStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 8: hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         default: return hipErrorInvalidValue;
     }
     if (ev) (void)hipEventRecord(ev[1], s);

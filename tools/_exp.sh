@@ -1,6 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "paths" -p no:cacheprovider --timeout 300 > gpurun_out/tpaths.log 2>&1; rc=$?; tail -3 gpurun_out/tpaths.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/pd.log 2>&1 && tail -1 gpurun_out/pd.log | cut -c1-250 &&
-RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_nodefer.so timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/pn.log 2>&1 && tail -1 gpurun_out/pn.log | cut -c1-250
+timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/p_base.log 2>&1 && tail -1 gpurun_out/p_base.log | cut -c1-160 || exit 1
+for v in w4s8 w5s8 w6s8; do
+RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/p_$v.log 2>&1 && echo $v && tail -1 gpurun_out/p_$v.log | cut -c1-160 || exit 1
+done

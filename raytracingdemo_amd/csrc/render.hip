@@ -274,18 +274,16 @@ __device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, 
 // A lane whose list overflows (after compaction against the culling
 // distance), or whose winner the reference cannot see, falls back to
 // trace_core (pass 0 / pass 1): the same answer, the slow way.
-template <int W, int S, int K, bool COUNT, class RayFn>
-__device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S>& st,
-                                              uint2 (*cand)[256], LaneCounts& lc) {
+//
+// lane_walk: the fp32 walk of ray q; on return cand[0..nc) hold the
+// survivors ({triangle, bits of t lower bound}), tcull the culling distance,
+// and `over` is set if a survivor had to be dropped.
+template <int W, int S, int K, bool COUNT>
+__device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, float tsl, LaneStack<S>& st,
+                                          uint2 (*cand)[256], LaneCounts& lc, float& tcull_out, int& nc_out,
+                                          bool& over_out) {
     constexpr int G = W < 4 ? W : 4;  // children tested per load group
     const int tid = st.tid;
-    Ray32 q;
-    float tsl;  // distance slack (trace_core's tslack), fp32 rounded up
-    {
-        const Ray64 ray = ray_of();
-        q = make_ray32(ray, pad);
-        tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
-    }
     const bool sx = q.ix < 0.f, sy = q.iy < 0.f, sz = q.iz < 0.f;
     float tcull = __builtin_huge_valf();
     int nc = 0;
@@ -386,17 +384,24 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
             }
         }
     }
-    if (over) return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 0, lc);
-    // exact resolve of the survivors (k_resolve's selection)
-    Win best;
+    tcull_out = tcull;
+    nc_out = nc;
+    over_out = over;
+}
+
+// Exact resolve of a candidate list (k_resolve's selection): the (distance,
+// visit rank) minimum of the fp64 hits among get(0 .. nc-1) whose t lower
+// bound is within tcull.  Returns 0 with the winner in best (tri < 0: none),
+// or 1 if the reference cannot see the winner (its ancestor chain fails).
+template <bool COUNT, class GetFn>
+__device__ __forceinline__ int resolve_cands(const RtDevScene& sc, const Ray64& ray, GetFn&& get, int nc, float tcull,
+                                             Win& best, LaneCounts& lc) {
     best.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
     best.t = 0.0;
     best.rank = 0xFFFFFFFFu;
     best.tri = -1;
-    if (nc == 0) return best;
-    const Ray64 ray = ray_of();
     for (int c = 0; c < nc; c++) {
-        const uint2 e = cand[c][tid];
+        const uint2 e = get(c);
         if (__uint_as_float(e.y) > tcull) continue;  // cannot beat a certain hit
         if (COUNT) lc.tris++;
         const double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)e.x;
@@ -419,7 +424,7 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
             best.tri = (int32_t)e.x;
         }
     }
-    if (best.tri < 0) return best;
+    if (best.tri < 0) return 0;
     if (best.rank == 0xFFFFFFFFu) best.rank = sc.tri_rank[best.tri];
     // the reference must see the winner: re-verify its ancestor chain
     double hx, hy, hz;
@@ -427,8 +432,30 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
     const uint32_t leaf =
         reinterpret_cast<const uint2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)best.tri + RT_T64_IDLEAF)->y;
     if (COUNT) lc.chain++;
-    if (chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz)) return best;
-    if (chain_ok(sc, leaf, ray, lc.chain_nodes)) return best;
+    if (chain_fast_ok(sc.rbox + 6 * (size_t)leaf, ray, hx, hy, hz)) return 0;
+    if (chain_ok(sc, leaf, ray, lc.chain_nodes)) return 0;
+    return 1;
+}
+
+template <int W, int S, int K, bool COUNT, class RayFn>
+__device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S>& st,
+                                              uint2 (*cand)[256], LaneCounts& lc) {
+    Ray32 q;
+    float tsl;  // distance slack (trace_core's tslack), fp32 rounded up
+    {
+        const Ray64 ray = ray_of();
+        q = make_ray32(ray, pad);
+        tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
+    }
+    float tcull;
+    int nc;
+    bool over;
+    lane_walk<W, S, K, COUNT>(sc, q, tsl, st, cand, lc, tcull, nc, over);
+    if (over) return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 0, lc);
+    Win best;
+    const int tid = st.tid;
+    if (resolve_cands<COUNT>(sc, ray_of(), [&](int c) { return cand[c][tid]; }, nc, tcull, best, lc) == 0)
+        return best;
     return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 1, lc);
 }
 
@@ -500,6 +527,7 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
 
 #include "packet_kernel.h"
 #include "path_kernel.h"
+#include "wavefront_paths.h"
 
 // Finishes the pixels the packet kernel handed over (redo list, count in
 // tile_ctr[RT_REDO_COUNT]) with the per-lane exact kernel: from pass 0 after a candidate
@@ -762,7 +790,11 @@ int exact_blocks_per_cu(int width, uint32_t stack_bound) {
     return n < 8 ? n : 8;
 }
 
-int exact_lds_stack() { return kLdsStack < kPathStack ? kLdsStack : kPathStack; }  // the smaller ring: spill sizing
+// the smallest LDS ring of the per-lane kernels (spill sizing)
+int exact_lds_stack() {
+    const int a = kLdsStack < kPathStack ? kLdsStack : kPathStack;
+    return a < RT_PW_STACK ? a : RT_PW_STACK;
+}
 int packet_candidates() { return RT_CAND_SLOTS; }  // HBM slots per pixel (LDS list + overflow)
 
 // Host entry: validates the launch geometry against what the kernels assume
@@ -834,6 +866,47 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
         case 8: hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         default: return hipErrorInvalidValue;
+    }
+    if (ev) (void)hipEventRecord(ev[1], s);
+    return hipGetLastError();
+}
+
+// Wavefront path tracing of one pose (wavefront_paths.h): per sample, walk +
+// shade for each of the 1 + bounces segments, then the accumulation.  ws.ctl
+// must be zero on entry (the kernels leave it zero).
+hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
+                           uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev) {
+    if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
+    if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.spill || aux.grid <= 0 || !aux.cand ||
+        aux.cand_cap < ws.P || ws.P != (uint32_t)fp.W * (uint32_t)fp.nrows || RT_PW_K > RT_CAND_SLOTS ||
+        aux.spill_cap + RT_PW_STACK < sc.stack_bound || aux.spill_cap + kLdsStack < sc.stack_bound)
+        return hipErrorInvalidValue;
+    const dim3 grid((unsigned)aux.grid), blk(256), agrid((ws.P + 255u) / 256u);
+    if (ev) (void)hipEventRecord(ev[0], s);
+    for (uint32_t smp = 0; smp < (uint32_t)fp.spp; smp++) {
+        for (int b = 0; b <= bounces; b++) {
+            switch (sc.width) {
+                case 2:
+                    hipLaunchKernelGGL((k_pw_walk<2, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
+                    hipLaunchKernelGGL((k_pw_shade<2, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
+                    break;
+                case 4:
+                    hipLaunchKernelGGL((k_pw_walk<4, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
+                    hipLaunchKernelGGL((k_pw_shade<4, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
+                    break;
+                case 8:
+                    hipLaunchKernelGGL((k_pw_walk<8, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
+                    hipLaunchKernelGGL((k_pw_shade<8, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
+                    break;
+                case 16:
+                    hipLaunchKernelGGL((k_pw_walk<16, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
+                    hipLaunchKernelGGL((k_pw_shade<16, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
+                    break;
+                default:
+                    return hipErrorInvalidValue;
+            }
+        }
+        hipLaunchKernelGGL(k_pw_accum, agrid, blk, 0, s, fp, ws, smp);
     }
     if (ev) (void)hipEventRecord(ev[1], s);
     return hipGetLastError();

@@ -22,6 +22,8 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 int exact_blocks_per_cu(int width, uint32_t stack_bound);
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
                         int bounces, hipStream_t s, const hipEvent_t* ev);
+hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
+                           uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
 int exact_lds_stack();
 }
@@ -84,6 +86,8 @@ struct Replica {
     uint64_t redo_cap = 0;
     void* d_cand = nullptr;      // packet kernel -> resolve kernel candidate lists
     uint64_t cand_cap = 0;       // pixels
+    void* d_pw = nullptr;        // wavefront path tracer workspace (PathWs), pw_cap paths
+    uint64_t pw_cap = 0;
     // RT_FLAG_TIMING: events around the traversal kernel per timed launch,
     // read and recycled by rt_frame_stats
     std::vector<std::array<hipEvent_t, 2>> tev;
@@ -122,6 +126,7 @@ void free_replica(Replica& r) {
     if (r.d_spill) hipFree(r.d_spill);
     if (r.d_redo) hipFree(r.d_redo);
     if (r.d_cand) hipFree(r.d_cand);
+    if (r.d_pw) hipFree(r.d_pw);
     for (auto& a : r.tev)
         for (hipEvent_t e : a) hipEventDestroy(e);
     if (r.ev_in) hipEventDestroy(r.ev_in);
@@ -239,6 +244,36 @@ void ensure_redo(Replica& r, uint64_t pixels) {
     r.redo_cap = 0;
     HIP_TRY(hipMalloc(&r.d_redo, pixels * sizeof(uint32_t)));
     r.redo_cap = pixels;
+}
+
+// Wavefront path-tracer workspace for P paths (grown, never shrunk): two
+// segment queues (64 B per entry), L and acc (24 B per path), control words.
+PathWs ensure_pw(Replica& r, uint64_t P) {
+    if (r.pw_cap < P) {
+        HIP_TRY(hipDeviceSynchronize());  // earlier launches may still use it
+        if (r.d_pw) HIP_TRY(hipFree(r.d_pw));
+        r.d_pw = nullptr;
+        r.pw_cap = 0;
+        HIP_TRY(hipMalloc(&r.d_pw, P * (2 * 64 + 2 * 24) + 256));
+        r.pw_cap = P;
+    }
+    uint8_t* base = static_cast<uint8_t*>(r.d_pw);
+    PathWs ws{};
+    ws.qray[0] = reinterpret_cast<double*>(base);
+    ws.qray[1] = reinterpret_cast<double*>(base + r.pw_cap * 64);
+    ws.L = reinterpret_cast<double*>(base + r.pw_cap * 128);
+    ws.acc = reinterpret_cast<double*>(base + r.pw_cap * 152);
+    ws.ctl = reinterpret_cast<uint32_t*>(base + r.pw_cap * 176);
+    ws.P = (uint32_t)P;
+    return ws;
+}
+
+// Paths through the megakernel (default, path_kernel.h k_paths) or the
+// wavefront pipeline (RT_PATHS_WF=1, wavefront_paths.h; bit-identical, but
+// 1.94 vs 2.81 G nominal rays/s on config c5: DESIGN.md §11).
+bool paths_wavefront() {
+    const char* e = std::getenv("RT_PATHS_WF");  // read per call: tests switch it in-process
+    return e && std::atoi(e) != 0;
 }
 
 void check_camera(const rt_scene* s, const rt_camera* c) {
@@ -584,8 +619,18 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             }
             tev = r->tev[r->tev_used++].data();
         }
-        order_on(*r, st);
-        const hipError_t e = rt::launch_paths(r->dev, fp, aux_of(*r), (uint32_t)frame, bounces, st, tev);
+        hipError_t e;
+        if (paths_wavefront()) {
+            const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows;
+            ensure_redo(*r, P);  // candidate lists, stride P
+            const PathWs ws = ensure_pw(*r, P);
+            order_on(*r, st);
+            HIP_TRY(hipMemsetAsync(ws.ctl, 0, 16 * sizeof(uint32_t), st));
+            e = rt::launch_paths_wf(r->dev, fp, aux_of(*r), ws, (uint32_t)frame, bounces, st, tev);
+        } else {
+            order_on(*r, st);
+            e = rt::launch_paths(r->dev, fp, aux_of(*r), (uint32_t)frame, bounces, st, tev);
+        }
         r->fresh = false;  // the work queue is left dirty: the next packet launch clears it
         HIP_TRY(e);
         return RT_OK;

@@ -147,3 +147,12 @@ struct RtFrameParams {
     RT_G unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits, chain_nodes] or NULL
     RtFrameCam cam[RT_MAX_BATCH];
 };
+
+// Workspace of the wavefront path tracer (wavefront_paths.h), per replica.
+struct PathWs {
+    RT_G double* qray[2];  // segment queues: 8 doubles per entry {o, d, path id (low word of [6]), -}
+    RT_G double* L;        // 3 per path: the current sample's radiance
+    RT_G double* acc;      // 3 per pixel: sum of the samples' radiance
+    RT_G uint32_t* ctl;    // [0], [1]: entries in qray[0], qray[1]; [2]: walk cursor (zero between launches)
+    uint32_t P;            // paths per sample = pixels of the shard
+};

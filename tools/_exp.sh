@@ -1,7 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/p_base.log 2>&1 && tail -1 gpurun_out/p_base.log | cut -c1-160 || exit 1
-for v in w4s8 w5s8 w6s8; do
-RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/p_$v.log 2>&1 && echo $v && tail -1 gpurun_out/p_$v.log | cut -c1-160 || exit 1
-done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pwprof -o pw -- python bench.py --paths --no-cpu --steps 1 --warmup 0 > gpurun_out/pwprof.log 2>&1; echo rc=$?
+cut -d, -f1-5 gpurun_out/pwprof/pw_kernel_stats.csv | head -12

@@ -123,6 +123,12 @@
 #define RT_OCT_TREE 0
 #endif
 
+// Octant dispatch hoisted out of the walk: the whole node loop is
+// specialised per tile octant (9 copies), instead of a per-step dispatch.
+#ifndef RT_OCT_HOIST
+#define RT_OCT_HOIST 1
+#endif
+
 // Node record fetch: 0 scalar loads (default), 1 uniform vector loads.
 #ifndef RT_NODE_FETCH
 #define RT_NODE_FETCH 0
@@ -514,6 +520,10 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
 #if RT_PRIO_STEPS
     uint32_t steps = 0;
 #endif
+#if RT_OCT_HOIST
+    // the walk specialised on the tile's octant (one dispatch per tile, not per node step)
+    auto walk = [&]<int OCT>() __attribute__((always_inline)) {
+#endif
     for (;;) {
 #if RT_PRIO_STEPS
         steps++;
@@ -616,7 +626,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                 // all lanes' rays share the tile's direction signs (nearly every
                 // tile): the near/far plane of each axis is known, no per-axis
                 // min/max; otherwise the general test
-#if RT_OCT_TREE
+#if RT_OCT_HOIST
+                child_hits<W, OCT>(bx, q, nox, noy, noz, tcull, hm);
+#elif RT_OCT_TREE
                 // binary dispatch on the octant bits (3 uniform branches)
                 if (oct > 7) {
                     child_hits<W, -1>(bx, q, nox, noy, noz, tcull, hm);
@@ -787,6 +799,20 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
 #endif
         RT_TACC(3, t_p0);
     }
+#if RT_OCT_HOIST
+    };
+    switch (oct) {
+        case 0: walk.template operator()<0>(); break;
+        case 1: walk.template operator()<1>(); break;
+        case 2: walk.template operator()<2>(); break;
+        case 3: walk.template operator()<3>(); break;
+        case 4: walk.template operator()<4>(); break;
+        case 5: walk.template operator()<5>(); break;
+        case 6: walk.template operator()<6>(); break;
+        case 7: walk.template operator()<7>(); break;
+        default: walk.template operator()<-1>(); break;
+    }
+#endif
     RT_TSTAMP(t_r0);
 #if RT_PREFETCH
     asm volatile("" ::"v"(pf_sink ^ pf_val ^ pf_val2));  // keeps the prefetch loads

@@ -203,6 +203,23 @@ __device__ __forceinline__ uint32_t any_bit(uint64_t m) {
 template <int W>
 __device__ __forceinline__ uint32_t any_mask(const uint64_t (&hm)[W]) {
     uint32_t m = 0;
+#if RT_ANY_ADDC == 2
+    if constexpr (W == 8) {
+        // one asm block: no hazard padding between the children's pairs
+        asm("s_cmp_lg_u64 %1, 0\n\ts_addc_u32 %0, %0, %0\n\t"
+            "s_cmp_lg_u64 %2, 0\n\ts_addc_u32 %0, %0, %0\n\t"
+            "s_cmp_lg_u64 %3, 0\n\ts_addc_u32 %0, %0, %0\n\t"
+            "s_cmp_lg_u64 %4, 0\n\ts_addc_u32 %0, %0, %0\n\t"
+            "s_cmp_lg_u64 %5, 0\n\ts_addc_u32 %0, %0, %0\n\t"
+            "s_cmp_lg_u64 %6, 0\n\ts_addc_u32 %0, %0, %0\n\t"
+            "s_cmp_lg_u64 %7, 0\n\ts_addc_u32 %0, %0, %0\n\t"
+            "s_cmp_lg_u64 %8, 0\n\ts_addc_u32 %0, %0, %0"
+            : "+s"(m)
+            : "s"(hm[7]), "s"(hm[6]), "s"(hm[5]), "s"(hm[4]), "s"(hm[3]), "s"(hm[2]), "s"(hm[1]), "s"(hm[0])
+            : "scc");
+        return m;
+    }
+#endif
 #if RT_ANY_ADDC
     // two SALU per child: SCC = (mask != 0), then m = 2m + SCC (children
     // from the last down, so child c lands in bit c)
@@ -335,7 +352,9 @@ __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32&
     // fresh copies per specialisation: stops the compiler from hoisting the
     // (identical) plane fmas of every switch case above the switch
     float ix = q.ix, iy = q.iy, iz = q.iz;
+#if !RT_OCT_HOIST
     asm volatile("" : "+v"(ix), "+v"(iy), "+v"(iz));
+#endif
 #pragma unroll
     for (int c = 0; c < W; c++) {
 #if RT_PK_SLAB
@@ -524,6 +543,14 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
     // the walk specialised on the tile's octant (one dispatch per tile, not per node step)
     auto walk = [&]<int OCT>() __attribute__((always_inline)) {
 #endif
+    // (without pop-time culling every popped ref is a real node or leaf, so
+    // only the root can be invalid: tested once, not per step)
+#if RT_OCT_HOIST
+    constexpr bool kRootOnly = !RT_POP_CULL;
+    if (kRootOnly && cur == RT_INVALID_REF) return;  // from the walk lambda
+#else
+    constexpr bool kRootOnly = false;
+#endif
     for (;;) {
 #if RT_PRIO_STEPS
         steps++;
@@ -531,7 +558,7 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
         if (steps == 2 * RT_PRIO_STEPS) __builtin_amdgcn_s_setprio(2);
         if (steps == 3 * RT_PRIO_STEPS) __builtin_amdgcn_s_setprio(3);
 #endif
-        if (cur != RT_INVALID_REF) {
+        if (kRootOnly || cur != RT_INVALID_REF) {
             if (!(cur & RT_LEAF_BIT)) {
                 RT_TSTAMP(t_n0);
                 if (COUNT || RT_DIAG_WAVE_STATS) {

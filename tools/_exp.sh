@@ -2,8 +2,10 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_nohoist.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 > gpurun_out/t2.log 2>&1; rc=$?; tail -2 gpurun_out/t2.log; [ $rc -eq 0 ] || exit $rc
-for rep in 1 2 3; do
-timeout -k 10 300 python bench.py --no-cpu --steps 10 > gpurun_out/r$rep.log 2>&1 && tail -1 gpurun_out/r$rep.log | cut -c1-140 || exit 1
-done
-grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/r*.log
+RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_f2.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 -k "sponza or batch or overflow" > gpurun_out/t2.log 2>&1; rc=$?; tail -2 gpurun_out/t2.log; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2; do
+for v in base f0 f2; do
+if [ $v = base ]; then L=""; else L=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so; fi
+RT_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 10 > gpurun_out/$v$rep.log 2>&1 || exit 1
+done; done
+grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/base*.log gpurun_out/f0*.log gpurun_out/f2*.log

@@ -923,6 +923,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
 // closer hit in its LIFO order (stack_bvh.hpp:633).  The winner's ancestor
 // chain is re-verified (the reference must see the triangle); a failure or
 // a candidate-list overflow sends the pixel to k_fixup.
+#ifndef RT_RESOLVE_PRELOAD
+#define RT_RESOLVE_PRELOAD 1
+#endif
 #ifndef RT_RESOLVE_SPEC
 #define RT_RESOLVE_SPEC 1
 #endif
@@ -958,16 +961,31 @@ __device__ __forceinline__ void resolve_sample(const RtDevScene& sc, const RtFra
     sh = Shade{0.0, 0.0, 0.0, RT_INVALID_REF};
     redo = 0;
     const uint32_t nlist = cnt & kCandCount;
+#if RT_RESOLVE_PRELOAD
+    // the whole 128-B record of entry 0 is requested as soon as its index
+    // arrives, and the fp64 ray is built while it is in flight (one
+    // dependent round trip instead of three: MT part, v0, shading fields)
+    double R0[RT_TRI64_DOUBLES];
+    if (cnt != 0) {
+        const RT_G double2* T2 = reinterpret_cast<const RT_G double2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)e0.x);
+#pragma unroll
+        for (int k = 0; k < RT_TRI64_DOUBLES / 2; k++) {
+            const double2 v = T2[k];
+            R0[2 * k] = v.x;
+            R0[2 * k + 1] = v.y;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the ray's fp64 set-up
+    }
+#endif
     if (cnt != 0) {
         const Ray64 ray = gen_ray<false>(fp, cam, i, fp.row0 + r * fp.row_stride);
         double best_t = 0.0;
         uint32_t leaf = 0;
         float lb[6];
-        // exact test of candidate e, kept if it is the (distance, visit rank) minimum
-        auto consider = [&](const uint2 e) {
+        // exact test of candidate e (record T: global or a register copy),
+        // kept if it is the (distance, visit rank) minimum
+        auto consider_rec = [&](const uint2 e, const auto* T) {
             if (COUNT) n_tris++;
-            // one 128-B record: triangle, normal, id, leaf and its box
-            const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)e.x;
             double t;
             if (!mt64(T, ray, t)) return;
             double hx, hy, hz;
@@ -992,15 +1010,23 @@ __device__ __forceinline__ void resolve_sample(const RtDevScene& sc, const RtFra
                 sh.nx = T[RT_T64_NORMAL];
                 sh.ny = T[RT_T64_NORMAL + 1];
                 sh.nz = T[RT_T64_NORMAL + 2];
-                const uint2 il = *reinterpret_cast<const RT_G uint2*>(T + RT_T64_IDLEAF);
-                sh.id = il.x;
-                leaf = il.y;
-                const RT_G float* B = reinterpret_cast<const RT_G float*>(T + RT_T64_BOX);
+                const uint64_t il = __builtin_bit_cast(uint64_t, (double)T[RT_T64_IDLEAF]);
+                sh.id = (uint32_t)il;
+                leaf = (uint32_t)(il >> 32);
 #pragma unroll
-                for (int a = 0; a < 6; a++) lb[a] = B[a];
+                for (int a = 0; a < 3; a++) {
+                    const uint64_t bb = __builtin_bit_cast(uint64_t, (double)T[RT_T64_BOX + a]);
+                    lb[2 * a] = __uint_as_float((uint32_t)bb);
+                    lb[2 * a + 1] = __uint_as_float((uint32_t)(bb >> 32));
+                }
             }
         };
-#if RT_RESOLVE_SPEC
+        // one 128-B record per candidate: triangle, normal, id, leaf and its box
+        auto consider = [&](const uint2 e) { consider_rec(e, sc.tri64 + RT_TRI64_DOUBLES * (size_t)e.x); };
+#if RT_RESOLVE_PRELOAD
+        if (nlist > 0) consider_rec(e0, R0);
+        for (uint32_t c = 1; c < nlist; c++) consider(cl[(size_t)c * npix + o]);
+#elif RT_RESOLVE_SPEC
         if (nlist > 0) consider(e0);
         for (uint32_t c = 1; c < nlist; c++) consider(cl[(size_t)c * npix + o]);
 #else

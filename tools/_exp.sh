@@ -1,11 +1,12 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_f2.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 -k "sponza or batch or overflow" > gpurun_out/t2.log 2>&1; rc=$?; tail -2 gpurun_out/t2.log; [ $rc -eq 0 ] || exit $rc
-for rep in 1 2; do
-for v in base f0 f2; do
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_rtdemo.py -m gpu -x -q -p no:cacheprovider --timeout 300 > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
+for rep in 1 2 3; do
+for v in base nopre; do
 if [ $v = base ]; then L=""; else L=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so; fi
 RT_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 10 > gpurun_out/$v$rep.log 2>&1 || exit 1
 done; done
-grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/base*.log gpurun_out/f0*.log gpurun_out/f2*.log
+grep -o '"value": [0-9.]*' gpurun_out/base*.log gpurun_out/nopre*.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rp -o r -- python bench.py --no-cpu --steps 3 --warmup 1 > gpurun_out/rp.log 2>&1
+grep -h "k_resolve<false, false>\|k_trace_packet<8, 128, 8, false>" gpurun_out/rp/r_kernel_stats.csv | cut -d, -f1-4

@@ -947,12 +947,17 @@ __device__ __forceinline__ void resolve_sample(const RtDevScene& sc, const RtFra
                                                Shade& sh, uint32_t& redo, uint32_t& n_tris, uint32_t& n_chain,
                                                uint32_t& n_chain_nodes) {
     const RtFrameCam& cam = fp.cam[f];
-    const uint32_t cnt = active ? aux.cand_cnt[o] : 0u;
     const RT_G uint2* const cl = reinterpret_cast<const RT_G uint2*>(aux.cand);
+    uint32_t cnt = 0u;
 #if RT_RESOLVE_SPEC
     // entry 0 is loaded alongside the count (one dependent round trip less)
     uint2 e0 = make_uint2(0u, 0u);
-    if (active) e0 = cl[o];
+    if (active) {
+        cnt = aux.cand_cnt[o];
+        e0 = cl[o];
+    }
+#else
+    if (active) cnt = aux.cand_cnt[o];
 #endif
     out.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
     out.rank = 0xFFFFFFFFu;
@@ -966,8 +971,12 @@ __device__ __forceinline__ void resolve_sample(const RtDevScene& sc, const RtFra
     // arrives, and the fp64 ray is built while it is in flight (one
     // dependent round trip instead of three: MT part, v0, shading fields)
     double R0[RT_TRI64_DOUBLES];
+    // the record array's base in SGPRs before the count arrives (else its
+    // kernel-argument load sits between the index and the record loads)
+    const RT_G double* tri64 = sc.tri64;
+    asm volatile("" : "+s"(tri64));
     if (cnt != 0) {
-        const RT_G double2* T2 = reinterpret_cast<const RT_G double2*>(sc.tri64 + RT_TRI64_DOUBLES * (size_t)e0.x);
+        const RT_G double2* T2 = reinterpret_cast<const RT_G double2*>(tri64 + RT_TRI64_DOUBLES * (size_t)e0.x);
 #pragma unroll
         for (int k = 0; k < RT_TRI64_DOUBLES / 2; k++) {
             const double2 v = T2[k];

@@ -138,6 +138,10 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
 #ifndef RT_PATHS_K
 #define RT_PATHS_K 4
 #endif
+// W = 8 paths walk the quantised node copy (lane_walk QN)
+#ifndef RT_QNODES
+#define RT_QNODES 1
+#endif
 template <int W, int S>
 __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
                                                int bounces) {
@@ -181,8 +185,8 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                 for (int b = 0; b <= bounces; b++) {
                     LaneCounts lc;
 #if RT_PATHS_DEFER
-                    const Win win = trace_deferred<W, S, RT_PATHS_K, false>(sc, [&]() { return with_inv(ray); },
-                                                                            ray_pad(sc, ray), st, pcand, lc);
+                    const Win win = trace_deferred<W, S, RT_PATHS_K, false, W == 8 && RT_QNODES>(
+                        sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, pcand, lc);
 #else
                     const Win win =
                         trace_core<W, S, false>(sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, 0, lc);

@@ -278,10 +278,15 @@ __device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, 
 // lane_walk: the fp32 walk of ray q; on return cand[0..nc) hold the
 // survivors ({triangle, bits of t lower bound}), tcull the culling distance,
 // and `over` is set if a survivor had to be dropped.
-template <int W, int S, int K, bool COUNT>
+// QN (W = 8): node boxes from the quantised copy sc.qnodes (96 B per node
+// instead of 256 B: 6 vector loads per node step instead of 16; the planes
+// are 8-bit offsets from a per-node origin in steps of 2^e, each plane's t
+// one fma from per-node terms — DESIGN.md §11).
+template <int W, int S, int K, bool COUNT, bool QN = false>
 __device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, float tsl, LaneStack<S>& st,
                                           uint2 (*cand)[256], LaneCounts& lc, float& tcull_out, int& nc_out,
                                           bool& over_out) {
+    static_assert(!QN || W == 8, "quantised nodes are 8 wide");
     constexpr int G = W < 4 ? W : 4;  // children tested per load group
     const int tid = st.tid;
     const bool sx = q.ix < 0.f, sy = q.iy < 0.f, sz = q.iz < 0.f;
@@ -305,10 +310,47 @@ __device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, 
     while (cur != RT_INVALID_REF) {
         if (!(cur & RT_LEAF_BIT)) {
             if (COUNT) lc.nodes++;
-            const float4* nb = reinterpret_cast<const float4*>(sc.nodes + (size_t)cur * sc.node_bytes);
             float tn[W];
             uint32_t rb[W];
             uint32_t mask = 0;
+            if constexpr (QN) {
+                const uint4* qb = reinterpret_cast<const uint4*>(sc.qnodes + (size_t)cur * RT_QNODE_BYTES);
+                const uint4 h = qb[0], PX = qb[1], PY = qb[2], PZ = qb[3], R0 = qb[4], R1 = qb[5];
+                // t of plane q: q (2^e ix) + (origin ix - o_near/far ix), exactly
+                // the fp32 walk's plane with o +- pad (make_ray32)
+                const float ox = __uint_as_float(h.x), oy = __uint_as_float(h.y), oz = __uint_as_float(h.z);
+                const float ssx = __uint_as_float((h.w & 0xFFu) << 23) * q.ix;
+                const float ssy = __uint_as_float(((h.w >> 8) & 0xFFu) << 23) * q.iy;
+                const float ssz = __uint_as_float(((h.w >> 16) & 0xFFu) << 23) * q.iz;
+                const float anx = __builtin_fmaf(ox, q.ix, -q.onx), afx = __builtin_fmaf(ox, q.ix, -q.ofx);
+                const float any_ = __builtin_fmaf(oy, q.iy, -q.ony), afy = __builtin_fmaf(oy, q.iy, -q.ofy);
+                const float anz = __builtin_fmaf(oz, q.iz, -q.onz), afz = __builtin_fmaf(oz, q.iz, -q.ofz);
+                // near / far plane bytes: lo for a positive direction, hi for a negative one
+                const uint32_t nx0 = sx ? PX.z : PX.x, nx1 = sx ? PX.w : PX.y, fx0 = sx ? PX.x : PX.z,
+                               fx1 = sx ? PX.y : PX.w;
+                const uint32_t ny0 = sy ? PY.z : PY.x, ny1 = sy ? PY.w : PY.y, fy0 = sy ? PY.x : PY.z,
+                               fy1 = sy ? PY.y : PY.w;
+                const uint32_t nz0 = sz ? PZ.z : PZ.x, nz1 = sz ? PZ.w : PZ.y, fz0 = sz ? PZ.x : PZ.z,
+                               fz1 = sz ? PZ.y : PZ.w;
+                const uint32_t refs[8] = {R0.x, R0.y, R0.z, R0.w, R1.x, R1.y, R1.z, R1.w};
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const int sh = 8 * (c & 3);
+                    auto byte = [&](uint32_t w0, uint32_t w1) { return (float)(((c < 4 ? w0 : w1) >> sh) & 0xFFu); };
+                    const float a0 = __builtin_fmaf(byte(nx0, nx1), ssx, anx);
+                    const float a1 = __builtin_fmaf(byte(fx0, fx1), ssx, afx);
+                    const float b0 = __builtin_fmaf(byte(ny0, ny1), ssy, any_);
+                    const float b1 = __builtin_fmaf(byte(fy0, fy1), ssy, afy);
+                    const float c0 = __builtin_fmaf(byte(nz0, nz1), ssz, anz);
+                    const float c1 = __builtin_fmaf(byte(fz0, fz1), ssz, afz);
+                    const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
+                    const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
+                    tn[c] = t0;
+                    rb[c] = refs[c];
+                    if (t0 <= t1 && refs[c] != RT_INVALID_REF) mask |= 1u << c;
+                }
+            } else {
+            const float4* nb = reinterpret_cast<const float4*>(sc.nodes + (size_t)cur * sc.node_bytes);
 #pragma unroll
             for (int g = 0; g < W; g += G) {
                 float4 lo[G], hi[G];  // {lx,hx,ly,hy}, {lz,hz,ref,pad}
@@ -332,6 +374,7 @@ __device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, 
                     rb[g + c] = ref;
                     if (t0 <= t1 && ref != RT_INVALID_REF) mask |= 1u << (g + c);
                 }
+            }
             }
             if (mask) {
                 // push all hit children but the nearest, farthest first
@@ -437,7 +480,7 @@ __device__ __forceinline__ int resolve_cands(const RtDevScene& sc, const Ray64& 
     return 1;
 }
 
-template <int W, int S, int K, bool COUNT, class RayFn>
+template <int W, int S, int K, bool COUNT, bool QN = false, class RayFn>
 __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S>& st,
                                               uint2 (*cand)[256], LaneCounts& lc) {
     Ray32 q;
@@ -450,7 +493,7 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
     float tcull;
     int nc;
     bool over;
-    lane_walk<W, S, K, COUNT>(sc, q, tsl, st, cand, lc, tcull, nc, over);
+    lane_walk<W, S, K, COUNT, QN>(sc, q, tsl, st, cand, lc, tcull, nc, over);
     if (over) return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 0, lc);
     Win best;
     const int tid = st.tid;

@@ -200,4 +200,69 @@ std::vector<int32_t> collapse_children(const WalkTree& w, int32_t b, int W) {
     return kids;
 }
 
+// Quantised copy of W = 8 wide nodes for the per-lane walk (render.hip
+// lane_walk, QN): RT_QNODE_BYTES per node —
+//   dwords 0-2   origin x, y, z (fp32)
+//   dword 3      exponents e_x, e_y, e_z as bytes (biased by 127)
+//   dwords 4-15  8-bit planes, SoA: lo.x[8] hi.x[8] lo.y[8] hi.y[8] lo.z[8] hi.z[8]
+//   dwords 16-23 the 8 child refs (as in the 32-B records)
+// Plane q of axis a stands for origin[a] + q 2^e[a], exactly: the origin is
+// an fp32 multiple of 2^e (|origin / 2^e| < 2^24), lo planes are rounded down
+// and hi planes up in exact (double) arithmetic, so every quantised box
+// contains its fp32 record box — a superset, which the exact traversal
+// allows.  Empty slots get lo = 255, hi = 0 and the invalid ref.
+std::vector<uint8_t> quantize_wide8(const uint8_t* wide, uint64_t n_nodes) {
+    std::vector<uint8_t> out(n_nodes * RT_QNODE_BYTES, 0);
+    for (uint64_t n = 0; n < n_nodes; n++) {
+        const float* rec = reinterpret_cast<const float*>(wide + n * 256);
+        uint32_t* q = reinterpret_cast<uint32_t*>(out.data() + n * RT_QNODE_BYTES);
+        uint8_t* planes = reinterpret_cast<uint8_t*>(q + 4);
+        bool valid[8];
+        double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+        bool any = false;
+        for (int c = 0; c < 8; c++) {
+            const uint32_t ref = reinterpret_cast<const uint32_t*>(rec + 8 * c)[RT_CHILD_REF];
+            q[16 + c] = ref;
+            valid[c] = ref != RT_INVALID_REF;
+            if (!valid[c]) continue;
+            for (int a = 0; a < 3; a++) {
+                const double l = rec[8 * c + 2 * a], h = rec[8 * c + 2 * a + 1];
+                lo[a] = any ? std::min(lo[a], l) : l;
+                hi[a] = any ? std::max(hi[a], h) : h;
+            }
+            any = true;
+        }
+        uint32_t exps = 0;
+        for (int a = 0; a < 3; a++) {
+            const double ext = hi[a] - lo[a];
+            int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -100;
+            e = std::max(e, -100);
+            double org = 0, sc = 0;
+            for (;; e++) {
+                sc = std::ldexp(1.0, e);
+                org = std::floor(lo[a] / sc) * sc;
+                if (std::fabs(org) / sc < 16777216.0 && (hi[a] - org) / sc <= 255.0) break;
+            }
+            if (e > 127) throw Error{RT_ERR_INVALID_ARGUMENT, "scene extent too large to quantise"};
+            reinterpret_cast<float*>(q)[a] = (float)org;  // exact: an fp32 multiple of 2^e
+            exps |= (uint32_t)(e + 127) << (8 * a);
+            for (int c = 0; c < 8; c++) {
+                uint8_t ql = 255, qh = 0;
+                if (valid[c]) {
+                    const double l = rec[8 * c + 2 * a], h = rec[8 * c + 2 * a + 1];
+                    const double fl = std::floor((l - org) / sc), ch = std::ceil((h - org) / sc);
+                    if (fl < 0 || ch > 255 || org + fl * sc > l || org + ch * sc < h)
+                        throw Error{RT_ERR_RUNTIME, "node quantisation out of range"};
+                    ql = (uint8_t)fl;
+                    qh = (uint8_t)ch;
+                }
+                planes[16 * a + c] = ql;      // lo[a] array
+                planes[16 * a + 8 + c] = qh;  // hi[a] array
+            }
+        }
+        q[3] = exps;
+    }
+    return out;
+}
+
 }  // namespace rt

@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(RtDevScene sc, RtFrameParams fp
         float tcull;
         int nc;
         bool over;
-        lane_walk<W, S, K, false>(sc, q, tsl, st, cand, lc, tcull, nc, over);
+        lane_walk<W, S, K, false, W == 8 && RT_QNODES>(sc, q, tsl, st, cand, lc, tcull, nc, over);
         uint32_t m = 0;
         if (!over) {
             for (int c = 0; c < nc; c++) {

@@ -1,9 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for rep in 1 2 3; do
-for v in base rw7; do
-if [ $v = base ]; then L=""; else L=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so; fi
-RT_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 10 > gpurun_out/$v$rep.log 2>&1 || exit 1
-done; done
-grep -o '"value": [0-9.]*' gpurun_out/base*.log gpurun_out/rw7*.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "paths" -p no:cacheprovider --timeout 300 > gpurun_out/tpaths.log 2>&1; rc=$?; tail -3 gpurun_out/tpaths.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/pq.log 2>&1 && tail -1 gpurun_out/pq.log | cut -c1-200 &&
+RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_noq.so timeout -k 10 300 python bench.py --paths --no-cpu --steps 2 --warmup 1 > gpurun_out/pn.log 2>&1 && tail -1 gpurun_out/pn.log | cut -c1-200

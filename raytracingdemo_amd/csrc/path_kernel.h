@@ -123,7 +123,7 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
 // spp paths of its pixel (segments in order), so the pixel's sum is formed in
 // sample order.  frame: the hash's frame number.
 #ifndef RT_PATHS_WPE
-#define RT_PATHS_WPE 4  // 128 VGPRs (a few spills): +13% over the compiler's 161 (3 waves/SIMD)
+#define RT_PATHS_WPE 5  // with the 8-entry LDS ring (RT_PATHS_STACK): 3.54 vs 3.37 G at 4 waves (128 VGPRs)
 #endif
 #if RT_PATHS_WPE > 0
 #define RT_PATHS_ATTR __attribute__((amdgpu_waves_per_eu(RT_PATHS_WPE)))

@@ -724,7 +724,7 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
 
 constexpr int kLdsStack = 16;      // per-lane kernel: LDS ring entries per lane (8 B each)
 #ifndef RT_PATHS_STACK
-#define RT_PATHS_STACK 16
+#define RT_PATHS_STACK 8  // 24 KB LDS per block with the candidates: 5 waves/SIMD fit
 #endif
 constexpr int kPathStack = RT_PATHS_STACK;  // path kernel: LDS ring entries per lane
 constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (4 B each)

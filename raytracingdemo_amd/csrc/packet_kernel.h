@@ -139,6 +139,15 @@
 #error "RT_PUSH_FLAT pushes refs only"
 #endif
 
+// W = 8 walk on the fp16-step node copy (sc.hnodes, 144 B per node instead
+// of 256 B: 3 scalar loads and 36 SGPRs per node step instead of 8 and 64;
+// each plane's t is one v_fma_mix_f32 of its fp16 step count).  Measured
+// slower (1.535 vs 1.398 ms per launch, parity green): 9 more VALU per node
+// step and looser boxes cost more than the scalar loads save — off.
+#ifndef RT_HNODES
+#define RT_HNODES 0
+#endif
+
 // Node record fetch: 0 scalar loads (default), 1 uniform vector loads.
 #ifndef RT_NODE_FETCH
 #define RT_NODE_FETCH 0
@@ -350,6 +359,59 @@ __device__ __forceinline__ T kword(const __attribute__((address_space(3))) T* p)
     return __builtin_bit_cast(T, uni(*(const __attribute__((address_space(3))) uint32_t*)p));
 }
 
+typedef const __attribute__((address_space(4))) uint32_t* cuint_p;
+
+// v_fma_mix_f32: fp16 half `hi` of uniform word w (an integer step count,
+// exact) times b plus c, fused in fp32 with one rounding.
+__device__ __forceinline__ float fma_h(uint32_t w, float b, float c, bool hi) {
+    float d;
+    if (hi)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "s"(w), "v"(b), "v"(c));
+    else
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "s"(w), "v"(b), "v"(c));
+    return d;
+}
+
+// child_hits on an fp16-step node (walk_tree.cpp quantize_wide8_f16): plane
+// q of axis a lies at origin + q 2^e exactly, so its t is
+// q (2^e i) + (origin i - o_lo/hi i) — the same slab value as the fp32
+// record's fma, from a box that contains the record's box.
+template <int OCT>
+__device__ __forceinline__ void child_hits_h(const uint32_t (&hw)[36], const Ray32& q, const f2 nox, const f2 noy,
+                                             const f2 noz, float tcull, uint64_t (&hm)[8]) {
+    const float sx = __uint_as_float((hw[3] & 0xFFu) << 23) * q.ix;
+    const float sy = __uint_as_float(((hw[3] >> 8) & 0xFFu) << 23) * q.iy;
+    const float sz = __uint_as_float(((hw[3] >> 16) & 0xFFu) << 23) * q.iz;
+    const float ox = __uint_as_float(hw[0]), oy = __uint_as_float(hw[1]), oz = __uint_as_float(hw[2]);
+    const float alx = __builtin_fmaf(ox, q.ix, nox.x), ahx = __builtin_fmaf(ox, q.ix, nox.y);
+    const float aly = __builtin_fmaf(oy, q.iy, noy.x), ahy = __builtin_fmaf(oy, q.iy, noy.y);
+    const float alz = __builtin_fmaf(oz, q.iz, noz.x), ahz = __builtin_fmaf(oz, q.iz, noz.y);
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        const bool h = c & 1;
+        const int k = c >> 1;
+        const float tlx = fma_h(hw[4 + k], sx, alx, h), thx = fma_h(hw[8 + k], sx, ahx, h);
+        const float tly = fma_h(hw[12 + k], sy, aly, h), thy = fma_h(hw[16 + k], sy, ahy, h);
+        const float tlz = fma_h(hw[20 + k], sz, alz, h), thz = fma_h(hw[24 + k], sz, ahz, h);
+        float t0, t1;
+        if constexpr (OCT < 0) {
+            t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
+            t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull));
+        } else {
+            const float nx = (OCT & 1) ? thx : tlx, fx = (OCT & 1) ? tlx : thx;
+            const float ny = (OCT & 2) ? thy : tly, fy = (OCT & 2) ? tly : thy;
+            const float nz = (OCT & 4) ? thz : tlz, fz = (OCT & 4) ? tlz : thz;
+            // min/max in asm: the compiler would canonicalise each asm result first
+            float m0, m1;
+            asm("v_max_f32 %0, 0, %1" : "=v"(m0) : "v"(nz));
+            asm("v_max3_f32 %0, %1, %2, %3" : "=v"(t0) : "v"(nx), "v"(ny), "v"(m0));
+            asm("v_min_f32 %0, %1, %2" : "=v"(m1) : "v"(fz), "v"(tcull));
+            asm("v_min3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(fx), "v"(fy), "v"(m1));
+        }
+        hm[c] = __ballot(t0 <= t1);
+    }
+}
+
 // Slab test of one node's W children for every lane's ray (fp32, outward
 // planes).  OCT >= 0: all rays share the direction signs OCT (bit a set =
 // negative along axis a), so each axis's near plane is the hi plane for a
@@ -489,6 +551,8 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
     // the tile's octant if every ray that takes part shares lane 0's signs, else 8
     const int oct = __ballot(valid && lsg != dsg) == 0 ? (int)dsg : 8;
     const RT_G uint8_t* const nodes = kload(&A->sc.nodes);
+    constexpr bool kHN = W == 8 && RT_HNODES && RT_OCT_HOIST && !RT_POP_CULL && RT_NODE_FETCH == 0 && !RT_GROUP_TEST;
+    const RT_G uint8_t* const hnodes = kHN ? kload(&A->sc.hnodes) : nullptr;
     const RT_G float* const tri32 = kload(&A->sc.tri32);
     // slab offsets for the lo / hi planes (pad moves lo down and hi up)
     const float olx = (q.ox + pd) * q.ix, ohx = (q.ox - pd) * q.ix;
@@ -602,6 +666,17 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                 RT_TSTAMP(t_n1);
 #else
 #if RT_NODE_FETCH == 0
+                uint32_t hw[36];  // kHN: the fp16-step node, in SGPRs
+                if constexpr (kHN) {
+                    const cuint_p hb = (cuint_p)(hnodes + (size_t)cur * RT_HNODE_BYTES);
+#pragma unroll
+                    for (int k = 0; k < 36; k++) hw[k] = hb[k];
+                    refv = 0;
+                    [&]<int... L>(std::integer_sequence<int, L...>) {
+                        ((refv = writelane<L>(refv, hw[28 + L])), ...);
+                    }(std::make_integer_sequence<int, 8>{});
+                    meta = hw[3] >> 24;
+                } else
                 {
                     // scalar path: all W records are loaded before any branch
                     // so their loads are in flight together
@@ -664,7 +739,8 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                 // tile): the near/far plane of each axis is known, no per-axis
                 // min/max; otherwise the general test
 #if RT_OCT_HOIST
-                child_hits<W, OCT>(bx, q, nox, noy, noz, tcull, hm);
+                if constexpr (kHN) child_hits_h<OCT>(hw, q, nox, noy, noz, tcull, *reinterpret_cast<uint64_t(*)[8]>(hm));
+                else child_hits<W, OCT>(bx, q, nox, noy, noz, tcull, hm);
 #elif RT_OCT_TREE
                 // binary dispatch on the octant bits (3 uniform branches)
                 if (oct > 7) {

@@ -157,6 +157,9 @@ void upload_one(rt_scene* s, int device) {
     struct Sec { const void* src; size_t bytes; size_t off; };
     // W = 8: the per-lane walk's quantised node copy (walk_tree.cpp)
     const std::vector<uint8_t> qn = f.width == 8 ? rt::quantize_wide8(f.wide.data(), f.n_wide) : std::vector<uint8_t>{};
+    // W = 8: the packet walk's fp16-step node copy
+    const std::vector<uint8_t> hn =
+        f.width == 8 ? rt::quantize_wide8_f16(f.wide.data(), f.n_wide) : std::vector<uint8_t>{};
     std::vector<Sec> secs = {
         {f.wide.data(), f.wide.size(), 0},
         {f.tri32.data(), f.tri32.size() * sizeof(float), 0},
@@ -172,6 +175,7 @@ void upload_one(rt_scene* s, int device) {
         {f.rrange.data(), f.rrange.size() * sizeof(uint32_t), 0},
         {f.ref2walk.data(), f.ref2walk.size() * sizeof(uint32_t), 0},
         {qn.data(), qn.size(), 0},
+        {hn.data(), hn.size(), 0},
     };
     size_t off = 0;
     for (auto& sc : secs) {
@@ -200,6 +204,7 @@ void upload_one(rt_scene* s, int device) {
     d.rrange = reinterpret_cast<const uint32_t*>(at(11));
     d.ref2walk = reinterpret_cast<const uint32_t*>(at(12));
     d.qnodes = qn.empty() ? nullptr : at(13);
+    d.hnodes = hn.empty() ? nullptr : at(14);
     d.root_ref = f.root_ref;
     std::memcpy(d.root_box, f.root_box, sizeof d.root_box);
     d.n_tris = (uint32_t)s->soup.n;

@@ -61,6 +61,8 @@
 // Quantised W = 8 node for the per-lane walk (walk_tree.cpp quantize_wide8):
 // origin, exponents, SoA 8-bit planes, refs.
 #define RT_QNODE_BYTES 96
+// Half-precision-step W = 8 node for the packet walk (quantize_wide8_f16).
+#define RT_HNODE_BYTES 144
 // tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
 #define RT_TRI32_PAD 4
 
@@ -96,6 +98,7 @@ struct RtDevScene {
     const RT_G uint32_t* rrange;  // real node primitive range [begin, end) (reference order)
     const RT_G uint32_t* ref2walk;// reference-order position -> BVH-order triangle index
     const RT_G uint8_t* qnodes;   // W = 8: quantised copy of `nodes` (RT_QNODE_BYTES each), else null
+    const RT_G uint8_t* hnodes;   // W = 8: fp16-step copy of `nodes` (RT_HNODE_BYTES each), else null
     uint32_t root_ref;
     float root_box[6];
     uint32_t n_tris;

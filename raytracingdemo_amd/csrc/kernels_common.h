@@ -179,6 +179,46 @@ __device__ __forceinline__ int tri_classify(const float4 A, const float4 B, cons
     return 2;
 }
 
+// tri_classify without early exits (selects only): the same classes and
+// bounds for every input — the exits of tri_classify become exec-mask
+// branches in a wave, this form is one straight block.
+__device__ __forceinline__ int tri_classify_nb(const float4 A, const float4 B, const float4 C, float ox, float oy,
+                                               float oz, float dx, float dy, float dz, float co, float tcull,
+                                               float& tl, float& tu) {
+    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = C.x;
+    const float M1 = C.y, M2 = C.z, Cv = C.w;
+    const float sx = ox - A.x, sy = oy - A.y, sz = oz - A.z;
+    const float hx = __builtin_fmaf(dy, e2z, -dz * e2y);
+    const float hy = __builtin_fmaf(dz, e2x, -dx * e2z);
+    const float hz = __builtin_fmaf(dx, e2y, -dy * e2x);
+    const float a = __builtin_fmaf(e1x, hx, __builtin_fmaf(e1y, hy, e1z * hz));
+    const float U = __builtin_fmaf(sx, hx, __builtin_fmaf(sy, hy, sz * hz));
+    const float qx = __builtin_fmaf(sy, e1z, -sz * e1y);
+    const float qy = __builtin_fmaf(sz, e1x, -sx * e1z);
+    const float qz = __builtin_fmaf(sx, e1y, -sy * e1x);
+    const float V = __builtin_fmaf(dx, qx, __builtin_fmaf(dy, qy, dz * qz));
+    const float T = __builtin_fmaf(e2x, qx, __builtin_fmaf(e2y, qy, e2z * qz));
+    const float Ms = fmaxf(fmaxf(__builtin_fabsf(sx), __builtin_fabsf(sy)), __builtin_fabsf(sz));
+    const float u = 0x1p-24f;
+    const float G = __builtin_fmaf(256.f, Ms, 64.f * (co + Cv));
+    const float errA = 256.f * u * M1 * M2;
+    const float errU = u * M2 * G, errV = u * M1 * G, errT = u * M1 * M2 * G;
+    const float aa = __builtin_fabsf(a);
+    const bool amb = !(aa > errA);  // sign of the determinant uncertain: let fp64 decide
+    const float sg = a > 0.f ? 1.f : -1.f;
+    const float Us = sg * U, Vs = sg * V, Ts = sg * T;
+    const bool rej = Us < -errU || Vs < -errV || Ts < -errT || Us + Vs > aa + errU + errV + errA ||
+                     Ts - errT > tcull * (aa + errA);
+    const float EPS = 1e-8f;
+    const bool certain = Us >= errU && Vs >= errV && Us + Vs <= aa - errU - errV - errA && aa - errA >= 2.f * EPS &&
+                         Ts - errT >= 2.f * EPS * (aa + errA);
+    const float tl_ = fmaxf((Ts - errT) * __builtin_amdgcn_rcpf(aa + errA), 0.f) * (1.f - 0x1p-20f);
+    const float tu_ = (Ts + errT) * __builtin_amdgcn_rcpf(aa - errA) * (1.f + 0x1p-20f);
+    tl = amb ? 0.f : tl_;
+    tu = (!amb && certain) ? tu_ : __builtin_huge_valf();
+    return amb ? 1 : rej ? 0 : certain ? 2 : 1;
+}
+
 // Camera pixel caches (camera.hpp:35-37), evaluated per pixel in the same
 // operation order as the host's pixel_caches (no contraction): bit-identical.
 // ox / oy: the sample's offset inside the pixel; the reference's pixel centre

@@ -148,6 +148,14 @@
 #define RT_HNODES 0
 #endif
 
+// Leaf triangle filter without early exits (tri_classify_nb): 1 on, 0 off.
+// Measured slower: 76 VGPRs (6 waves/SIMD) 1.483 ms, held to 72 (7 waves,
+// spills) 1.444 ms, against 1.411-1.421 ms with the exits — the exits skip
+// the rest of the test for triangles no lane of the tile can hit.
+#ifndef RT_TRI_NB
+#define RT_TRI_NB 0
+#endif
+
 // Node record fetch: 0 scalar loads (default), 1 uniform vector loads.
 #ifndef RT_NODE_FETCH
 #define RT_NODE_FETCH 0
@@ -861,9 +869,15 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                         if (k >= end) break;
                         if (COUNT) n_pre += valid;
                         float tl, tu;
+#if RT_TRI_NB
+                        int cls = tri_classify_nb(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co,
+                                                  tcull, tl, tu);
+                        cls = valid ? cls : 0;
+#else
                         const int cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz,
                                                              q.co, tcull, tl, tu)
                                               : 0;
+#endif
                         if (__ballot(cls != 0) == 0) continue;
                         if (cls != 0) {
                             // dist of a certain hit <= (tu + slack)(1 + 2^-20)

@@ -280,16 +280,11 @@ def main():
         # de-interleaved there (image row j = r * world + rank) into frames[b]
         if world == 1:
             return
-        if rehearse:  # gloo over host copies: synchronous
-            dist.gather(coll(cnt[b]), list(gather_cnt[b].unbind(0)) if root else None, dst=0)
-            full = gather_frames(coll(rgb[b]), H, world, rank, out=gather_rgb[b] if root else None)
-            if root:
-                frames[b].copy_(full)
-            return
         post.wait_stream(stream)
         with torch.cuda.stream(post):
-            w1 = dist.gather(cnt[b], list(gather_cnt[b].unbind(0)) if root else None, dst=0, async_op=True)
-            w2 = dist.gather(rgb[b], list(gather_rgb[b].unbind(0)) if root else None, dst=0, async_op=True)
+            # (rehearsal: the same calls on host copies over gloo)
+            w1 = dist.gather(coll(cnt[b]), list(gather_cnt[b].unbind(0)) if root else None, dst=0, async_op=True)
+            w2 = dist.gather(coll(rgb[b]), list(gather_rgb[b].unbind(0)) if root else None, dst=0, async_op=True)
             w1.wait()
             w2.wait()
             if root:

@@ -1,10 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 -k "sponza or overflow or batch or reference" > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-for rep in 1 2; do
-for v in nbw7 tb; do
-if [ $v = base ]; then L=""; else L=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so; fi
-RT_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 10 > gpurun_out/$v$rep.log 2>&1 || exit 1
-done; done
-grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/base*.log gpurun_out/tb*.log
+RT_BENCH_REHEARSE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu > gpurun_out/r2.log 2>&1 && tail -1 gpurun_out/r2.log | grep -o '"gather_verified": [a-z]*\|"n_gpus": [0-9]*' &&
+RT_BENCH_REHEARSE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 7 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 7 --steps 3 --warmup 1 --frames 12 --no-cpu > gpurun_out/r7.log 2>&1 && tail -1 gpurun_out/r7.log | grep -o '"gather_verified": [a-z]*\|"n_gpus": [0-9]*'

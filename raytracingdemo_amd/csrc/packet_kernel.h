@@ -148,6 +148,14 @@
 #define RT_HNODES 0
 #endif
 
+// Scalar-cache prefetch of the stack top's node at each leaf (the pop that
+// follows a leaf then hits the scalar cache): 1 on, 0 off.  Measured slower
+// (1.437-1.445 vs 1.416-1.418 ms per launch): the stack-top LDS read it
+// needs sits in front of the leaf's own loads.
+#ifndef RT_POP_PREFETCH
+#define RT_POP_PREFETCH 0
+#endif
+
 // Leaf triangle filter without early exits (tri_classify_nb): 1 on, 0 off.
 // Measured slower: 76 VGPRs (6 waves/SIMD) 1.483 ms, held to 72 (7 waves,
 // spills) 1.444 ms, against 1.411-1.421 ms with the exits — the exits skip
@@ -848,6 +856,17 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                     w_leaves++;
                     w_tris += cnt;
                 }
+#if RT_POP_PREFETCH
+                // a leaf is followed by a pop: touch the stack top's node (one
+                // word per 64-B line) so its records are in the scalar cache
+                // when the pop loads them; the words are consumed after the
+                // leaf, whose own waits cover them
+                // (straight-line: an invalid target reads the root node instead)
+                const uint32_t nxt = uni(wstack[sp > 0 ? sp - 1 : 0]);
+                const uint32_t pnode = (sp > 0 && !(nxt & RT_LEAF_BIT)) ? nxt : 0u;
+                const cuint_p pfp = (cuint_p)(nodes + (size_t)pnode * (32 * W));
+                const uint32_t pf0 = pfp[0], pf1 = pfp[16], pf2 = pfp[32], pf3 = pfp[48];
+#endif
                 // triangles come in chunks of kLeafChunk records: all their
                 // scalar loads are issued, then waited on once (tri32 carries
                 // kLeafChunk padding records, so reading past a leaf is safe)
@@ -905,6 +924,9 @@ __device__ __forceinline__ void trace_packet(args_p A, int f, int i, int r, bool
                 }
 #if RT_GROUP_TEST
                 tg = group_max<W>(tcull);
+#endif
+#if RT_POP_PREFETCH
+                asm volatile("" ::"s"(pf0), "s"(pf1), "s"(pf2), "s"(pf3));
 #endif
                 RT_TACC(2, t_l0);
             }

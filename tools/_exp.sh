@@ -1,10 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cacheprovider --timeout 300 > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc -eq 0 ] || exit $rc
-for rep in 1 2 3; do
-for b in 12 18; do
-RT_BATCH=$b timeout -k 10 300 python bench.py --no-cpu --steps 10 > gpurun_out/b$b_$rep.log 2>&1 || exit 1
-cp gpurun_out/b$b_$rep.log gpurun_out/bt${b}_$rep.log
-done; done
-grep -o '"value": [0-9.]*' gpurun_out/bt*.log
+timeout -k 10 300 python bench.py --paths --steps 2 --warmup 1 > gpurun_out/paths_bench.log 2>&1 && tail -1 gpurun_out/paths_bench.log | cut -c1-150 &&
+timeout -k 10 300 python bench.py --spp 4 --no-cpu > gpurun_out/spp4_bench.log 2>&1 && tail -1 gpurun_out/spp4_bench.log | cut -c1-150

@@ -29,9 +29,9 @@ for s in $STEPS; do
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
                    -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
         pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
-                   -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu --key-out gpurun_out/pmc_key.txt && \
+                   -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu --key-out gpurun_out/pmc_key.txt && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
-                   -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu && \
+                   -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu && \
                python tools/pmc_traffic.py gpurun_out/pmc/fetch_counter_collection.csv \
                    gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
         list)  run list 120 rocprofv3 -L ;;
@@ -52,7 +52,7 @@ for s in $STEPS; do
                            "SQC_DCACHE_MISSES_DUPLICATE SQC_DCACHE_REQ_READ_16 SQC_DCACHE_REQ_READ_8 SQC_DCACHE_REQ_READ_4 TCC_TAG_STALL_sum TCC_LATENCY_FIFO_FULL_sum"; do
                    pn=$((${pn:-0}+1))
                    run sq$pn 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$pn \
-                       -- python bench.py --steps 1 --warmup 0 --frames 12 --no-cpu --key-out gpurun_out/pmc_key.txt || exit 1
+                       -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu --key-out gpurun_out/pmc_key.txt || exit 1
                done
                python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt
                python tools/pmc_valu.py gpurun_out/pmc_key.txt gpurun_out/pmc_valu.json gpurun_out/sq/sq*_counter_collection.csv ;;

@@ -1,5 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py --paths --steps 2 --warmup 1 > gpurun_out/paths_bench.log 2>&1 && tail -1 gpurun_out/paths_bench.log | cut -c1-150 &&
-timeout -k 10 300 python bench.py --spp 4 --no-cpu > gpurun_out/spp4_bench.log 2>&1 && tail -1 gpurun_out/spp4_bench.log | cut -c1-150
+for rep in 1 2; do
+for v in base w8k6; do
+if [ $v = base ]; then L=""; else L=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so; fi
+RT_LIB=$L timeout -k 10 300 python bench.py --no-cpu --steps 10 > gpurun_out/$v$rep.log 2>&1 || exit 1
+done; done
+grep -o '"value": [0-9.]*\|"kernel_ms_avg": [0-9.]*' gpurun_out/base*.log gpurun_out/w8k6*.log

@@ -353,8 +353,8 @@ RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row
 int batch_frames() {
     static const int b = [] {
         const char* e = std::getenv("RT_BATCH");
-        const int v = e ? std::atoi(e) : 18;
-        return v >= 1 && v <= RT_MAX_BATCH ? v : 18;
+        const int v = e ? std::atoi(e) : RT_MAX_BATCH;
+        return v >= 1 && v <= RT_MAX_BATCH ? v : RT_MAX_BATCH;
     }();
     return b;
 }

@@ -49,7 +49,9 @@
 // RT_MAX_BATCH frames (camera poses) of the same geometry, so the persistent
 // traversal kernel's ramp-up and tail, and the launch gaps, are paid once per
 // batch instead of once per frame.
+#ifndef RT_MAX_BATCH
 #define RT_MAX_BATCH 18
+#endif
 #define RT_QUEUE_WORDS (RT_HIT_BASE + RT_MAX_BATCH * RT_HIT_SLOTS * RT_QUEUE_STRIDE)
 // Candidate lists handed from the traversal to the resolve kernel, per pixel:
 // RT_CAND_LDS entries kept in LDS during the walk plus overflow slots written

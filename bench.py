@@ -34,9 +34,36 @@ METRIC = "Mrays/sec (primary, 1spp) on Sponza 1920×1080; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 TRI32_BYTES = 48       # fp32 pre-filter record (v0, e1, e2 + 3 bounds)
 TRI64_BYTES = 128      # fp64 record (v0, e1, e2, normal, id, leaf, leaf box) per exact test
+MT64_BYTES = 72        # its Moller-Trumbore part (v0, e1, e2) per exact test (fused resolve)
+WIN_BYTES = 56         # the winner's normal, {id, leaf} and leaf box, once per hit pixel
 CHAIN_BYTES = 52       # fp64 box (48 B) + parent (4 B) per re-verified ancestor
-OUT_BYTES = 7          # u32 hit-id + 3 B rgb written per ray
+OUT_BYTES = 15         # u32 hit-id + f64 distance + 3 B rgb written per ray
 CAND_BYTES = 8         # one candidate entry {triangle, t bound} handed to the resolve kernel
+
+
+def host_cores():
+    """CPUs this process may use: the cgroup CPU quota (cpu.max) and the
+    affinity mask, next to what the machine reports (nproc honours
+    OMP_NUM_THREADS; std::thread::hardware_concurrency = os.cpu_count())."""
+    info = {"hardware_concurrency": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        import subprocess
+        info["nproc"] = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except (OSError, ValueError):
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+            info["cgroup_cpu_max"] = f"{q} {per}"
+    except (OSError, ValueError):
+        pass
+    usable = info["affinity"]
+    if quota:
+        usable = min(usable, max(1, int(quota)))
+    info["usable"] = usable
+    return info
 
 
 def parse():
@@ -50,6 +77,9 @@ def parse():
     p.add_argument("--paths", action="store_true",
                    help="config c5: diffuse path tracing (secondary rays), 16 spp x (1 + 4 bounces) by default")
     p.add_argument("--bounces", type=int, default=4, help="paths: secondary bounces per sample")
+    p.add_argument("--scene", default="sponza", choices=["sponza", "armadillo"],
+                   help="sponza: configs c4/c5 (the headline; proxy unless RT_SPONZA_OBJ); "
+                        "armadillo: config c3 (needs RT_ARMADILLO_OBJ, the geometry is stripped from the reference)")
     p.add_argument("--algo", default="bsah")
     p.add_argument("--k", type=int, default=8)
     p.add_argument("--mode", default="exact", choices=["exact", "fp64"])
@@ -70,11 +100,15 @@ def parse():
 
 def cpu_baseline(tris, algo, k, cams, W, H, target_s):
     """Reference traversal (oracle/_ref: the reference's own headers compiled -O3,
-    OpenMP over pixel columns) or, without it, the oracle restatement.  Bounded
-    sample: whole frames of the same camera orbit until ~target_s of CPU time."""
+    OpenMP over pixel columns; the timed scope of runTest, src/main.cpp:253-255)
+    or, without it, the oracle restatement, in two legs: every host core this
+    process may use (the cgroup quota on the GPU box) and one core.  Bounded
+    samples: whole frames of the same camera orbit until ~target_s of CPU time
+    (all cores), ~target_s / 3 (one core: whole rows, a frame is ~3 s there)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
-    threads = int(os.environ.get("RT_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    host = host_cores()
+    threads = int(os.environ.get("RT_CPU_THREADS", host["usable"]))
     if pyoracle.Reference.available():
         lib, kind = pyoracle.Reference(), "reference"
     else:
@@ -88,9 +122,39 @@ def cpu_baseline(tris, algo, k, cams, W, H, target_s):
         spent += time.perf_counter() - t0
         frames += 1
         rays += W * H
+    # one core: bands of 60 rows spread over the orbit's frames
+    rows1, spent1, f1 = 0, 0.0, 0
+    while spent1 < target_s / 3 and f1 < len(cams) * (H // 60):
+        pos, d = cams[f1 % len(cams)]
+        row0 = (f1 * 7 * 60) % (H - 60 + 1)
+        t0 = time.perf_counter()
+        b.render(pos, d, W, H, row0=row0, nrows=60, threads=1)
+        spent1 += time.perf_counter() - t0
+        rows1 += 60
+        f1 += 1
+    one = rows1 * W / spent1 / 1e6
     return {"value": round(rays / spent / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": kind,
             "sample": f"{frames} full {W}x{H} frames of the same camera orbit ({rays} rays, {spent:.1f} s), "
-                      f"same scene and {algo}-{k} tree, reference traversal semantics (no culling)"}
+                      f"same scene and {algo}-{k} tree, reference traversal semantics (no culling)",
+            "all_cores": {"value": round(rays / spent / 1e6, 4), "cores": threads},
+            "one_core": {"value": round(one, 4), "cores": 1,
+                         "sample": f"{f1} bands of 60 rows x {W} px over the orbit ({rows1 * W} rays, {spent1:.1f} s)"},
+            "host": host,
+            "published_O0": "none for Sponza: the reference's only Sponza datum is an old-code run "
+                            "(testruns_2025_12_25/testrun_47, ~99 s per 500x500 frame at -O0, 1 core); "
+                            "BASELINE.md lists the published -O0 figures for the other models"}
+
+
+def scene_difficulty(label, algo, k):
+    """The reference's own per-ray work on this scene (oracle traversal
+    counters over sampled frames; tools/scene_difficulty.py writes the
+    committed summary), next to SURVEY.md §8(a) a1's bunny and teapot probes."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "scene_difficulty.json")))
+    except (OSError, ValueError):
+        return None
+    key = f"{label}|{algo}-{k}"
+    return d.get(key)
 
 
 def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
@@ -202,7 +266,7 @@ def main():
     import torch.distributed as dist
 
     import raytracingdemo_amd as rt
-    from raytracingdemo_amd.scenes import sponza_scene
+    from raytracingdemo_amd.scenes import armadillo_scene, sponza_scene
     from raytracingdemo_amd.shards import deinterleave_into, gather_frames, rows_per_rank, shard_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,8 +289,21 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
     coll = (lambda t: t.cpu()) if rehearse else (lambda t: t)  # collective-side tensors
 
-    tris, label = sponza_scene()
-    scene = rt.Scene(tris, a.algo, a.k).upload([local])
+    if a.scene == "armadillo":
+        sc = armadillo_scene()
+        if sc is None:
+            raise SystemExit("config c3 needs RT_ARMADILLO_OBJ=<armadillo.obj> (stripped from the reference)")
+        tris, label = sc
+    else:
+        tris, label = sponza_scene()
+    t_build = time.perf_counter()
+    scene = rt.Scene(tris, a.algo, a.k)
+    t_upload = time.perf_counter()
+    scene.upload([local])
+    torch.cuda.synchronize(dev)
+    t_ready = time.perf_counter()
+    build_ms = {"scene_create_ms": round((t_upload - t_build) * 1e3, 1),
+                "upload_ms": round((t_ready - t_upload) * 1e3, 1)}
     if a.paths:
         return run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse)
     st = scene.stats()
@@ -243,6 +320,8 @@ def main():
     # k + 1; the render of step k + 2 waits for the gather of step k).
     NB = 2 if world > 1 else 1
     ids = [torch.empty((F, rows, W, S), dtype=torch.int32, device=dev) for _ in range(NB)]
+    # per-sample hit distance |hit - o| (stack_bvh.hpp:631), written in the timed region
+    dists = torch.empty((F, my_rows, W, S), dtype=torch.float64, device=dev)
     rgb = [torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
     cnt = [torch.zeros((F,), dtype=torch.int64, device=dev) for _ in range(NB)]
     # the library writes frame f at f * W * my_rows: a short shard renders
@@ -268,8 +347,8 @@ def main():
             stream.wait_event(shipped[b])  # set b's previous gather has read it
         cnt[b].zero_()
         scene.render_batch_device(local, cams, W, H, rank, world, my_rows, hit_id=r_ids[b].data_ptr(),
-                                  rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(), stream=stream.cuda_stream,
-                                  mode=mode, timing=timing, count=count, spp=S)
+                                  dist=dists.data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
+                                  stream=stream.cuda_stream, mode=mode, timing=timing, count=count, spp=S)
         if padded:
             ids[b][:, :my_rows] = r_ids[b]
             rgb[b][:, :my_rows] = r_rgb[b]
@@ -319,10 +398,18 @@ def main():
     # SURVEY.md 8(d)'s per-ray figure: what each ray's own traversal touches
     survey_bytes_per_ray = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
                             cs["rays"] * OUT_BYTES) / max(cs["rays"], 1)
-    if cs["wave_tiles"]:
-        # packet traversal kernel (the dominant kernel): a node or triangle
-        # record is fetched once per wave for its 64 rays; plus the candidate
-        # lists it writes (rays are generated in-kernel: no camera reads)
+    fused = cs["wave_tiles"] and S == 1 and os.environ.get("RT_RESOLVE", "")[:1] != "s"
+    if fused:
+        # packet traversal kernel with the fused resolve (the dominant kernel):
+        # a node or triangle record is fetched once per wave for its 64 rays;
+        # per ray the Moller-Trumbore part of each exact test, the winner's
+        # shading fields, the ancestor boxes re-verified and the outputs
+        # (rays are generated in-kernel: no camera reads)
+        trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES + cs["tri_tests"] * MT64_BYTES +
+                       cs["hits"] * WIN_BYTES + cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * OUT_BYTES)
+    elif cs["wave_tiles"]:
+        # packet traversal kernel, split resolve: the walk plus the candidate
+        # lists it writes
         trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES +
                        cs["rays"] * 1 + cs["tri_tests"] * CAND_BYTES)
     else:  # per-lane kernel: each ray fetches its own records
@@ -359,11 +446,8 @@ def main():
             verified = bool(torch.equal(g_ids.to(dev), f_ids) and torch.equal(frames[bl], f_rgb) and
                             torch.equal(gather_cnt[bl].to(dev).sum(0), f_cnt))
         dist.barrier()
-    # per-kernel HIP-event times of the timed launches (library stream), and
-    # in diagnostic builds the per-wave clock split
+    # per-kernel HIP-event times of the timed launches (library stream)
     ks = scene.frame_stats(local, reset=True)
-    diag = ks["diag_cycles"]
-    tiles_timed = a.steps * F * S * ((W + 7) // 8) * ((my_rows + 7) // 8)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         t = coll(t)
@@ -384,7 +468,8 @@ def main():
     achieved = alg_bytes_per_launch / avg_kernel_s / 1e9
 
     if rank == 0:
-        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}|fpl{frames_per_launch:g}" + (f"|spp{S}" if S > 1 else "")
+        key = (f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}|fpl{frames_per_launch:g}" + (f"|spp{S}" if S > 1 else "")
+               + ("|fused" if fused else ""))
         if a.key_out:
             with open(a.key_out, "w") as fh:
                 fh.write(key + "\n")
@@ -407,6 +492,9 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
         cpu = None
+        dropin = None
+        if world == 1:
+            dropin = dropin_rate(scene, cams, W, H, mode)
         if world == 1 and not a.no_cpu:
             cpu = cpu_baseline(tris, a.algo, a.k, cams, W, H, a.cpu_seconds)
         line = {
@@ -424,7 +512,8 @@ def main():
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "valu": valu,
-                         "kernel": "k_trace_packet" if cs["wave_tiles"] else "k_trace_exact",
+                         "kernel": ("k_trace_packet (walk + fused exact resolve)" if fused else
+                                    "k_trace_packet (walk)" if cs["wave_tiles"] else "k_trace_exact"),
                          "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": int(alg_bytes_per_launch),
                          "frames_per_launch": round(frames_per_launch, 3),
@@ -442,21 +531,38 @@ def main():
                                      "wave_tris_per_tile": round(cs["wave_tris"] / max(cs["wave_tiles"], 1), 2),
                                      "redo_rays": round(cs["redo_rays"] / max(cs["rays"], 1), 7),
                                      "redo_chain": round(cs["redo_chain"] / max(cs["rays"], 1), 7),
-                                     **({"diag_ticks_per_tile": [round(x / tiles_timed) for x in diag[:8]],
-                                         "diag_wave_life_mean_us": round(diag[8] / max(diag[10], 1) / 100, 2),
-                                         "diag_wave_life_max_us": round(diag[9] / 100, 2),
-                                         "diag_busy_fraction": round(diag[8] / max(diag[10], 1) / 100 /
-                                                                     (avg_kernel_s * 1e6), 3),
-                                         "diag_waves_per_launch": round(diag[10] / launches_timed, 1),
-                                         "diag_max_tiles_per_wave": int(diag[11])}
-                                        if any(diag) else {}),
+                                     "spilled_rays": round(cs["spilled_rays"] / max(cs["rays"], 1), 7),
+                                     "dropped_rays": round(cs["dropped_rays"] / max(cs["rays"], 1), 7),
                                      "node_bytes": st["node_bytes"], "tri32_bytes": TRI32_BYTES,
                                      "tri64_bytes": TRI64_BYTES}},
             "cpu_baseline": cpu,
+            "dropin_frame_path": dropin,
+            "scene_build": build_ms,
+            "scene_difficulty": scene_difficulty(label, a.algo, a.k),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dropin_rate(scene, cams, W, H, mode):
+    """The drop-in path INTEGRATION.md §2 binds (rt_render_frame: one pose per
+    call into host buffers, blocking, as runTest's calculateScreen call,
+    src/main.cpp:253-255): hit ids, distances and PPM bytes for every pose of
+    the orbit, D2H copies included.  Reported beside the headline, never as it."""
+    for p, d in cams[:2]:
+        scene.calculate_screen(p, d, W, H, mode=mode, want=("hit_id", "dist", "rgb"))
+    t0 = time.perf_counter()
+    dev_s = 0.0
+    for p, d in cams:
+        g = scene.calculate_screen(p, d, W, H, mode=mode, want=("hit_id", "dist", "rgb"))
+        dev_s += g["seconds"]
+    wall = time.perf_counter() - t0
+    n = len(cams) * W * H
+    return {"value": round(n / wall / 1e6, 2), "unit": "Mrays/s", "entry_point": "rt_render_frame",
+            "frames": len(cams), "ms_per_frame": round(wall / len(cams) * 1e3, 3),
+            "device_ms_per_frame": round(dev_s / len(cams) * 1e3, 3),
+            "note": "one pose per call, host buffers (hit_id + dist + rgb D2H), blocking"}
 
 
 if __name__ == "__main__":

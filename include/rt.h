@@ -119,11 +119,13 @@ typedef struct {
     uint64_t wave_tris;     /* packet kernel: triangle records fetched per wave */
     uint64_t redo_rays;     /* rays finished by the fix-up kernel (exact per-lane path) */
     uint64_t redo_chain;    /*   of which: winner invisible to the reference (chain check) */
-    uint64_t diag_cycles[12]; /* diagnostic builds only (else 0): wave clock ticks in
-                                node-load wait, node work, leaves, stack pops, ray
-                                set-up, candidate output, -, tile fetch; then
-                                traversal-wave lifetime sum and max (10-ns ticks),
-                                wave count, max tiles per wave */
+    uint64_t spilled_rays;  /* packet kernel: rays whose candidate list overflowed
+                               LDS into a pool chunk in HBM                */
+    uint64_t dropped_rays;  /*   of which: the chunk filled too, a candidate was
+                               dropped (certified bound, else fix-up)      */
+    uint64_t empty_node_steps; /* packet kernel: node steps where no lane entered
+                                  any child                                */
+    uint64_t reserved[9];
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */
@@ -219,9 +221,8 @@ int rt_frame_stats(rt_scene *s, int device, int reset, rt_frame_stats_t *out);
 
 int rt_scene_stats(const rt_scene *s, rt_scene_stats_t *out);
 
-/* Diagnostics: copy up to n words of the device's raw counter block (the
- * rt_frame_stats counters followed by the diagnostic-build accumulators;
- * tools/diag_hist.py).  Synchronises the device. */
+/* Diagnostics: copy up to n (<= 16) words of the device's raw counter block
+ * (the rt_frame_stats counters).  Waits for the scene's launches on it. */
 int rt_diag_raw(rt_scene *s, int device, uint64_t *out, size_t n);
 
 /* Reference visit order rank of every triangle (loader index -> rank) and

@@ -73,7 +73,8 @@ class rt_frame_stats_t(C.Structure):
                 ("chain_checks", C.c_uint64), ("hits", C.c_uint64), ("chain_nodes", C.c_uint64),
                 ("tri_prefilter", C.c_uint64), ("wave_nodes", C.c_uint64), ("wave_leaves", C.c_uint64),
                 ("wave_tiles", C.c_uint64), ("wave_tris", C.c_uint64), ("redo_rays", C.c_uint64), ("redo_chain", C.c_uint64),
-                ("diag_cycles", C.c_uint64 * 12), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
+                ("spilled_rays", C.c_uint64), ("dropped_rays", C.c_uint64), ("empty_node_steps", C.c_uint64),
+                ("reserved", C.c_uint64 * 9), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
 
 
 _lib = None

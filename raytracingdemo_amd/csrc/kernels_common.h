@@ -108,9 +108,6 @@ __device__ __forceinline__ bool tri_prefilter(const float4 A, const float4 B, co
     return true;
 }
 
-#ifndef RT_TRI_UGATE
-#define RT_TRI_UGATE 0
-#endif
 // Classifying variant of tri_prefilter for the deferred fp64 resolve.
 //   0  the exact fp64 test must reject (or t > tcull)
 //   1  borderline: only the fp64 test can decide
@@ -145,78 +142,19 @@ __device__ __forceinline__ int tri_classify(const float4 A, const float4 B, cons
     tu = __builtin_huge_valf();
     if (!(aa > errA)) return 1;  // sign of the determinant uncertain: let fp64 decide
     const float sg = a > 0.f ? 1.f : -1.f;
-#if RT_TRI_UGATE
-    // first gate on u alone (u < 0 or u > 1, triangle.hpp:50): a tile's rays
-    // mostly miss a leaf triangle together, and u needs neither q, V nor T
-    {
-        const float Us = sg * U;
-        if (Us < -errU || Us > aa + errU + errA) return 0;
-    }
-#endif
     const float Us = sg * U, Vs = sg * V, Ts = sg * T;
     if (Us < -errU || Vs < -errV || Ts < -errT) return 0;
     if (Us + Vs > aa + errU + errV + errA) return 0;
     if (Ts - errT > tcull * (aa + errA)) return 0;  // t > tcull: cannot improve
     // bounds through v_rcp_f32 (<= 1 ulp) and one rounded multiply: the
     // 2^-20 factors cover both roundings with room to spare
-#ifndef RT_RCP_BOUNDS
-#define RT_RCP_BOUNDS 1
-#endif
-#if RT_RCP_BOUNDS
     tl = fmaxf((Ts - errT) * __builtin_amdgcn_rcpf(aa + errA), 0.f) * (1.f - 0x1p-20f);
-#else
-    tl = fmaxf((Ts - errT) / (aa + errA), 0.f) * (1.f - 0x1p-20f);
-#endif
     const float EPS = 1e-8f;
     const bool certain = Us >= errU && Vs >= errV && Us + Vs <= aa - errU - errV - errA && aa - errA >= 2.f * EPS &&
                          Ts - errT >= 2.f * EPS * (aa + errA);
     if (!certain) return 1;
-#if RT_RCP_BOUNDS
     tu = (Ts + errT) * __builtin_amdgcn_rcpf(aa - errA) * (1.f + 0x1p-20f);
-#else
-    tu = (Ts + errT) / (aa - errA) * (1.f + 0x1p-20f);
-#endif
     return 2;
-}
-
-// tri_classify without early exits (selects only): the same classes and
-// bounds for every input — the exits of tri_classify become exec-mask
-// branches in a wave, this form is one straight block.
-__device__ __forceinline__ int tri_classify_nb(const float4 A, const float4 B, const float4 C, float ox, float oy,
-                                               float oz, float dx, float dy, float dz, float co, float tcull,
-                                               float& tl, float& tu) {
-    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = C.x;
-    const float M1 = C.y, M2 = C.z, Cv = C.w;
-    const float sx = ox - A.x, sy = oy - A.y, sz = oz - A.z;
-    const float hx = __builtin_fmaf(dy, e2z, -dz * e2y);
-    const float hy = __builtin_fmaf(dz, e2x, -dx * e2z);
-    const float hz = __builtin_fmaf(dx, e2y, -dy * e2x);
-    const float a = __builtin_fmaf(e1x, hx, __builtin_fmaf(e1y, hy, e1z * hz));
-    const float U = __builtin_fmaf(sx, hx, __builtin_fmaf(sy, hy, sz * hz));
-    const float qx = __builtin_fmaf(sy, e1z, -sz * e1y);
-    const float qy = __builtin_fmaf(sz, e1x, -sx * e1z);
-    const float qz = __builtin_fmaf(sx, e1y, -sy * e1x);
-    const float V = __builtin_fmaf(dx, qx, __builtin_fmaf(dy, qy, dz * qz));
-    const float T = __builtin_fmaf(e2x, qx, __builtin_fmaf(e2y, qy, e2z * qz));
-    const float Ms = fmaxf(fmaxf(__builtin_fabsf(sx), __builtin_fabsf(sy)), __builtin_fabsf(sz));
-    const float u = 0x1p-24f;
-    const float G = __builtin_fmaf(256.f, Ms, 64.f * (co + Cv));
-    const float errA = 256.f * u * M1 * M2;
-    const float errU = u * M2 * G, errV = u * M1 * G, errT = u * M1 * M2 * G;
-    const float aa = __builtin_fabsf(a);
-    const bool amb = !(aa > errA);  // sign of the determinant uncertain: let fp64 decide
-    const float sg = a > 0.f ? 1.f : -1.f;
-    const float Us = sg * U, Vs = sg * V, Ts = sg * T;
-    const bool rej = Us < -errU || Vs < -errV || Ts < -errT || Us + Vs > aa + errU + errV + errA ||
-                     Ts - errT > tcull * (aa + errA);
-    const float EPS = 1e-8f;
-    const bool certain = Us >= errU && Vs >= errV && Us + Vs <= aa - errU - errV - errA && aa - errA >= 2.f * EPS &&
-                         Ts - errT >= 2.f * EPS * (aa + errA);
-    const float tl_ = fmaxf((Ts - errT) * __builtin_amdgcn_rcpf(aa + errA), 0.f) * (1.f - 0x1p-20f);
-    const float tu_ = (Ts + errT) * __builtin_amdgcn_rcpf(aa - errA) * (1.f + 0x1p-20f);
-    tl = amb ? 0.f : tl_;
-    tu = (!amb && certain) ? tu_ : __builtin_huge_valf();
-    return amb ? 1 : rej ? 0 : certain ? 2 : 1;
 }
 
 // Camera pixel caches (camera.hpp:35-37), evaluated per pixel in the same
@@ -338,13 +276,11 @@ __device__ __forceinline__ void shade_color(const RtFrameCam& cam, const Best& b
 __device__ __forceinline__ void store_sample(const RtFrameParams& fp, size_t so, const Best& b, const Shade& sh) {
     if (fp.hit_id) fp.hit_id[so] = b.tri >= 0 ? sh.id : RT_INVALID_REF;
     if (fp.dist) fp.dist[so] = b.tri >= 0 ? b.dist : -1.0;
-#if !defined(RT_DIAG_TILECOST) && !defined(RT_DIAG_WAVES)
     if (fp.hit_pos) {
         fp.hit_pos[3 * so] = b.tri >= 0 ? b.px : 0.0;
         fp.hit_pos[3 * so + 1] = b.tri >= 0 ? b.py : 0.0;
         fp.hit_pos[3 * so + 2] = b.tri >= 0 ? b.pz : 0.0;
     }
-#endif
 }
 // Pixel colour as PPM bytes (benchmark.hpp:105-114 truncating cast) from the
 // sum of its samples' colours (summed in sample order from 0.0): the mean

@@ -572,28 +572,47 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
 #include "path_kernel.h"
 #include "wavefront_paths.h"
 
-// Finishes the pixels the packet kernel handed over (redo list, count in
-// tile_ctr[RT_REDO_COUNT]) with the per-lane exact kernel: from pass 0 after a candidate
-// list overflow, straight into the inline-verifying pass 1 when the winner's
-// ancestor chain failed.  Grid-stride; every thread reaches the exit test.
+// Finishes the pixels the packet pipeline handed over (redo list, count in
+// tile_ctr[RT_REDO_COUNT]) with the per-lane exact kernel: from pass 0 after a
+// candidate overflow, straight into the inline-verifying pass 1 when the
+// winner's ancestor chain failed.  Grid-stride; every thread reaches the exit
+// test.  It also leaves the launch's work-queue block zeroed for the next
+// launch: block 0 folds the per-frame hit-count partials into the caller's
+// counters and clears them, the tile queues and the pool counter (nothing
+// else reads them now); the last block to have read the redo count clears it.
 template <int W, int S, bool COUNT>
 __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux) {
     __shared__ uint2 lds[S][256];
     __shared__ unsigned long long frame_sum[RT_MAX_BATCH];
+    __shared__ uint32_t n_sh;
     const int tid = threadIdx.x;
-    if (blockIdx.x == 0 && fp.hit_count && aux.cand) {
-        // fold k_resolve's per-frame hit-count partials into the caller's counters
+    if (tid == 0) {
+        n_sh = *(volatile uint32_t*)(aux.tile_ctr + RT_REDO_COUNT);
+        __threadfence();
+        if (atomicAdd(aux.tile_ctr + RT_FIXUP_DONE, 1u) == gridDim.x - 1) {
+            aux.tile_ctr[RT_REDO_COUNT] = 0;
+            aux.tile_ctr[RT_FIXUP_DONE] = 0;
+        }
+    }
+    if (blockIdx.x == 0) {
         if (tid < RT_MAX_BATCH) frame_sum[tid] = 0;
         __syncthreads();
         const int poses = fp.nframes / fp.spp;
         for (int k = tid; k < poses * RT_HIT_SLOTS; k += 256) {
-            const uint32_t v = aux.tile_ctr[RT_HIT_BASE + k * RT_QUEUE_STRIDE];
-            if (v) atomicAdd(&frame_sum[k / RT_HIT_SLOTS], (unsigned long long)v);
+            RT_G uint32_t* const slot = aux.tile_ctr + RT_HIT_BASE + k * RT_QUEUE_STRIDE;
+            const uint32_t v = *slot;
+            if (v) {
+                atomicAdd(&frame_sum[k / RT_HIT_SLOTS], (unsigned long long)v);
+                *slot = 0;
+            }
         }
+        if (tid < RT_QUEUES) aux.tile_ctr[tid * RT_QUEUE_STRIDE] = 0;
+        if (tid == 0) aux.tile_ctr[RT_POOL_COUNT] = 0;
         __syncthreads();
-        if (tid < poses && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
+        if (fp.hit_count && tid < poses && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
     }
-    const uint32_t n = *(volatile uint32_t*)(aux.tile_ctr + RT_REDO_COUNT);
+    __syncthreads();
+    const uint32_t n = n_sh;
     if (n == 0) return;
     LaneStack<S> st;
     st.lds = lds;
@@ -729,6 +748,7 @@ constexpr int kLdsStack = 16;      // per-lane kernel: LDS ring entries per lane
 constexpr int kPathStack = RT_PATHS_STACK;  // path kernel: LDS ring entries per lane
 constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (4 B each)
 constexpr int kCandidates = RT_CAND_LDS;  // packet kernel: LDS candidate list entries per lane (8 B each)
+static_assert(RT_PW_K <= RT_CAND_LDS, "wavefront walk lists share the candidate buffers");
 constexpr int kFixupGrid = 256;    // k_fixup blocks (the redo list is short)
 
 // Kernel choice: the packet kernel unless its stack cannot hold the tree's
@@ -757,6 +777,16 @@ RtFrameParams single_pose(const RtFrameParams& fp, int p) {
     return o;
 }
 
+// Resolve placement of the packet pipeline for spp = 1: fused into the walk
+// kernel's tile epilogue (default) or, with RT_RESOLVE=split, the separate
+// k_resolve pass over candidate lists in HBM (the spp > 1 path; kept for
+// A/B measurement).  Read per call (tests switch it in-process).
+bool split_resolve(int spp) {
+    if (spp > 1) return true;
+    const char* e = getenv("RT_RESOLVE");
+    return e && e[0] == 's';
+}
+
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
                         hipStream_t s, const hipEvent_t* ev) {
@@ -766,25 +796,30 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     if (ev) (void)hipEventRecord(ev[0], s);
     if (use_packet(sc.stack_bound)) {
         const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
-        // k_resolve: frame f owns blocks [f * bpf, (f + 1) * bpf)
-        // k_resolve: one block per 16x16 tile, 8 XCD bands of T8 tiles per pose
-        const uint64_t rt8 = (((uint64_t)(fp.W + 15) / 16) * ((uint64_t)(fp.nrows + 15) / 16) + 7) / 8;
-        const dim3 rgrid((unsigned)(8 * rt8 * (uint64_t)(fp.nframes / fp.spp)));
-        if (count) {
-            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true>), grid, blk, 0, s,
-                               PacketArgs{sc, fp, aux});
+        if (!split_resolve(fp.spp)) {
+            if (count)
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, true>), grid, blk, 0, s,
+                                   PacketArgs{sc, fp, aux});
+            else
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true>), grid, blk, 0, s,
+                                   PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
-            if (fp.spp == 1) hipLaunchKernelGGL((k_resolve<true, false>), rgrid, blk, 0, s, sc, fp, aux);
-            else hipLaunchKernelGGL((k_resolve<true, true>), rgrid, blk, 0, s, sc, fp, aux);
-            hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, blk, 0, s, sc, fp, aux);
         } else {
-            hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false>), grid, blk, 0, s,
-                               PacketArgs{sc, fp, aux});
+            // k_resolve: one block per 16x16 tile, 8 XCD bands of T8 tiles per pose
+            const uint64_t rt8 = (((uint64_t)(fp.W + 15) / 16) * ((uint64_t)(fp.nrows + 15) / 16) + 7) / 8;
+            const dim3 rgrid((unsigned)(8 * rt8 * (uint64_t)(fp.nframes / fp.spp)));
+            if (count)
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, false>), grid, blk, 0, s,
+                                   PacketArgs{sc, fp, aux});
+            else
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, false>), grid, blk, 0, s,
+                                   PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
-            if (fp.spp == 1) hipLaunchKernelGGL((k_resolve<false, false>), rgrid, blk, 0, s, sc, fp, aux);
-            else hipLaunchKernelGGL((k_resolve<false, true>), rgrid, blk, 0, s, sc, fp, aux);
-            hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, blk, 0, s, sc, fp, aux);
+            if (count) hipLaunchKernelGGL((k_resolve<true>), rgrid, blk, 0, s, sc, fp, aux);
+            else hipLaunchKernelGGL((k_resolve<false>), rgrid, blk, 0, s, sc, fp, aux);
         }
+        if (count) hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, blk, 0, s, sc, fp, aux);
+        else hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, blk, 0, s, sc, fp, aux);
     } else {
         // per-lane kernel (trees deeper than the packet stack): one launch
         // per frame of the batch, each on a zeroed work queue
@@ -806,8 +841,8 @@ template <int W>
 int blocks_per_cu_w(uint32_t stack_bound) {
     int n = 0;
     hipError_t e = use_packet(stack_bound)
-                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_packet<W, kPacketStack, kCandidates, false>,
-                                                                   256, 0)
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                 &n, k_trace_packet<W, kPacketStack, kCandidates, false, true>, 256, 0)
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<W, kLdsStack, false, 3>, 256, 0);
     return e == hipSuccess ? n : 1;
 }
@@ -838,7 +873,9 @@ int exact_lds_stack() {
     const int a = kLdsStack < kPathStack ? kLdsStack : kPathStack;
     return a < RT_PW_STACK ? a : RT_PW_STACK;
 }
-int packet_candidates() { return RT_CAND_SLOTS; }  // HBM slots per pixel (LDS list + overflow)
+int packet_candidates() { return RT_CAND_LDS; }  // HBM list entries per pixel (spp > 1, wavefront paths)
+bool packet_split(int spp) { return split_resolve(spp); }
+uint32_t params_bytes() { return (uint32_t)sizeof(RtFrameParams); }
 
 // Host entry: validates the launch geometry against what the kernels assume
 // and dispatches on node width.  mode 0 = exact fast, 1 = literal.
@@ -871,10 +908,13 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     }
     if (aux.spill_cap + kLdsStack < sc.stack_bound || !aux.tile_ctr || !aux.spill || aux.grid <= 0)
         return hipErrorInvalidValue;
-    // the redo list must hold every pixel of the shard
+    // the redo list must hold every pixel of the shard; the split resolve
+    // needs candidate lists for every pixel of the batch
     const uint64_t bpix = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.nframes;  // pixels of the batch
-    if (use_packet(sc.stack_bound) &&
-        (!aux.redo || aux.redo_cap < bpix || !aux.cand || !aux.cand_cnt || !aux.cand_drop || aux.cand_cap < bpix))
+    if (use_packet(sc.stack_bound) && (!aux.redo || aux.redo_cap < bpix / (uint64_t)fp.spp || !aux.pool))
+        return hipErrorInvalidValue;
+    if (use_packet(sc.stack_bound) && split_resolve(fp.spp) &&
+        (!aux.cand || !aux.cand_cnt || !aux.cand_drop || !aux.cand_ovf || aux.cand_cap < bpix))
         return hipErrorInvalidValue;
     const bool packet = use_packet(sc.stack_bound);
     if (!fresh || !packet) {
@@ -921,7 +961,7 @@ hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const 
                            uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev) {
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
     if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.spill || aux.grid <= 0 || !aux.cand ||
-        aux.cand_cap < ws.P || ws.P != (uint32_t)fp.W * (uint32_t)fp.nrows || RT_PW_K > RT_CAND_SLOTS ||
+        aux.cand_cap < ws.P || ws.P != (uint32_t)fp.W * (uint32_t)fp.nrows || RT_PW_K > RT_CAND_LDS ||
         aux.spill_cap + RT_PW_STACK < sc.stack_bound || aux.spill_cap + kLdsStack < sc.stack_bound)
         return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((ws.P + 255u) / 256u);

@@ -25,6 +25,8 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
                            uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
+bool packet_split(int spp);
+uint32_t params_bytes();
 int exact_lds_stack();
 }
 
@@ -61,16 +63,19 @@ size_t align_up(size_t x) {
     return (x + 255) & ~size_t(255);
 }
 
-// d_counters: [0..15] RT_FLAG_COUNT counters, [16..) diagnostic block
-// (packet_kernel.h RT_DIAG_*: 16 words, then 64 spread slots of 8 words)
-constexpr size_t kCounterWords = 16 + 16 + 64 * 8;
+// d_counters: RT_FLAG_COUNT counters (rt_frame_stats)
+constexpr size_t kCounterWords = 16;
+// Candidate overflow pool: chunks of RT_POOL_CHUNK entries, one per lane whose
+// LDS list overflows in a launch (a dry pool falls back to the certified
+// dropped bound, so the size trades memory against fix-up work only).
+constexpr uint32_t kPoolChunks = 1u << 17;  // 24 MiB
 
 struct Replica {
     int device = -1;
     void* blob = nullptr;       // one allocation for the whole scene
     size_t blob_bytes = 0;
     RtDevScene dev{};
-    unsigned long long* d_counters = nullptr;  // [0..15] RT_FLAG_COUNT counters, [16..23] diagnostics
+    unsigned long long* d_counters = nullptr;  // RT_FLAG_COUNT counters
     // staging for the host-output frame call
     void* frame = nullptr;
     size_t frame_bytes = 0;
@@ -82,9 +87,10 @@ struct Replica {
     uint64_t* d_spill = nullptr;
     uint32_t spill_cap = 0;
     int grid = 0;
-    uint32_t* d_redo = nullptr;  // packet kernel -> fix-up kernel pixel list
+    uint32_t* d_redo = nullptr;  // packet pipeline -> fix-up kernel pixel list
     uint64_t redo_cap = 0;
-    void* d_cand = nullptr;      // packet kernel -> resolve kernel candidate lists
+    uint64_t* d_pool = nullptr;  // candidate overflow pool (kPoolChunks x RT_POOL_CHUNK entries)
+    void* d_cand = nullptr;      // spp > 1 / wavefront paths: candidate lists in HBM
     uint64_t cand_cap = 0;       // pixels
     void* d_pw = nullptr;        // wavefront path tracer workspace (PathWs), pw_cap paths
     uint64_t pw_cap = 0;
@@ -107,7 +113,7 @@ struct rt_scene {
     rt::Soup soup;
     rt::Tree tree;
     rt::Flat flat;
-    std::vector<Replica> reps;
+    std::vector<std::unique_ptr<Replica>> reps;  // stable addresses: a replica outlives the lock
     std::mutex mu;
     uint32_t literal_stack = 0;  // stack bound of the literal (reference-order) traversal
 };
@@ -125,6 +131,7 @@ void free_replica(Replica& r) {
     if (r.d_tiles) hipFree(r.d_tiles);
     if (r.d_spill) hipFree(r.d_spill);
     if (r.d_redo) hipFree(r.d_redo);
+    if (r.d_pool) hipFree(r.d_pool);
     if (r.d_cand) hipFree(r.d_cand);
     if (r.d_pw) hipFree(r.d_pw);
     for (auto& a : r.tev)
@@ -140,7 +147,7 @@ void free_replica(Replica& r) {
 
 Replica& replica_for(rt_scene* s, int device) {
     for (auto& r : s->reps)
-        if (r.device == device) return r;
+        if (r->device == device) return *r;
     throw rt::Error{RT_ERR_NO_DEVICE, "scene not uploaded to device " + std::to_string(device)};
 }
 
@@ -150,16 +157,16 @@ void upload_one(rt_scene* s, int device) {
     HIP_TRY(hipGetDeviceProperties(&prop, device));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         throw rt::Error{RT_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950"};
+    if (rt::params_bytes() != sizeof(RtFrameParams))  // host and device built with one RT_MAX_BATCH
+        throw rt::Error{RT_ERR_RUNTIME, "library built inconsistently (RtFrameParams layout differs)"};
     const rt::Flat& f = s->flat;
-    Replica r;
+    auto rp = std::make_unique<Replica>();
+    Replica& r = *rp;
     r.device = device;
     // carve one allocation (256-B aligned sections)
     struct Sec { const void* src; size_t bytes; size_t off; };
     // W = 8: the per-lane walk's quantised node copy (walk_tree.cpp)
     const std::vector<uint8_t> qn = f.width == 8 ? rt::quantize_wide8(f.wide.data(), f.n_wide) : std::vector<uint8_t>{};
-    // W = 8: the packet walk's fp16-step node copy
-    const std::vector<uint8_t> hn =
-        f.width == 8 ? rt::quantize_wide8_f16(f.wide.data(), f.n_wide) : std::vector<uint8_t>{};
     std::vector<Sec> secs = {
         {f.wide.data(), f.wide.size(), 0},
         {f.tri32.data(), f.tri32.size() * sizeof(float), 0},
@@ -175,7 +182,6 @@ void upload_one(rt_scene* s, int device) {
         {f.rrange.data(), f.rrange.size() * sizeof(uint32_t), 0},
         {f.ref2walk.data(), f.ref2walk.size() * sizeof(uint32_t), 0},
         {qn.data(), qn.size(), 0},
-        {hn.data(), hn.size(), 0},
     };
     size_t off = 0;
     for (auto& sc : secs) {
@@ -204,7 +210,6 @@ void upload_one(rt_scene* s, int device) {
     d.rrange = reinterpret_cast<const uint32_t*>(at(11));
     d.ref2walk = reinterpret_cast<const uint32_t*>(at(12));
     d.qnodes = qn.empty() ? nullptr : at(13);
-    d.hnodes = hn.empty() ? nullptr : at(14);
     d.root_ref = f.root_ref;
     std::memcpy(d.root_box, f.root_box, sizeof d.root_box);
     d.n_tris = (uint32_t)s->soup.n;
@@ -230,24 +235,22 @@ void upload_one(rt_scene* s, int device) {
     HIP_TRY(hipMalloc(&r.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
     HIP_TRY(hipMemset(r.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&r.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
-    s->reps.push_back(r);
+    HIP_TRY(hipMalloc(&r.d_pool, (size_t)kPoolChunks * RT_POOL_CHUNK * sizeof(uint64_t)));
+    s->reps.push_back(std::move(rp));
 }
 
-// Redo list and candidate buffers large enough for every pixel of a launch
-// (grown, never shrunk).
+// Waits for every launch issued on the replica so far (before its buffers
+// are replaced): only the replica's last stream, not the whole device.
+void quiesce(Replica& r) {
+    if (!r.used) return;
+    HIP_TRY(hipEventRecord(r.ev_out, r.last));
+    HIP_TRY(hipEventSynchronize(r.ev_out));
+}
+
+// Redo list for `pixels` pose pixels of a launch (grown, never shrunk).
 void ensure_redo(Replica& r, uint64_t pixels) {
-    if (r.cand_cap < pixels) {
-        HIP_TRY(hipDeviceSynchronize());  // earlier launches may still use it
-        if (r.d_cand) HIP_TRY(hipFree(r.d_cand));
-        r.d_cand = nullptr;
-        r.cand_cap = 0;
-        const uint64_t k = (uint64_t)rt::packet_candidates();
-        // [K][pixels] entries | [pixels] f32 drop bounds | [pixels] counts
-        HIP_TRY(hipMalloc(&r.d_cand, pixels * (8 * k + 4 + 1)));
-        r.cand_cap = pixels;
-    }
     if (r.redo_cap >= pixels) return;
-    HIP_TRY(hipDeviceSynchronize());  // earlier launches may still use it
+    quiesce(r);
     if (r.d_redo) HIP_TRY(hipFree(r.d_redo));
     r.d_redo = nullptr;
     r.redo_cap = 0;
@@ -255,11 +258,25 @@ void ensure_redo(Replica& r, uint64_t pixels) {
     r.redo_cap = pixels;
 }
 
+// Candidate lists in HBM for `pixels` sample pixels (spp > 1 resolve, the
+// wavefront path tracer; grown, never shrunk):
+// [K][pixels] entries | [pixels] f32 drop bounds | [pixels] u32 chunks | [pixels] counts
+constexpr uint64_t kCandBytesPerPixel = 8 * RT_CAND_LDS + 4 + 4 + 1;
+void ensure_cand(Replica& r, uint64_t pixels) {
+    if (r.cand_cap >= pixels) return;
+    quiesce(r);
+    if (r.d_cand) HIP_TRY(hipFree(r.d_cand));
+    r.d_cand = nullptr;
+    r.cand_cap = 0;
+    HIP_TRY(hipMalloc(&r.d_cand, pixels * kCandBytesPerPixel));
+    r.cand_cap = pixels;
+}
+
 // Wavefront path-tracer workspace for P paths (grown, never shrunk): two
 // segment queues (64 B per entry), L and acc (24 B per path), control words.
 PathWs ensure_pw(Replica& r, uint64_t P) {
     if (r.pw_cap < P) {
-        HIP_TRY(hipDeviceSynchronize());  // earlier launches may still use it
+        quiesce(r);  // earlier launches may still use it
         if (r.d_pw) HIP_TRY(hipFree(r.d_pw));
         r.d_pw = nullptr;
         r.pw_cap = 0;
@@ -381,13 +398,15 @@ RtLaunchAux aux_of(Replica& r) {
     a.grid = r.grid;
     a.redo = r.d_redo;
     a.redo_cap = r.redo_cap;
-    a.diag = r.d_counters + 16;
+    a.pool = r.d_pool;
+    a.pool_chunks = kPoolChunks;
     a.cand = static_cast<uint64_t*>(r.d_cand);
     if (r.d_cand) {
         uint8_t* base = static_cast<uint8_t*>(r.d_cand);
         const uint64_t k = (uint64_t)rt::packet_candidates();
         a.cand_drop = reinterpret_cast<float*>(base + r.cand_cap * 8 * k);
-        a.cand_cnt = base + r.cand_cap * (8 * k + 4);
+        a.cand_ovf = reinterpret_cast<uint32_t*>(base + r.cand_cap * (8 * k + 4));
+        a.cand_cnt = base + r.cand_cap * (8 * k + 8);
     }
     a.cand_cap = r.cand_cap;
     return a;
@@ -516,7 +535,7 @@ int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {
         for (int q = 0; q < n_devices; q++) {
             if (devices[q] < 0 || devices[q] >= count) return fail(RT_ERR_NO_DEVICE, "bad device ordinal");
             bool have = false;
-            for (auto& r : s->reps) have |= r.device == devices[q];
+            for (auto& r : s->reps) have |= r->device == devices[q];
             if (!have) upload_one(s, devices[q]);
         }
         return RT_OK;
@@ -543,11 +562,10 @@ int rt_render_batch_spp_device(rt_scene* s, int device, const rt_camera* cams, i
         const rt_camera* cam = &cams[0];
         if (row0 < 0 || row_stride < 1 || nrows < 0 || (nrows > 0 && row0 + (int64_t)(nrows - 1) * row_stride >= cam->height))
             return fail(RT_ERR_INVALID_ARGUMENT, "row shard outside the image");
-        Replica* r;
-        {
-            std::lock_guard<std::mutex> lk(s->mu);
-            r = &replica_for(s, device);
-        }
+        // one caller at a time per scene: launches on a replica share its
+        // work-queue block, redo list and pool
+        std::lock_guard<std::mutex> lk(s->mu);
+        Replica* r = &replica_for(s, device);
         DevGuard g(device);
         hipStream_t st = (hipStream_t)stream;
         const uint64_t fpix = (uint64_t)cam->width * (uint64_t)nrows;  // pixels per frame
@@ -556,9 +574,19 @@ int rt_render_batch_spp_device(rt_scene* s, int device, const rt_camera* cams, i
         int per = std::max(1, batch_frames() / spp);
         while (per > 1 && fpix * (uint64_t)(per * spp) >= (1ull << 31)) per--;
         if (fpix * (uint64_t)spp >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "image too large for spp");
+        const bool split = mode == RT_MODE_EXACT && rt::packet_split(spp);
+        if (split) {
+            // candidate lists in HBM (73 B per sample pixel): at most half of
+            // the device memory that is free (or already ours), fewer poses
+            // per launch otherwise
+            size_t mfree = 0, mtotal = 0;
+            HIP_TRY(hipMemGetInfo(&mfree, &mtotal));
+            const uint64_t avail = (uint64_t)mfree + r->cand_cap * kCandBytesPerPixel;
+            while (per > 1 && fpix * (uint64_t)(per * spp) * kCandBytesPerPixel > avail / 2) per--;
+            ensure_cand(*r, fpix * (uint64_t)(std::min(per, nframes) * spp));
+        }
+        ensure_redo(*r, fpix * (uint64_t)std::min(per, nframes));
         // serialise on the replica's stream: the caller's stream waits for it
-        std::lock_guard<std::mutex> lk(s->mu);
-        ensure_redo(*r, fpix * (uint64_t)(std::min(per, nframes) * spp));
         order_on(*r, st);
         for (int f0 = 0; f0 < nframes; f0 += per) {
             const int n = std::min(per, nframes - f0);
@@ -603,11 +631,8 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             return fail(RT_ERR_INVALID_ARGUMENT, "row shard outside the image");
         if ((uint64_t)cam->width * (uint64_t)nrows * (uint64_t)spp >= (1ull << 31))
             return fail(RT_ERR_INVALID_ARGUMENT, "image too large for spp");
-        Replica* r;
-        {
-            std::lock_guard<std::mutex> lk(s->mu);
-            r = &replica_for(s, device);
-        }
+        std::lock_guard<std::mutex> lk(s->mu);
+        Replica* r = &replica_for(s, device);
         DevGuard g(device);
         hipStream_t st = (hipStream_t)stream;
         RtFrameParams fp = frame_params(s, cam, 1, row0, row_stride, nrows);
@@ -618,7 +643,6 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
         fp.hit_pos = out->pos;
         fp.rgb = out->rgb;
         fp.hit_count = out->hit_count;
-        std::lock_guard<std::mutex> lk(s->mu);
         const hipEvent_t* tev = nullptr;
         if (flags & RT_FLAG_TIMING) {
             if (r->tev_used == r->tev.size()) {
@@ -631,7 +655,7 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
         hipError_t e;
         if (paths_wavefront()) {
             const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows;
-            ensure_redo(*r, P);  // candidate lists, stride P
+            ensure_cand(*r, P);  // candidate lists, stride P
             const PathWs ws = ensure_pw(*r, P);
             order_on(*r, st);
             HIP_TRY(hipMemsetAsync(ws.ctl, 0, 16 * sizeof(uint32_t), st));
@@ -656,10 +680,11 @@ int rt_render_rows_device(rt_scene* s, int device, const rt_camera* cam, int mod
 
 int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* out) {
     if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
-    if (s->reps.empty()) return fail(RT_ERR_NO_DEVICE, "scene not uploaded");
     try {
         check_camera(s, cam);
-        Replica& r = s->reps.front();
+        std::lock_guard<std::mutex> lk(s->mu);
+        if (s->reps.empty()) return fail(RT_ERR_NO_DEVICE, "scene not uploaded");
+        Replica& r = *s->reps.front();
         DevGuard g(r.device);
         const size_t npx = (size_t)cam->width * cam->height;
         // staging: hit_id u32 | dist f64 | pos 3xf64 | rgb 3xu8 | hit counter
@@ -688,6 +713,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         fp.rgb = d.rgb;
         fp.hit_count = d.hit_count;
         ensure_redo(r, npx);
+        if (mode == RT_MODE_EXACT && rt::packet_split(1)) ensure_cand(r, npx);
         order_on(r, r.stream);
         HIP_TRY(hipEventRecord(r.ev0, r.stream));
         launch(s, r, fp, mode, false, r.stream, nullptr);
@@ -712,9 +738,10 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
 int rt_diag_raw(rt_scene* s, int device, uint64_t* out, size_t n) {
     if (!s || (!out && n)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     try {
+        std::lock_guard<std::mutex> lk(s->mu);
         Replica& r = replica_for(s, device);
         DevGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        quiesce(r);
         HIP_TRY(hipMemcpy(out, r.d_counters, std::min(n, kCounterWords) * sizeof(uint64_t), hipMemcpyDeviceToHost));
         return RT_OK;
     } catch (const rt::Error& e) {
@@ -725,9 +752,10 @@ int rt_diag_raw(rt_scene* s, int device, uint64_t* out, size_t n) {
 int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
     if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     try {
+        std::lock_guard<std::mutex> lk(s->mu);
         Replica& r = replica_for(s, device);
         DevGuard g(device);
-        HIP_TRY(hipDeviceSynchronize());
+        quiesce(r);
         std::vector<unsigned long long> cv(kCounterWords);
         HIP_TRY(hipMemcpy(cv.data(), r.d_counters, cv.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         const unsigned long long* c = cv.data();
@@ -744,20 +772,9 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->wave_tris = c[12];
         out->redo_rays = c[10] + c[11];
         out->redo_chain = c[11];
-        for (int q = 0; q < 8; q++) out->diag_cycles[q] = c[16 + q];
-        // spread slots: lifetime sum, lifetime max, waves, max tiles per wave
-        uint64_t lsum = 0, lmax = 0, nw = 0, tmax = 0;
-        for (int q = 0; q < 64; q++) {
-            const unsigned long long* sl = c + 32 + 8 * q;
-            lsum += sl[0];
-            lmax = std::max<uint64_t>(lmax, sl[1]);
-            nw += sl[2];
-            tmax = std::max<uint64_t>(tmax, sl[3]);
-        }
-        out->diag_cycles[8] = lsum;
-        out->diag_cycles[9] = lmax;
-        out->diag_cycles[10] = nw;
-        out->diag_cycles[11] = tmax;
+        out->spilled_rays = c[13];
+        out->dropped_rays = c[14];
+        out->empty_node_steps = c[15];
         out->timed_launches = r.tev_used;
         out->trace_ms = 0.0;
         for (size_t k = 0; k < r.tev_used; k++) {
@@ -814,7 +831,7 @@ int rt_scene_tree_dump(const rt_scene* s, double* boxes, int64_t* meta, int64_t*
 
 void rt_scene_destroy(rt_scene* s) {
     if (!s) return;
-    for (auto& r : s->reps) free_replica(r);
+    for (auto& r : s->reps) free_replica(*r);
     delete s;
 }
 

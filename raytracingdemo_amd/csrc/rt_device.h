@@ -40,6 +40,10 @@
 #define RT_QUEUES 8
 #define RT_QUEUE_STRIDE 16
 #define RT_REDO_COUNT (RT_QUEUES * RT_QUEUE_STRIDE)
+// chunks of the candidate overflow pool handed out so far
+#define RT_POOL_COUNT (RT_REDO_COUNT + RT_QUEUE_STRIDE)
+// k_fixup blocks that have read the redo count (the last one clears it)
+#define RT_FIXUP_DONE (RT_REDO_COUNT + 2 * RT_QUEUE_STRIDE)
 // then, per frame of the launch, RT_HIT_SLOTS hit-count partial sums
 // RT_QUEUE_STRIDE words apart (frame f's slot s at RT_HIT_BASE + (f *
 // RT_HIT_SLOTS + s) * RT_QUEUE_STRIDE)
@@ -53,18 +57,17 @@
 #define RT_MAX_BATCH 18
 #endif
 #define RT_QUEUE_WORDS (RT_HIT_BASE + RT_MAX_BATCH * RT_HIT_SLOTS * RT_QUEUE_STRIDE)
-// Candidate lists handed from the traversal to the resolve kernel, per pixel:
-// RT_CAND_LDS entries kept in LDS during the walk plus overflow slots written
-// straight to HBM, RT_CAND_SLOTS in all ({triangle, t lower bound}, 8 B each).
-#ifndef RT_CAND_LDS
+// Candidate lists of the packet walk, per pixel: RT_CAND_LDS entries kept in
+// LDS ({triangle, t lower bound}, 8 B each); past them a lane takes one chunk
+// of RT_POOL_CHUNK entries from a shared overflow pool in HBM (allocated with
+// one atomic, sized by the host; a dry pool falls back to the certified
+// dropped bound).  With spp > 1 the LDS entries go to HBM for k_resolve
+// ([RT_CAND_LDS][pixels] + count byte + dropped bound + chunk index).
 #define RT_CAND_LDS 8
-#endif
-#define RT_CAND_SLOTS 32
+#define RT_POOL_CHUNK 24
 // Quantised W = 8 node for the per-lane walk (walk_tree.cpp quantize_wide8):
 // origin, exponents, SoA 8-bit planes, refs.
 #define RT_QNODE_BYTES 96
-// Half-precision-step W = 8 node for the packet walk (quantize_wide8_f16).
-#define RT_HNODE_BYTES 144
 // tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
 #define RT_TRI32_PAD 4
 
@@ -100,7 +103,6 @@ struct RtDevScene {
     const RT_G uint32_t* rrange;  // real node primitive range [begin, end) (reference order)
     const RT_G uint32_t* ref2walk;// reference-order position -> BVH-order triangle index
     const RT_G uint8_t* qnodes;   // W = 8: quantised copy of `nodes` (RT_QNODE_BYTES each), else null
-    const RT_G uint8_t* hnodes;   // W = 8: fp16-step copy of `nodes` (RT_HNODE_BYTES each), else null
     uint32_t root_ref;
     float root_box[6];
     uint32_t n_tris;
@@ -118,11 +120,15 @@ struct RtLaunchAux {
     int32_t grid;         // persistent blocks (CUs x resident blocks per CU)
     RT_G uint32_t* redo;       // packet kernel -> k_fixup: pixel index | start-pass bit
     uint64_t redo_cap;    // entries (>= pixels of the launch)
-    RT_G unsigned long long* diag;  // 8 cycle-split accumulators (RT_DIAG_TIMING builds)
-    RT_G uint64_t* cand;       // packet kernel -> k_resolve: {tri, t lower bound} per entry, [K][pixels]
-    RT_G uint8_t* cand_cnt;    // entries per pixel (0xFF: overflow)
+    RT_G uint64_t* pool;       // candidate overflow pool: pool_chunks x RT_POOL_CHUNK entries
+    uint32_t pool_chunks;
+    uint32_t reserved;
+    // spp > 1 (packet kernel -> k_resolve) and the wavefront path tracer:
+    RT_G uint64_t* cand;       // {tri, t lower bound} per entry, [K][pixels]
+    RT_G uint8_t* cand_cnt;    // entries per pixel | kCandSpilled | kCandDropped (wavefront: 0xFF = overflow)
     uint64_t cand_cap;         // pixels the candidate buffers hold
     RT_G float* cand_drop;     // per pixel: smallest t bound of a dropped candidate (if flagged)
+    RT_G uint32_t* cand_ovf;   // per pixel: its overflow pool chunk (if flagged)
 };
 
 // One camera pose of a launch (Camera, camera.hpp:20-38: position, view

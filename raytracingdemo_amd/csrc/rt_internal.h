@@ -59,8 +59,6 @@ WalkTree build_walk_tree(const Soup& s);
 std::vector<int32_t> collapse_children(const WalkTree& w, int32_t b, int W);
 // 8-bit quantised copy of W = 8 wide nodes (RT_QNODE_BYTES each; walk_tree.cpp).
 std::vector<uint8_t> quantize_wide8(const uint8_t* wide, uint64_t n_nodes);
-// fp16-step variant for the packet walk (RT_HNODE_BYTES each; walk_tree.cpp).
-std::vector<uint8_t> quantize_wide8_f16(const uint8_t* wide, uint64_t n_nodes);
 
 // Device-format scene (wide fp32 nodes + fp64 leaf data), built from Tree.
 struct Flat {

@@ -265,75 +265,5 @@ std::vector<uint8_t> quantize_wide8(const uint8_t* wide, uint64_t n_nodes) {
     return out;
 }
 
-// Half-precision variant for the packet walk (packet_kernel.h, RT_HNODES):
-// RT_HNODE_BYTES per W = 8 node —
-//   dwords 0-2   origin x, y, z (fp32)
-//   dword 3      exponents e_x, e_y, e_z (bytes, biased by 127) | meta byte
-//                (slot 0's pad: sort axis | valid slots << 2)
-//   dwords 4-27  planes as fp16 integers 0..2048, SoA: lo.x[8] hi.x[8] lo.y[8]
-//                hi.y[8] lo.z[8] hi.z[8] (child c in half c & 1 of dword c / 2)
-//   dwords 28-35 the 8 child refs
-// Same exactness as quantize_wide8 (plane = origin + q 2^e exactly, lo down,
-// hi up), 11-bit steps; invalid slots lie past the valid count (meta).
-std::vector<uint8_t> quantize_wide8_f16(const uint8_t* wide, uint64_t n_nodes) {
-    std::vector<uint8_t> out(n_nodes * RT_HNODE_BYTES, 0);
-    auto f16 = [](double q) -> uint16_t {  // integers 0..2048: exact in binary16
-        const int v = (int)q;
-        if (v == 0) return 0;
-        int e = 0;
-        while ((v >> (e + 1)) != 0) e++;
-        const uint32_t mant = (e <= 10 ? ((uint32_t)v << (10 - e)) : ((uint32_t)v >> (e - 10))) & 0x3FFu;
-        return (uint16_t)(((uint32_t)(e + 15) << 10) | mant);
-    };
-    for (uint64_t n = 0; n < n_nodes; n++) {
-        const float* rec = reinterpret_cast<const float*>(wide + n * 256);
-        uint32_t* q = reinterpret_cast<uint32_t*>(out.data() + n * RT_HNODE_BYTES);
-        uint16_t* planes = reinterpret_cast<uint16_t*>(q + 4);
-        bool valid[8];
-        double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-        bool any = false;
-        for (int c = 0; c < 8; c++) {
-            const uint32_t ref = reinterpret_cast<const uint32_t*>(rec + 8 * c)[RT_CHILD_REF];
-            q[28 + c] = ref;
-            valid[c] = ref != RT_INVALID_REF;
-            if (!valid[c]) continue;
-            for (int a = 0; a < 3; a++) {
-                const double l = rec[8 * c + 2 * a], h = rec[8 * c + 2 * a + 1];
-                lo[a] = any ? std::min(lo[a], l) : l;
-                hi[a] = any ? std::max(hi[a], h) : h;
-            }
-            any = true;
-        }
-        uint32_t hdr = (reinterpret_cast<const uint32_t*>(rec)[7] & 0xFFu) << 24;  // meta
-        for (int a = 0; a < 3; a++) {
-            const double ext = hi[a] - lo[a];
-            int e = ext > 0 ? (int)std::ceil(std::log2(ext / 2048.0)) : -100;
-            e = std::max(e, -100);
-            double org = 0, sc = 0;
-            for (;; e++) {
-                sc = std::ldexp(1.0, e);
-                org = std::floor(lo[a] / sc) * sc;
-                if (std::fabs(org) / sc < 16777216.0 && (hi[a] - org) / sc <= 2048.0) break;
-            }
-            if (e > 127) throw Error{RT_ERR_INVALID_ARGUMENT, "scene extent too large to quantise"};
-            reinterpret_cast<float*>(q)[a] = (float)org;
-            hdr |= (uint32_t)(e + 127) << (8 * a);
-            for (int c = 0; c < 8; c++) {
-                double ql = 2048, qh = 0;
-                if (valid[c]) {
-                    const double l = rec[8 * c + 2 * a], h = rec[8 * c + 2 * a + 1];
-                    ql = std::floor((l - org) / sc);
-                    qh = std::ceil((h - org) / sc);
-                    if (ql < 0 || qh > 2048 || org + ql * sc > l || org + qh * sc < h)
-                        throw Error{RT_ERR_RUNTIME, "node quantisation out of range"};
-                }
-                planes[16 * a + c] = f16(ql);      // lo[a] array
-                planes[16 * a + 8 + c] = f16(qh);  // hi[a] array
-            }
-        }
-        q[3] = hdr;
-    }
-    return out;
-}
 
 }  // namespace rt

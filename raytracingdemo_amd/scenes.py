@@ -183,3 +183,19 @@ def sponza_scene():
         from . import load_obj
         return load_obj(path, 1.0), f"sponza.obj ({path})"
     return sponza_proxy_triangles(), "sponza-proxy (procedural, 262267 tris)"
+
+
+ARMADILLO_SCALE = 0.035  # the reference runner's scale (testruns_2025_12_25/testrun_62/render_times.csv:2)
+
+
+def armadillo_scene():
+    """(triangles, label) of config c3 (armadillo.obj at the runner's scale
+    0.035), or None: the geometry is stripped from the reference
+    (.MISSING_LARGE_BLOBS), so it runs only where RT_ARMADILLO_OBJ names the
+    file.  The reference's published frames of it (testruns_final/testrun_0)
+    pin the result (tests/golden/reference_frames.json)."""
+    path = os.environ.get("RT_ARMADILLO_OBJ")
+    if not path or not os.path.exists(path):
+        return None
+    from . import load_obj
+    return load_obj(path, ARMADILLO_SCALE), f"armadillo.obj ({path})"

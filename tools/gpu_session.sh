@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
-# One GPU-box session: smoke -> parity tests -> bench -> rocprofv3 kernel trace.
-# Each GPU step has its own time limit; the session stops at the first fault,
-# abort, segfault or timeout (exit >= 2 other than pytest's "tests failed" = 1).
+# One GPU-box session: named steps, each under its own time limit; the session
+# stops at the first fault, abort, segfault or timeout (exit >= 2 other than
+# pytest's "tests failed" = 1).  Logs go to gpurun_out/<step>.log.
 # Usage: tools/gpu_session.sh [steps...]   (default: smoke tests bench prof)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -15,7 +15,7 @@ run() {  # name limit cmd...
     timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
     local rc=$?
     echo "=== $name exit=$rc"
-    tail -n 25 "gpurun_out/$name.log"
+    tail -n 4 "gpurun_out/$name.log" | cut -c1-1500
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name exit $rc"; exit $rc; fi
     if [ $rc -eq 1 ] && [ "$name" != "tests" ]; then echo "STOP: $name failed"; exit 1; fi
     return 0
@@ -24,8 +24,12 @@ run() {  # name limit cmd...
 for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python __graft_entry__.py smoke ;;
-        tests) run tests 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+        tests) run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         bench) run bench 600 python bench.py ;;
+        quick) run bench_quick 300 python bench.py --no-cpu --steps 10 ;;
+        split) RT_RESOLVE=split run bench_split 300 python bench.py --no-cpu --steps 10 ;;
+        spp4)  run bench_spp4 300 python bench.py --no-cpu --steps 5 --spp 4 ;;
+        paths) run bench_paths 300 python bench.py --no-cpu --paths --steps 3 --warmup 1 ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
                    -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
         pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
@@ -34,22 +38,13 @@ for s in $STEPS; do
                    -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu && \
                python tools/pmc_traffic.py gpurun_out/pmc/fetch_counter_collection.csv \
                    gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
-        list)  run list 120 rocprofv3 -L ;;
-        waves) for w in 3 4 5; do RT_WAVES=$w run bench_w$w 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
-        quick) run bench_quick 300 python bench.py --no-cpu --steps 5 ;;
-        occ)   for b in 3 4 5 6; do RT_BLOCKS_PER_CU=$b run bench_b$b 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
-        notime) RT_BENCH_NO_KTIMING=1 run bench_notime 300 python bench.py --no-cpu --steps 5 ;;
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}" 300 \
-                          python bench.py --no-cpu --steps 5 || exit 1; done ;;
-        batches) for b in 1 4 6 12; do RT_BATCH=$b run bench_b$b 300 python bench.py --no-cpu --steps 5 || exit 1; done ;;
-        lane)  RT_KERNEL=lane run bench_lane 300 python bench.py --no-cpu --steps 5 ;;
-        lanetests) RT_KERNEL=lane run tests_lane 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+                          python bench.py --no-cpu --steps 10 || exit 1; done ;;
         sq)    for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
                            "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD" \
                            "SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_TC_DATA_READ_REQ SQC_TC_STALL SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
-                           "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" \
-                           "SQC_DCACHE_MISSES_DUPLICATE SQC_DCACHE_REQ_READ_16 SQC_DCACHE_REQ_READ_8 SQC_DCACHE_REQ_READ_4 TCC_TAG_STALL_sum TCC_LATENCY_FIFO_FULL_sum"; do
+                           "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
                    pn=$((${pn:-0}+1))
                    run sq$pn 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$pn \
                        -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu --key-out gpurun_out/pmc_key.txt || exit 1

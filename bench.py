@@ -87,6 +87,7 @@ def parse():
                                                          "(config c4: 4; headline: 1), paths default 16")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-dropin", action="store_true", help="skip the rt_render_frame (drop-in path) rate")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="committed rocprofv3 PMC summary supplying roofline.traffic")
     p.add_argument("--key-out", default="", help="write this run's workload key (for tools/pmc_traffic.py)")
@@ -493,7 +494,7 @@ def main():
             pass
         cpu = None
         dropin = None
-        if world == 1:
+        if world == 1 and not a.no_dropin and S == 1:
             dropin = dropin_rate(scene, cams, W, H, mode)
         if world == 1 and not a.no_cpu:
             cpu = cpu_baseline(tris, a.algo, a.k, cams, W, H, a.cpu_seconds)

@@ -89,7 +89,8 @@ struct Replica {
     int grid = 0;
     uint32_t* d_redo = nullptr;  // packet pipeline -> fix-up kernel pixel list
     uint64_t redo_cap = 0;
-    uint64_t* d_pool = nullptr;  // candidate overflow pool (kPoolChunks x RT_POOL_CHUNK entries)
+    uint64_t* d_pool = nullptr;  // candidate overflow pool (pool_chunks x RT_POOL_CHUNK entries)
+    uint32_t pool_chunks = 0;
     void* d_cand = nullptr;      // spp > 1 / wavefront paths: candidate lists in HBM
     uint64_t cand_cap = 0;       // pixels
     void* d_pw = nullptr;        // wavefront path tracer workspace (PathWs), pw_cap paths
@@ -235,7 +236,12 @@ void upload_one(rt_scene* s, int device) {
     HIP_TRY(hipMalloc(&r.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
     HIP_TRY(hipMemset(r.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&r.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
-    HIP_TRY(hipMalloc(&r.d_pool, (size_t)kPoolChunks * RT_POOL_CHUNK * sizeof(uint64_t)));
+    r.pool_chunks = kPoolChunks;
+    if (const char* e = std::getenv("RT_POOL_CHUNKS")) {  // test hook: a small pool runs dry
+        const long v = std::atol(e);
+        if (v >= 1 && v <= (long)kPoolChunks) r.pool_chunks = (uint32_t)v;
+    }
+    HIP_TRY(hipMalloc(&r.d_pool, (size_t)r.pool_chunks * RT_POOL_CHUNK * sizeof(uint64_t)));
     s->reps.push_back(std::move(rp));
 }
 
@@ -399,7 +405,7 @@ RtLaunchAux aux_of(Replica& r) {
     a.redo = r.d_redo;
     a.redo_cap = r.redo_cap;
     a.pool = r.d_pool;
-    a.pool_chunks = kPoolChunks;
+    a.pool_chunks = r.pool_chunks;
     a.cand = static_cast<uint64_t*>(r.d_cand);
     if (r.d_cand) {
         uint8_t* base = static_cast<uint8_t*>(r.d_cand);

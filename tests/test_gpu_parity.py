@@ -195,12 +195,12 @@ def _stack_scene(eps: float, n: int, far_hit: bool) -> np.ndarray:
 
 def test_candidate_overflow_paths(oracle):
     """More borderline candidates than the per-lane LDS list holds (8): the
-    next 24 go to the pixel's HBM overflow slots, past those they are dropped.
+    next 24 go to the lane's overflow pool chunk, past those they are dropped.
 
     (a) corners exactly on the ray: the nearest is a real hit (certified
         against the smallest dropped bound when there are > 32);
     (b) corners 1e-7 off the ray: every listed candidate fails the exact test;
-        with 14 the real hit is still in the overflow slots (no redo), with 40
+        with 14 the real hit is still in the pool chunk (no redo), with 40
         it was dropped, so the pixel must be redone by the fix-up kernel.
     All must equal the reference traversal."""
     torch = pytest.importorskip("torch")
@@ -257,7 +257,7 @@ def test_row_shards_reassemble_to_full_frame():
 
 @pytest.mark.parametrize("mode", ["exact", "fp64"])
 def test_batched_frames_equal_single_frames(mode):
-    """rt_render_batch_device over 27 poses (three launches: 12 + 12 + 3 frames)
+    """rt_render_batch_device over 27 poses (two launches: 18 + 9 frames)
     of a row shard equals 27 single-frame renders: ids, distances, positions,
     colours and per-frame hit counts, bit for bit."""
     torch = pytest.importorskip("torch")

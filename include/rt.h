@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* status codes */
 #define RT_OK 0
@@ -158,12 +158,41 @@ int rt_camera_path(const double scene_center[3], int resolution, int step, doubl
  * reference's.  The scene is host-only until rt_scene_upload. */
 int rt_scene_create(const double *tri_v, uint64_t n_tris, int algo, int k, int collapse, rt_scene **out);
 
-/* Replicate the flattened scene on each listed HIP device (ordinal). */
+/* Replicate the flattened scene on each listed HIP device (ordinal).  With
+ * more than one device the library also creates an RCCL communicator over
+ * them (ncclCommInitAll, one rank per device in this process; rank g = the
+ * g-th uploaded device), used by rt_render_frame / rt_render_batch_multi. */
 int rt_scene_upload(rt_scene *s, const int *devices, int n_devices);
 
-/* One whole frame on the first uploaded device, blocking; replaces
- * calculateScreen + shadeScreen (main.cpp:253-262). */
+/* One whole frame, blocking; replaces calculateScreen + shadeScreen
+ * (main.cpp:253-262).  On one device it renders there; on G uploaded devices
+ * image rows are interleaved (row j on the (j mod G)-th device), each device
+ * renders its rows, and the shards (hit-id + dist + pos + rgb as requested,
+ * hit counts) are gathered to the first device with RCCL and de-interleaved
+ * there before the copy to the host.  seconds: device time
+ * of the frame on the first device's stream (renders to gather). */
 int rt_render_frame(rt_scene *s, const rt_camera *cam, int mode, rt_frame_out *out);
+
+/* rt_render_batch_spp_device over every uploaded device: nframes poses of full
+ * frames (row0 = 0, stride 1, nrows = height) into device buffers `out` on the
+ * FIRST uploaded device, asynchronous on `stream` (a stream of that device).
+ * With G > 1 devices rows are interleaved as in rt_render_frame, each device
+ * renders its rows of every pose, and one RCCL gather per call brings the
+ * shards to the first device, which de-interleaves them; hit_count[f] adds
+ * all shards.  Results are identical to a one-device render.  (Test hook:
+ * RT_VIRTUAL_SHARDS=N shards a one-device scene into N row shards on that
+ * device, gathered with device copies.) */
+int rt_render_batch_multi(rt_scene *s, const rt_camera *cams, int nframes, int spp, int mode, const rt_device_out *out,
+                          void *stream, uint32_t flags);
+
+/* The de-interleave of rt_render_batch_multi on the host (the same index
+ * arithmetic as the device kernel; for tests and host-side gathers):
+ * `gathered` holds `shards` blocks of block_bytes; each block's section at
+ * section_offset is [frames][rt_shard_pad rows][width] elements of
+ * elem_bytes, shard g holding image rows g, g + shards, ...; writes
+ * frames_out[frames][height][width] elements. */
+int rt_deinterleave_rows(const void *gathered, uint64_t block_bytes, uint64_t section_offset, int shards, int frames,
+                         int height, int width, int elem_bytes, void *frames_out);
 
 /* Asynchronous shard render into caller device buffers on a caller stream
  * (hipStream_t passed as void*; NULL = the null stream).  Used by the

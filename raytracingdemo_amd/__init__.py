@@ -232,6 +232,18 @@ class Scene:
                                                    (N.RT_FLAG_COUNT if count else 0) |
                                                    (N.RT_FLAG_TIMING if timing else 0)))
 
+    def render_batch_multi(self, cams, W: int, H: int, hit_id=0, dist=0, hit_pos=0, rgb=0, hit_count=0, stream=0,
+                           mode: str = "exact", count: bool = False, timing: bool = False, spp: int = 1):
+        """Full frames of every pose in ``cams`` over all uploaded devices (rows
+        interleaved, RCCL gather to the first device, de-interleaved there) into
+        device pointers on the first device (include/rt.h rt_render_batch_multi)."""
+        n = len(cams)
+        arr = (N.rt_camera * max(n, 1))(*[_camera(p, d, W, H) for p, d in cams])
+        o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
+        m = N.RT_MODE_FP64 if mode in ("fp64", "literal") else N.RT_MODE_EXACT
+        N.check(N.lib().rt_render_batch_multi(self._h, arr, n, int(spp), m, C.byref(o), C.c_void_p(stream or None),
+                                              (N.RT_FLAG_COUNT if count else 0) | (N.RT_FLAG_TIMING if timing else 0)))
+
     def render_paths_device(self, device: int, pos, d, W: int, H: int, row0: int, row_stride: int, nrows: int,
                             frame: int = 0, spp: int = 16, bounces: int = 4, hit_id=0, dist=0, hit_pos=0, rgb=0,
                             hit_count=0, stream=0, timing: bool = False, count: bool = False):
@@ -253,6 +265,18 @@ class Scene:
             v = getattr(s, f)
             out[f] = list(v) if isinstance(v, C.Array) else v
         return out
+
+
+def deinterleave_rows(gathered: np.ndarray, shards: int, frames: int, H: int, W: int, elem_bytes: int,
+                      block_bytes: int | None = None, section_offset: int = 0) -> np.ndarray:
+    """Host de-interleave of gathered row shards (include/rt.h rt_deinterleave_rows):
+    uint8 [frames, H, W * elem_bytes]."""
+    g = np.ascontiguousarray(gathered, dtype=np.uint8).reshape(-1)
+    block = len(g) // shards if block_bytes is None else int(block_bytes)
+    out = np.empty((frames, H, W * elem_bytes), np.uint8)
+    N.check(N.lib().rt_deinterleave_rows(g.ctypes.data, block, int(section_offset), int(shards), int(frames), int(H),
+                                         int(W), int(elem_bytes), out.ctypes.data))
+    return out
 
 
 def ppm_bytes(rgb: np.ndarray, W: int, H: int) -> bytes:

@@ -34,6 +34,7 @@ EXPORTS = [
     "rt_load_obj", "rt_load_obj_cached", "rt_free", "rt_scene_center", "rt_camera_path", "rt_scene_create", "rt_scene_upload",
     "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_render_paths_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
     "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
+    "rt_render_batch_multi", "rt_deinterleave_rows",
 ]
 
 
@@ -95,9 +96,10 @@ def _share_hip_runtime_with_torch() -> None:
     spec = importlib.util.find_spec("torch")
     if spec is None or not spec.submodule_search_locations:
         return
-    cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
-    if os.path.exists(cand):
-        C.CDLL(cand, mode=C.RTLD_GLOBAL)
+    for name in ("libamdhip64.so", "librccl.so"):  # (RCCL: opened by the library on a multi-device upload)
+        cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", name)
+        if os.path.exists(cand):
+            C.CDLL(cand, mode=C.RTLD_GLOBAL)
 
 
 def lib() -> C.CDLL:
@@ -131,6 +133,10 @@ def lib() -> C.CDLL:
                                              C.c_uint32]
     L.rt_render_paths_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_int, C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
+    L.rt_render_batch_multi.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
+                                        C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
+    L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_void_p]
     L.rt_frame_stats.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(rt_frame_stats_t)]
     L.rt_scene_stats.argtypes = [C.c_void_p, C.POINTER(rt_scene_stats_t)]
     L.rt_diag_raw.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]

@@ -931,6 +931,55 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     }
 }
 
+// Multi-device frames: the shards gathered to the first device ([G][block]
+// bytes) become full frames.  One block per image row of a frame copies the
+// row's W * eb bytes from its shard (rt_gathered_row), in words when both
+// sides allow it.
+__global__ void __launch_bounds__(256) k_deinterleave(const uint8_t* __restrict__ gather, uint64_t block,
+                                                      uint64_t sec_off, int G, int F, int H, int W, int R, int eb,
+                                                      uint8_t* __restrict__ dst) {
+    const int f = (int)(blockIdx.x / (unsigned)H), j = (int)(blockIdx.x % (unsigned)H);
+    if (f >= F) return;
+    const uint64_t n = (uint64_t)W * eb;
+    const uint8_t* src = gather + rt_gathered_row(j, f, G, R, W, eb, block, sec_off);
+    uint8_t* d = dst + ((uint64_t)f * H + j) * n;
+    if (((uintptr_t)src | (uintptr_t)d | n) % 4 == 0) {
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
+        for (uint64_t k = threadIdx.x; k < n / 4; k += blockDim.x) d4[k] = s4[k];
+    } else {
+        for (uint64_t k = threadIdx.x; k < n; k += blockDim.x) d[k] = src[k];
+    }
+}
+
+// Per-frame hit counts of the G shards (u64 [F] at cnt_off of each block) added
+// to the caller's counters.
+__global__ void k_sum_counts(const uint8_t* __restrict__ gather, uint64_t block, uint64_t cnt_off, int G, int F,
+                             unsigned long long* __restrict__ out) {
+    const int f = (int)threadIdx.x;
+    if (f >= F) return;
+    unsigned long long t = 0;
+    for (int g = 0; g < G; g++) t += reinterpret_cast<const unsigned long long*>(gather + g * block + cnt_off)[f];
+    out[f] += t;
+}
+
+hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_off, int G, int F, int H, int W,
+                               int eb, void* dst, hipStream_t s) {
+    if (F <= 0 || H <= 0 || W <= 0 || G <= 0 || eb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)((uint64_t)F * H)), dim3(256), 0, s,
+                       static_cast<const uint8_t*>(gather), block, sec_off, G, F, H, W, rt_shard_pad(H, G), eb,
+                       static_cast<uint8_t*>(dst));
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_off, int G, int F,
+                             unsigned long long* out, hipStream_t s) {
+    if (F <= 0 || F > 1024) return F <= 0 ? hipSuccess : hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_sum_counts, dim3(1), dim3(1024), 0, s, static_cast<const uint8_t*>(gather), block, cnt_off,
+                       G, F, out);
+    return hipGetLastError();
+}
+
 // Diffuse path tracing of one pose (path_kernel.h): spp paths per pixel of
 // 1 + bounces segments each, on a zeroed work queue; leaves it dirty.
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,

@@ -1,7 +1,9 @@
 // extern "C" surface of librtmi355x.so (include/rt.h).  Host C++ around the
 // gfx950 kernels in render.hip: scene ownership, device replicas, the frame
 // call that replaces calculateScreen + shadeScreen (src/main.cpp:253-262).
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -28,6 +30,10 @@ int packet_candidates();
 bool packet_split(int spp);
 uint32_t params_bytes();
 int exact_lds_stack();
+hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_off, int G, int F, int H, int W,
+                               int eb, void* dst, hipStream_t s);
+hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_off, int G, int F,
+                             unsigned long long* out, hipStream_t s);
 }
 
 namespace {
@@ -110,6 +116,20 @@ struct Replica {
 
 }  // namespace
 
+// Multi-device frames (rt_render_batch_multi): per shard a staging block on
+// its device, the gathered blocks on the first device, and the RCCL
+// communicator over the uploaded devices (one rank per device, this process).
+struct Group {
+    std::vector<void*> stage;      // shard g's block (on its shard's device)
+    std::vector<int> stage_dev;
+    uint64_t block = 0;            // bytes per block (grown, never shrunk)
+    void* gather = nullptr;        // [G][block] on the first device
+    uint64_t gather_bytes = 0;
+    std::vector<ncclComm_t> comms; // comms[g]: rank g = reps[g] (distinct devices only)
+    hipEvent_t ev_in = nullptr, ev_out = nullptr, ev0 = nullptr, ev1 = nullptr;  // on the first device
+    std::vector<hipEvent_t> ev_shard;  // per shard: its render is done (copy transport)
+};
+
 struct rt_scene {
     rt::Soup soup;
     rt::Tree tree;
@@ -117,9 +137,72 @@ struct rt_scene {
     std::vector<std::unique_ptr<Replica>> reps;  // stable addresses: a replica outlives the lock
     std::mutex mu;
     uint32_t literal_stack = 0;  // stack bound of the literal (reference-order) traversal
+    Group grp;
 };
 
 namespace {
+
+// RCCL, opened on the first multi-device upload (dlopen, so single-device
+// users never initialise it): the process's copy when one is mapped already
+// (PyTorch's librccl.so.1, preloaded by the Python binding), else ROCm's.
+struct Rccl {
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGather) gather = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) throw rt::Error{RT_ERR_RUNTIME, std::string("RCCL not found: ") + dlerror()};
+        x.init_all = (decltype(x.init_all))dlsym(h, "ncclCommInitAll");
+        x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
+        x.gather = (decltype(x.gather))dlsym(h, "ncclGather");
+        x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+        x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
+        x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+        if (!x.init_all || !x.destroy || !x.gather || !x.group_start || !x.group_end || !x.error_string)
+            throw rt::Error{RT_ERR_RUNTIME, "RCCL lacks ncclCommInitAll / ncclGather / group calls"};
+        return x;
+    }();
+    return r;
+}
+#define NCCL_TRY(expr)                                                                               \
+    do {                                                                                             \
+        ncclResult_t e_ = (expr);                                                                    \
+        if (e_ != ncclSuccess) throw rt::Error{RT_ERR_HIP, std::string(#expr) + ": " + rccl().error_string(e_)}; \
+    } while (0)
+
+void free_group(rt_scene* s) {
+    Group& g = s->grp;
+    int prev = -1;
+    hipGetDevice(&prev);
+    for (size_t k = 0; k < g.stage.size(); k++)
+        if (g.stage[k]) {
+            hipSetDevice(g.stage_dev[k]);
+            hipFree(g.stage[k]);
+        }
+    g.stage.clear();
+    g.stage_dev.clear();
+    g.block = 0;
+    if (!s->reps.empty()) hipSetDevice(s->reps.front()->device);
+    if (g.gather) hipFree(g.gather);
+    g.gather = nullptr;
+    g.gather_bytes = 0;
+    for (hipEvent_t e : {g.ev_in, g.ev_out, g.ev0, g.ev1})
+        if (e) hipEventDestroy(e);
+    g.ev_in = g.ev_out = g.ev0 = g.ev1 = nullptr;
+    for (hipEvent_t e : g.ev_shard)
+        if (e) hipEventDestroy(e);
+    g.ev_shard.clear();
+    for (ncclComm_t c : g.comms) rccl().destroy(c);
+    g.comms.clear();
+    if (prev >= 0) hipSetDevice(prev);
+}
 
 void free_replica(Replica& r) {
     if (r.device < 0) return;
@@ -442,6 +525,181 @@ void launch(const rt_scene* s, Replica& r, const RtFrameParams& fp, int mode, bo
     HIP_TRY(e);
 }
 
+// Poses cams[0..nframes) of one row shard on replica r, into device buffers
+// `out`, on stream st (scene lock held, r's device current): up to
+// batch_frames() sample frames per launch.
+void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nframes, int spp, int mode, int row0,
+                         int row_stride, int nrows, const rt_device_out* out, hipStream_t st, uint32_t flags) {
+    Replica* r = &rr;
+    const rt_camera* cam = &cams[0];
+    const uint64_t fpix = (uint64_t)cam->width * (uint64_t)nrows;  // pixels per frame
+    // poses per launch: the batch's sample-frame limit, and batch pixels
+    // < 2^31 (redo-list entries)
+    int per = std::max(1, batch_frames() / spp);
+    while (per > 1 && fpix * (uint64_t)(per * spp) >= (1ull << 31)) per--;
+    if (fpix * (uint64_t)spp >= (1ull << 31)) throw rt::Error{RT_ERR_INVALID_ARGUMENT, "image too large for spp"};
+    const bool split = mode == RT_MODE_EXACT && rt::packet_split(spp);
+    if (split) {
+        // candidate lists in HBM (73 B per sample pixel): at most half of
+        // the device memory that is free (or already ours), fewer poses
+        // per launch otherwise
+        size_t mfree = 0, mtotal = 0;
+        HIP_TRY(hipMemGetInfo(&mfree, &mtotal));
+        const uint64_t avail = (uint64_t)mfree + r->cand_cap * kCandBytesPerPixel;
+        while (per > 1 && fpix * (uint64_t)(per * spp) * kCandBytesPerPixel > avail / 2) per--;
+        ensure_cand(*r, fpix * (uint64_t)(std::min(per, nframes) * spp));
+    }
+    ensure_redo(*r, fpix * (uint64_t)std::min(per, nframes));
+    // serialise on the replica's stream: the caller's stream waits for it
+    order_on(*r, st);
+    for (int f0 = 0; f0 < nframes; f0 += per) {
+        const int n = std::min(per, nframes - f0);
+        RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows, spp);
+        const uint64_t off = (uint64_t)f0 * fpix, soff = off * (uint64_t)spp;
+        fp.hit_id = out->hit_id ? out->hit_id + soff : nullptr;
+        fp.dist = out->dist ? out->dist + soff : nullptr;
+        fp.hit_pos = out->pos ? out->pos + 3 * soff : nullptr;
+        fp.rgb = out->rgb ? out->rgb + 3 * off : nullptr;
+        fp.hit_count = out->hit_count ? out->hit_count + f0 : nullptr;
+        fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
+        const hipEvent_t* tev = nullptr;
+        if (flags & RT_FLAG_TIMING) {
+            if (r->tev_used == r->tev.size()) {
+                std::array<hipEvent_t, 2> a{};
+                for (auto& e : a) HIP_TRY(hipEventCreate(&e));
+                r->tev.push_back(a);
+            }
+            tev = r->tev[r->tev_used++].data();
+        }
+        launch(s, *r, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, tev);
+    }
+}
+
+// Shards of a multi-device frame: RT_VIRTUAL_SHARDS=N (test hook, read per
+// call) splits a one-device scene into N shards on that device, gathered by
+// device copies instead of RCCL.
+int group_shards(const rt_scene* s) {
+    if (s->reps.size() > 1) return (int)s->reps.size();
+    const char* e = std::getenv("RT_VIRTUAL_SHARDS");
+    const int v = e ? std::atoi(e) : 1;
+    return v >= 1 && v <= 64 ? v : 1;
+}
+
+// Block layout of one shard (256-B aligned sections): per-sample hit ids,
+// distances and positions, per-pixel rgb, per-pose hit counts — only the
+// outputs the caller asked for.
+struct ShardLayout {
+    uint64_t id = 0, dist = 0, pos = 0, rgb = 0, cnt = 0, bytes = 0;
+};
+ShardLayout shard_layout(const rt_device_out* out, int F, int R, int W, int spp) {
+    ShardLayout L;
+    const uint64_t px = (uint64_t)F * R * W;
+    uint64_t off = 0;
+    auto sec = [&](bool want, uint64_t bytes) {
+        const uint64_t o = off;
+        if (want) off += align_up<char>(bytes);
+        return o;
+    };
+    L.id = sec(out->hit_id, px * spp * 4);
+    L.dist = sec(out->dist, px * spp * 8);
+    L.pos = sec(out->pos, px * spp * 24);
+    L.rgb = sec(out->rgb, px * 3);
+    L.cnt = sec(true, (uint64_t)F * 8);
+    L.bytes = off;
+    return L;
+}
+
+// All poses over every shard (row g of every G-th row on the g-th device),
+// gathered to the first device and de-interleaved there into full frames
+// `out` (device pointers on the first device), asynchronous on st0 (a stream
+// of the first device).  Scene lock held.
+void render_group(rt_scene* s, const rt_camera* cams, int nframes, int spp, int mode, const rt_device_out* out,
+                  hipStream_t st0, uint32_t flags) {
+    Group& gp = s->grp;
+    const int G = group_shards(s);
+    const int W = cams[0].width, H = cams[0].height, R = rt_shard_pad(H, G);
+    const bool virt = s->reps.size() == 1;
+    Replica& r0 = *s->reps.front();
+    const ShardLayout L = shard_layout(out, nframes, R, W, spp);
+    // buffers (grown, never shrunk; earlier groups finished first)
+    if (gp.block < L.bytes || (int)gp.stage.size() != G) {
+        for (auto& r : s->reps) quiesce(*r);
+        for (size_t k = 0; k < gp.stage.size(); k++) {
+            DevGuard dg(gp.stage_dev[k]);
+            HIP_TRY(hipFree(gp.stage[k]));
+        }
+        gp.stage.assign(G, nullptr);
+        gp.stage_dev.assign(G, r0.device);
+        for (int g = 0; g < G; g++) {
+            gp.stage_dev[g] = virt ? r0.device : s->reps[g]->device;
+            DevGuard dg(gp.stage_dev[g]);
+            HIP_TRY(hipMalloc(&gp.stage[g], L.bytes));
+        }
+        gp.block = L.bytes;
+    }
+    const uint64_t block = gp.block;
+    DevGuard d0(r0.device);
+    if (gp.gather_bytes < block * G) {
+        quiesce(r0);
+        if (gp.gather) HIP_TRY(hipFree(gp.gather));
+        gp.gather = nullptr;
+        HIP_TRY(hipMalloc(&gp.gather, block * G));
+        gp.gather_bytes = block * G;
+    }
+    if (!gp.ev_in) {
+        for (hipEvent_t* e : {&gp.ev_in, &gp.ev_out}) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        for (hipEvent_t* e : {&gp.ev0, &gp.ev1}) HIP_TRY(hipEventCreate(e));
+    }
+    HIP_TRY(hipEventRecord(gp.ev_in, st0));
+    HIP_TRY(hipEventRecord(gp.ev0, r0.stream));
+    // every shard renders its rows of every pose into its block
+    for (int g = 0; g < G; g++) {
+        Replica& r = virt ? r0 : *s->reps[g];
+        DevGuard dg(r.device);
+        HIP_TRY(hipStreamWaitEvent(r.stream, gp.ev_in, 0));
+        uint8_t* b = static_cast<uint8_t*>(gp.stage[g]);
+        HIP_TRY(hipMemsetAsync(b + L.cnt, 0, (size_t)nframes * 8, r.stream));
+        rt_device_out so{};
+        so.hit_id = out->hit_id ? reinterpret_cast<uint32_t*>(b + L.id) : nullptr;
+        so.dist = out->dist ? reinterpret_cast<double*>(b + L.dist) : nullptr;
+        so.pos = out->pos ? reinterpret_cast<double*>(b + L.pos) : nullptr;
+        so.rgb = out->rgb ? b + L.rgb : nullptr;
+        so.hit_count = reinterpret_cast<unsigned long long*>(b + L.cnt);
+        const int nrows = rt_shard_rows(H, G, g);
+        if (nrows > 0) render_batch_locked(s, r, cams, nframes, spp, mode, g, G, nrows, &so, r.stream, flags);
+    }
+    // gather to the first device: RCCL between distinct devices (one group of
+    // ncclGather calls, each on its shard's stream), device copies otherwise
+    if (!virt) {
+        NCCL_TRY(rccl().group_start());
+        for (int g = 0; g < G; g++) {
+            DevGuard dg(s->reps[g]->device);
+            NCCL_TRY(rccl().gather(gp.stage[g], g == 0 ? gp.gather : nullptr, block, ncclUint8, 0, gp.comms[g],
+                                   s->reps[g]->stream));
+        }
+        NCCL_TRY(rccl().group_end());
+    } else {
+        for (int g = 0; g < G; g++)
+            HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(gp.gather) + (uint64_t)g * block, gp.stage[g], block,
+                                   hipMemcpyDeviceToDevice, r0.stream));
+    }
+    // de-interleave on the first device (its stream follows its gather)
+    const int ssz = spp;
+    if (out->hit_id)
+        HIP_TRY(rt::launch_deinterleave(gp.gather, block, L.id, G, nframes, H, W, 4 * ssz, out->hit_id, r0.stream));
+    if (out->dist)
+        HIP_TRY(rt::launch_deinterleave(gp.gather, block, L.dist, G, nframes, H, W, 8 * ssz, out->dist, r0.stream));
+    if (out->pos)
+        HIP_TRY(rt::launch_deinterleave(gp.gather, block, L.pos, G, nframes, H, W, 24 * ssz, out->pos, r0.stream));
+    if (out->rgb) HIP_TRY(rt::launch_deinterleave(gp.gather, block, L.rgb, G, nframes, H, W, 3, out->rgb, r0.stream));
+    if (out->hit_count)
+        HIP_TRY(rt::launch_sum_counts(gp.gather, block, L.cnt, G, nframes, out->hit_count, r0.stream));
+    HIP_TRY(hipEventRecord(gp.ev1, r0.stream));
+    HIP_TRY(hipEventRecord(gp.ev_out, r0.stream));
+    HIP_TRY(hipStreamWaitEvent(st0, gp.ev_out, 0));
+    order_on(r0, st0);  // later single-device launches on the first device follow the group
+}
+
 }  // namespace
 
 extern "C" {
@@ -544,6 +802,15 @@ int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {
             for (auto& r : s->reps) have |= r->device == devices[q];
             if (!have) upload_one(s, devices[q]);
         }
+        // more than one device: a fresh communicator over all of them (rank g =
+        // the g-th uploaded device, the shard order of rt_render_batch_multi)
+        if (s->reps.size() > 1 && s->grp.comms.size() != s->reps.size()) {
+            free_group(s);
+            std::vector<int> devs;
+            for (auto& r : s->reps) devs.push_back(r->device);
+            s->grp.comms.resize(devs.size());
+            NCCL_TRY(rccl().init_all(s->grp.comms.data(), (int)devs.size(), devs.data()));
+        }
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
@@ -573,48 +840,36 @@ int rt_render_batch_spp_device(rt_scene* s, int device, const rt_camera* cams, i
         std::lock_guard<std::mutex> lk(s->mu);
         Replica* r = &replica_for(s, device);
         DevGuard g(device);
-        hipStream_t st = (hipStream_t)stream;
-        const uint64_t fpix = (uint64_t)cam->width * (uint64_t)nrows;  // pixels per frame
-        // poses per launch: the batch's sample-frame limit, and batch pixels
-        // < 2^31 (redo-list entries)
-        int per = std::max(1, batch_frames() / spp);
-        while (per > 1 && fpix * (uint64_t)(per * spp) >= (1ull << 31)) per--;
-        if (fpix * (uint64_t)spp >= (1ull << 31)) return fail(RT_ERR_INVALID_ARGUMENT, "image too large for spp");
-        const bool split = mode == RT_MODE_EXACT && rt::packet_split(spp);
-        if (split) {
-            // candidate lists in HBM (73 B per sample pixel): at most half of
-            // the device memory that is free (or already ours), fewer poses
-            // per launch otherwise
-            size_t mfree = 0, mtotal = 0;
-            HIP_TRY(hipMemGetInfo(&mfree, &mtotal));
-            const uint64_t avail = (uint64_t)mfree + r->cand_cap * kCandBytesPerPixel;
-            while (per > 1 && fpix * (uint64_t)(per * spp) * kCandBytesPerPixel > avail / 2) per--;
-            ensure_cand(*r, fpix * (uint64_t)(std::min(per, nframes) * spp));
+        render_batch_locked(s, *r, cams, nframes, spp, mode, row0, row_stride, nrows, out, (hipStream_t)stream, flags);
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
+int rt_render_batch_multi(rt_scene* s, const rt_camera* cams, int nframes, int spp, int mode, const rt_device_out* out,
+                          void* stream, uint32_t flags) {
+    if (!s || !out || (nframes > 0 && !cams)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (nframes < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative frame count");
+    if (nframes > 1024) return fail(RT_ERR_INVALID_ARGUMENT, "at most 1024 poses per call");
+    if (spp < 1 || spp > RT_MAX_BATCH || spp_grid(spp) * spp_grid(spp) != spp)
+        return fail(RT_ERR_INVALID_ARGUMENT, "spp must be n*n samples (1, 4, 9 or 16)");
+    if (mode != RT_MODE_EXACT && mode != RT_MODE_FP64) return fail(RT_ERR_INVALID_ARGUMENT, "bad mode");
+    try {
+        for (int f = 0; f < nframes; f++) {
+            check_camera(s, &cams[f]);
+            if (cams[f].width != cams[0].width || cams[f].height != cams[0].height)
+                return fail(RT_ERR_INVALID_ARGUMENT, "frames of a batch must share the image size");
         }
-        ensure_redo(*r, fpix * (uint64_t)std::min(per, nframes));
-        // serialise on the replica's stream: the caller's stream waits for it
-        order_on(*r, st);
-        for (int f0 = 0; f0 < nframes; f0 += per) {
-            const int n = std::min(per, nframes - f0);
-            RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows, spp);
-            const uint64_t off = (uint64_t)f0 * fpix, soff = off * (uint64_t)spp;
-            fp.hit_id = out->hit_id ? out->hit_id + soff : nullptr;
-            fp.dist = out->dist ? out->dist + soff : nullptr;
-            fp.hit_pos = out->pos ? out->pos + 3 * soff : nullptr;
-            fp.rgb = out->rgb ? out->rgb + 3 * off : nullptr;
-            fp.hit_count = out->hit_count ? out->hit_count + f0 : nullptr;
-            fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
-            const hipEvent_t* tev = nullptr;
-            if (flags & RT_FLAG_TIMING) {
-                if (r->tev_used == r->tev.size()) {
-                    std::array<hipEvent_t, 2> a{};
-                    for (auto& e : a) HIP_TRY(hipEventCreate(&e));
-                    r->tev.push_back(a);
-                }
-                tev = r->tev[r->tev_used++].data();
-            }
-            launch(s, *r, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, tev);
-        }
+        if (nframes == 0) return RT_OK;
+        std::lock_guard<std::mutex> lk(s->mu);
+        if (s->reps.empty()) return fail(RT_ERR_NO_DEVICE, "scene not uploaded");
+        Replica& r0 = *s->reps.front();
+        DevGuard g(r0.device);
+        if (group_shards(s) == 1)
+            render_batch_locked(s, r0, cams, nframes, spp, mode, 0, 1, cams[0].height, out, (hipStream_t)stream, flags);
+        else
+            render_group(s, cams, nframes, spp, mode, out, (hipStream_t)stream, flags);
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
@@ -718,12 +973,22 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         fp.hit_pos = d.pos;
         fp.rgb = d.rgb;
         fp.hit_count = d.hit_count;
-        ensure_redo(r, npx);
-        if (mode == RT_MODE_EXACT && rt::packet_split(1)) ensure_cand(r, npx);
-        order_on(r, r.stream);
-        HIP_TRY(hipEventRecord(r.ev0, r.stream));
-        launch(s, r, fp, mode, false, r.stream, nullptr);
-        HIP_TRY(hipEventRecord(r.ev1, r.stream));
+        hipEvent_t e0 = r.ev0, e1 = r.ev1;
+        if (group_shards(s) > 1) {
+            // every uploaded device renders its interleaved rows; the frame
+            // is gathered and de-interleaved on the first device (the device
+            // time is the group's, first device's stream: renders to gather)
+            render_group(s, cam, 1, 1, mode, &d, r.stream, 0);
+            e0 = s->grp.ev0;
+            e1 = s->grp.ev1;
+        } else {
+            ensure_redo(r, npx);
+            if (mode == RT_MODE_EXACT && rt::packet_split(1)) ensure_cand(r, npx);
+            order_on(r, r.stream);
+            HIP_TRY(hipEventRecord(r.ev0, r.stream));
+            launch(s, r, fp, mode, false, r.stream, nullptr);
+            HIP_TRY(hipEventRecord(r.ev1, r.stream));
+        }
         if (out->hit_id) HIP_TRY(hipMemcpyAsync(out->hit_id, d.hit_id, npx * 4, hipMemcpyDeviceToHost, r.stream));
         if (out->dist) HIP_TRY(hipMemcpyAsync(out->dist, d.dist, npx * 8, hipMemcpyDeviceToHost, r.stream));
         if (out->pos) HIP_TRY(hipMemcpyAsync(out->pos, d.pos, npx * 24, hipMemcpyDeviceToHost, r.stream));
@@ -732,13 +997,28 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         HIP_TRY(hipMemcpyAsync(&hc, d.hit_count, 8, hipMemcpyDeviceToHost, r.stream));
         HIP_TRY(hipStreamSynchronize(r.stream));
         float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, r.ev0, r.ev1));
+        HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
         out->hit_count = hc;
         out->seconds = ms * 1e-3;
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
     }
+}
+
+int rt_deinterleave_rows(const void* gathered, uint64_t block_bytes, uint64_t section_offset, int shards, int frames,
+                         int height, int width, int elem_bytes, void* frames_out) {
+    if (!gathered || !frames_out || shards < 1 || frames < 0 || height < 0 || width < 0 || elem_bytes < 1)
+        return fail(RT_ERR_INVALID_ARGUMENT, "bad de-interleave arguments");
+    const int R = rt_shard_pad(height, shards);
+    const uint64_t n = (uint64_t)width * elem_bytes;
+    for (int f = 0; f < frames; f++)
+        for (int j = 0; j < height; j++)
+            std::memcpy(static_cast<uint8_t*>(frames_out) + ((uint64_t)f * height + j) * n,
+                        static_cast<const uint8_t*>(gathered) +
+                            rt_gathered_row(j, f, shards, R, width, elem_bytes, block_bytes, section_offset),
+                        n);
+    return RT_OK;
 }
 
 int rt_diag_raw(rt_scene* s, int device, uint64_t* out, size_t n) {
@@ -837,6 +1117,7 @@ int rt_scene_tree_dump(const rt_scene* s, double* boxes, int64_t* meta, int64_t*
 
 void rt_scene_destroy(rt_scene* s) {
     if (!s) return;
+    free_group(s);
     for (auto& r : s->reps) free_replica(*r);
     delete s;
 }

@@ -71,6 +71,24 @@
 // tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
 #define RT_TRI32_PAD 4
 
+#if defined(__HIPCC__)
+#define RT_HD __host__ __device__
+#else
+#define RT_HD
+#endif
+// Row-interleaved image shards (multi-device frames, rt_render_batch_multi;
+// SURVEY.md §8(e)): shard g of G holds image rows g, g + G, g + 2G, ...; every
+// shard's block is padded to rt_shard_pad(H, G) rows so the gathered blocks
+// have one size.  Image row j of a frame is row j / G of shard j % G.
+static inline RT_HD int rt_shard_rows(int H, int G, int g) { return g < H ? (H - 1 - g) / G + 1 : 0; }
+static inline RT_HD int rt_shard_pad(int H, int G) { return (H + G - 1) / G; }
+// byte offset of image row j of frame f inside the gathered [G][block] buffer
+// (section at sec_off of each block: [F][R][W] elements of eb bytes)
+static inline RT_HD uint64_t rt_gathered_row(int j, int f, int G, int R, int W, int eb, uint64_t block,
+                                             uint64_t sec_off) {
+    return (uint64_t)(j % G) * block + sec_off + ((uint64_t)f * (uint64_t)R + (uint64_t)(j / G)) * (uint64_t)W * eb;
+}
+
 #ifdef __cplusplus
 static inline constexpr uint32_t rt_node_bytes(int W) { return (uint32_t)(32 * W); }
 static inline constexpr uint32_t rt_make_leaf(uint32_t first, uint32_t count) {

@@ -18,8 +18,13 @@
 // generation + traversal + resolve + shading of the frame (rt_frame_out.seconds);
 // the reference timed calculateScreen on one CPU core.
 //
+// Multi-GPU: --devices 0,1,...,N-1 uploads the scene to every listed device;
+// rt_render_frame then interleaves image rows over them and gathers the frame
+// to the first device with RCCL (include/rt.h), unchanged for this caller.
+//
 // Usage: rtdemo [--objects DIR] [--out DIR] [--reps N] [--algos a-k,...]
 //               [--models name,...] [--frames N] [--size W] [--device D]
+//               [--devices D0,D1,...]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -95,7 +100,7 @@ struct Config {
     int reps = 10;
     int frames = 36;
     int size = 500;
-    int device = 0;
+    std::vector<int> devices{0};
     std::vector<std::pair<std::string, int>> algos;
     std::vector<std::pair<std::string, double>> models;
 };
@@ -141,7 +146,7 @@ void run_test(const Config& cfg, const std::string& model, double scale, const s
         bm.save_data_frame("bvh_build_times.csv", model, scale, full, cam, s);
         std::printf("Time build BVH using %s Split: %f \n", full.c_str(), s);
     }
-    check(rt_scene_upload(scene, &cfg.device, 1));
+    check(rt_scene_upload(scene, cfg.devices.data(), (int)cfg.devices.size()));
 
     const int W = cfg.size, H = cfg.size;
     std::vector<uint8_t> rgb((size_t)W * H * 3);
@@ -191,7 +196,11 @@ int main(int argc, char** argv) {
         else if (k == "--reps") cfg.reps = std::stoi(val());
         else if (k == "--frames") cfg.frames = std::stoi(val());
         else if (k == "--size") cfg.size = std::stoi(val());
-        else if (k == "--device") cfg.device = std::stoi(val());
+        else if (k == "--device") cfg.devices = {std::stoi(val())};
+        else if (k == "--devices") {
+            cfg.devices.clear();
+            for (const auto& t : split(val())) cfg.devices.push_back(std::stoi(t));
+        }
         else if (k == "--algos") {
             cfg.algos.clear();
             for (const auto& t : split(val())) {

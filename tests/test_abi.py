@@ -111,3 +111,26 @@ def test_batch_render_rejects_mixed_sizes_and_needs_a_device():
     assert L.rt_render_batch_device(s.handle, 0, cams, -1, N.RT_MODE_EXACT, 0, 1, 8, C.byref(o), None, 0) \
         == N.RT_ERR_INVALID_ARGUMENT
     assert np.isfinite(s.tris).all()
+
+
+@pytest.mark.parametrize("G,F,H,W,eb", [(1, 2, 5, 3, 4), (2, 3, 7, 5, 3), (3, 2, 1080, 16, 8), (8, 1, 1081, 9, 24),
+                                        (5, 4, 3, 2, 1)])
+def test_deinterleave_rows_matches_row_interleaving(G, F, H, W, eb):
+    """rt_deinterleave_rows (the host twin of the device kernel that
+    rt_render_batch_multi runs after the RCCL gather): shard g holds image
+    rows g, g + G, ... of every frame, padded to ceil(H / G) rows; the
+    de-interleave puts row j of frame f back from shard j % G, row j // G."""
+    import numpy as np
+    import raytracingdemo_amd as rt
+    rng = np.random.default_rng(G * 1000 + H)
+    frames = rng.integers(0, 256, size=(F, H, W * eb), dtype=np.uint8)
+    R = -(-H // G)
+    sec_off, pad = 256, 64  # a section inside each block, as the library lays it out
+    block = sec_off + F * R * W * eb + pad
+    gathered = rng.integers(0, 256, size=(G, block), dtype=np.uint8)  # padding rows stay garbage
+    for g in range(G):
+        rows = frames[:, g::G]  # [F, rows_g, W*eb]
+        sec = gathered[g, sec_off:sec_off + F * R * W * eb].reshape(F, R, W * eb)
+        sec[:, :rows.shape[1]] = rows
+    out = rt.deinterleave_rows(gathered, G, F, H, W, eb, block_bytes=block, section_offset=sec_off)
+    assert np.array_equal(out, frames)

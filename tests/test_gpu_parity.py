@@ -492,3 +492,42 @@ def test_errors_fail_loudly():
     s = rt.Scene(golden_scene("teapot.obj"), "bsah", 2)
     with pytest.raises(rt.RTError, match="not uploaded"):
         s.calculate_screen([0, 0, 5], [0, 0, -1], 8, 8)
+
+
+@pytest.mark.parametrize("shards", [1, 2, 3, 8])
+def test_sharded_frames_through_the_abi_equal_one_device(monkeypatch, shards):
+    """rt_render_batch_multi / rt_render_frame shard image rows over the uploaded
+    devices, gather the shards to the first device and de-interleave them there
+    (RCCL between distinct devices).  RT_VIRTUAL_SHARDS runs the same shard,
+    gather-layout, de-interleave and hit-count code on one device (device copies
+    in place of RCCL): outputs equal the unsharded render bit for bit."""
+    torch = pytest.importorskip("torch")
+    tris = golden_scene("stanford-bunny.obj")
+    s = scene("stanford-bunny.obj", "bsah", 8)
+    path = rt.CameraPath(rt.scene_center(tris), 36)
+    cams = [path.circular_path(f) for f in (0, 5, 11, 23, 30)]
+    W, H, F = 203, 117, 5
+    ref = {}
+    for key, dt, per in (("id", torch.int32, 1), ("dist", torch.float64, 1), ("pos", torch.float64, 3),
+                         ("rgb", torch.uint8, 3)):
+        ref[key] = torch.empty(F * H * W * per, dtype=dt, device="cuda:0")
+    ref_cnt = torch.zeros(F, dtype=torch.int64, device="cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    s.render_batch_device(0, cams, W, H, 0, 1, H, hit_id=ref["id"].data_ptr(), dist=ref["dist"].data_ptr(),
+                          hit_pos=ref["pos"].data_ptr(), rgb=ref["rgb"].data_ptr(), hit_count=ref_cnt.data_ptr(),
+                          stream=st)
+    monkeypatch.setenv("RT_VIRTUAL_SHARDS", str(shards))
+    got = {k: torch.full_like(v, 7) for k, v in ref.items()}
+    cnt = torch.zeros(F, dtype=torch.int64, device="cuda:0")
+    s.render_batch_multi(cams, W, H, hit_id=got["id"].data_ptr(), dist=got["dist"].data_ptr(),
+                         hit_pos=got["pos"].data_ptr(), rgb=got["rgb"].data_ptr(), hit_count=cnt.data_ptr(), stream=st)
+    torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), (shards, k)
+    assert torch.equal(cnt, ref_cnt)
+    # the blocking host-buffer frame call takes the same path
+    p, d = cams[2]
+    g = s.calculate_screen(p, d, W, H)
+    assert np.array_equal(g["hit_id"], ref["id"].cpu().numpy().view(np.uint32).reshape(F, -1)[2])
+    assert np.array_equal(g["rgb"].reshape(-1), ref["rgb"].cpu().numpy().reshape(F, -1)[2])
+    assert g["hits"] == int(ref_cnt[2])

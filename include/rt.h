@@ -187,10 +187,10 @@ int rt_render_batch_multi(rt_scene *s, const rt_camera *cams, int nframes, int s
 
 /* The de-interleave of rt_render_batch_multi on the host (the same index
  * arithmetic as the device kernel; for tests and host-side gathers):
- * `gathered` holds `shards` blocks of block_bytes; each block's section at
- * section_offset is [frames][rt_shard_pad rows][width] elements of
- * elem_bytes, shard g holding image rows g, g + shards, ...; writes
- * frames_out[frames][height][width] elements. */
+ * `gathered` holds `shards` blocks of block_bytes; shard g's block holds at
+ * section_offset its frames back to back, [frames][rows_g][width] elements
+ * of elem_bytes, rows_g = the image rows g, g + shards, ... below height;
+ * writes frames_out[frames][height][width] elements. */
 int rt_deinterleave_rows(const void *gathered, uint64_t block_bytes, uint64_t section_offset, int shards, int frames,
                          int height, int width, int elem_bytes, void *frames_out);
 

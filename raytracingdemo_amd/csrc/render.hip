@@ -936,12 +936,12 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 // row's W * eb bytes from its shard (rt_gathered_row), in words when both
 // sides allow it.
 __global__ void __launch_bounds__(256) k_deinterleave(const uint8_t* __restrict__ gather, uint64_t block,
-                                                      uint64_t sec_off, int G, int F, int H, int W, int R, int eb,
+                                                      uint64_t sec_off, int G, int F, int H, int W, int eb,
                                                       uint8_t* __restrict__ dst) {
     const int f = (int)(blockIdx.x / (unsigned)H), j = (int)(blockIdx.x % (unsigned)H);
     if (f >= F) return;
     const uint64_t n = (uint64_t)W * eb;
-    const uint8_t* src = gather + rt_gathered_row(j, f, G, R, W, eb, block, sec_off);
+    const uint8_t* src = gather + rt_gathered_row(j, f, G, H, W, eb, block, sec_off);
     uint8_t* d = dst + ((uint64_t)f * H + j) * n;
     if (((uintptr_t)src | (uintptr_t)d | n) % 4 == 0) {
         const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
@@ -967,7 +967,7 @@ hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_
                                int eb, void* dst, hipStream_t s) {
     if (F <= 0 || H <= 0 || W <= 0 || G <= 0 || eb <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)((uint64_t)F * H)), dim3(256), 0, s,
-                       static_cast<const uint8_t*>(gather), block, sec_off, G, F, H, W, rt_shard_pad(H, G), eb,
+                       static_cast<const uint8_t*>(gather), block, sec_off, G, F, H, W, eb,
                        static_cast<uint8_t*>(dst));
     return hipGetLastError();
 }

@@ -1010,13 +1010,12 @@ int rt_deinterleave_rows(const void* gathered, uint64_t block_bytes, uint64_t se
                          int height, int width, int elem_bytes, void* frames_out) {
     if (!gathered || !frames_out || shards < 1 || frames < 0 || height < 0 || width < 0 || elem_bytes < 1)
         return fail(RT_ERR_INVALID_ARGUMENT, "bad de-interleave arguments");
-    const int R = rt_shard_pad(height, shards);
     const uint64_t n = (uint64_t)width * elem_bytes;
     for (int f = 0; f < frames; f++)
         for (int j = 0; j < height; j++)
             std::memcpy(static_cast<uint8_t*>(frames_out) + ((uint64_t)f * height + j) * n,
                         static_cast<const uint8_t*>(gathered) +
-                            rt_gathered_row(j, f, shards, R, width, elem_bytes, block_bytes, section_offset),
+                            rt_gathered_row(j, f, shards, height, width, elem_bytes, block_bytes, section_offset),
                         n);
     return RT_OK;
 }

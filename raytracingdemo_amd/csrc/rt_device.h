@@ -77,16 +77,20 @@
 #define RT_HD
 #endif
 // Row-interleaved image shards (multi-device frames, rt_render_batch_multi;
-// SURVEY.md §8(e)): shard g of G holds image rows g, g + G, g + 2G, ...; every
-// shard's block is padded to rt_shard_pad(H, G) rows so the gathered blocks
-// have one size.  Image row j of a frame is row j / G of shard j % G.
+// SURVEY.md §8(e)): shard g of G holds image rows g, g + G, g + 2G, ...
+// (rt_shard_rows of them).  Its block holds, per output section, the shard's
+// frames back to back ([F][rows][W] elements, as the row-shard render writes
+// them); blocks are sized for rt_shard_pad(H, G) rows so all have one size.
+// Image row j of frame f is row j / G of frame f in shard j % G.
 static inline RT_HD int rt_shard_rows(int H, int G, int g) { return g < H ? (H - 1 - g) / G + 1 : 0; }
 static inline RT_HD int rt_shard_pad(int H, int G) { return (H + G - 1) / G; }
 // byte offset of image row j of frame f inside the gathered [G][block] buffer
-// (section at sec_off of each block: [F][R][W] elements of eb bytes)
-static inline RT_HD uint64_t rt_gathered_row(int j, int f, int G, int R, int W, int eb, uint64_t block,
+// (section at sec_off of each block, elements of eb bytes)
+static inline RT_HD uint64_t rt_gathered_row(int j, int f, int G, int H, int W, int eb, uint64_t block,
                                              uint64_t sec_off) {
-    return (uint64_t)(j % G) * block + sec_off + ((uint64_t)f * (uint64_t)R + (uint64_t)(j / G)) * (uint64_t)W * eb;
+    const int g = j % G;
+    return (uint64_t)g * block + sec_off +
+           ((uint64_t)f * (uint64_t)rt_shard_rows(H, G, g) + (uint64_t)(j / G)) * (uint64_t)W * eb;
 }
 
 #ifdef __cplusplus

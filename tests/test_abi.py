@@ -118,19 +118,20 @@ def test_batch_render_rejects_mixed_sizes_and_needs_a_device():
 def test_deinterleave_rows_matches_row_interleaving(G, F, H, W, eb):
     """rt_deinterleave_rows (the host twin of the device kernel that
     rt_render_batch_multi runs after the RCCL gather): shard g holds image
-    rows g, g + G, ... of every frame, padded to ceil(H / G) rows; the
-    de-interleave puts row j of frame f back from shard j % G, row j // G."""
+    rows g, g + G, ... of every frame; the
+    de-interleave puts row j of frame f back from shard j % G, row j // G
+    (each shard's frames back to back in its block, as its row-shard render
+    wrote them)."""
     import numpy as np
     import raytracingdemo_amd as rt
     rng = np.random.default_rng(G * 1000 + H)
     frames = rng.integers(0, 256, size=(F, H, W * eb), dtype=np.uint8)
     R = -(-H // G)
     sec_off, pad = 256, 64  # a section inside each block, as the library lays it out
-    block = sec_off + F * R * W * eb + pad
-    gathered = rng.integers(0, 256, size=(G, block), dtype=np.uint8)  # padding rows stay garbage
+    block = sec_off + F * R * W * eb + pad  # sized for the tallest shard
+    gathered = rng.integers(0, 256, size=(G, block), dtype=np.uint8)  # the unused tail stays garbage
     for g in range(G):
-        rows = frames[:, g::G]  # [F, rows_g, W*eb]
-        sec = gathered[g, sec_off:sec_off + F * R * W * eb].reshape(F, R, W * eb)
-        sec[:, :rows.shape[1]] = rows
+        rows = np.ascontiguousarray(frames[:, g::G]).reshape(-1)  # [F, rows_g, W*eb], frames back to back
+        gathered[g, sec_off:sec_off + len(rows)] = rows
     out = rt.deinterleave_rows(gathered, G, F, H, W, eb, block_bytes=block, section_offset=sec_off)
     assert np.array_equal(out, frames)

@@ -14,15 +14,24 @@ Usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV KEY_FILE OUT_JSON
 """
 import collections
 import csv
+import re
 import json
 import sys
+
+
+
+def counting(name):
+    """k_trace_packet<W, SP, K, COUNT, FUSED>: the COUNT instantiation is the
+    counting pass, not the timed kernel."""
+    m = re.search(r"k_trace_packet<\d+, \d+, \d+, (true|false)", name)
+    return bool(m and m.group(1) == "true")
 
 
 def per_dispatch(path, kernel_sub):
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        if kernel_sub not in name or "true>" in name:  # skip the counting variant
+        if kernel_sub not in name or counting(name):  # skip the counting variant
             continue
         vals[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
     return vals

@@ -13,8 +13,17 @@ Usage: tools/pmc_valu.py KEY_FILE OUT_JSON SQ_CSV [SQ_CSV ...]
 """
 import collections
 import csv
+import re
 import json
 import sys
+
+
+
+def counting(name):
+    """k_trace_packet<W, SP, K, COUNT, FUSED>: the COUNT instantiation is the
+    counting pass, not the timed kernel."""
+    m = re.search(r"k_trace_packet<\d+, \d+, \d+, (true|false)", name)
+    return bool(m and m.group(1) == "true")
 
 
 def main():
@@ -24,7 +33,7 @@ def main():
     for path in sys.argv[3:]:
         for r in csv.DictReader(open(path)):
             n = r["Kernel_Name"]
-            if "k_trace_packet" not in n or "true>" in n:
+            if "k_trace_packet" not in n or counting(n):
                 continue
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
             disp[r["Counter_Name"]].add((path, r["Dispatch_Id"]))

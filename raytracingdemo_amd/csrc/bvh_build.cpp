@@ -402,22 +402,35 @@ struct Flattener {
             if (n.first > RT_LEAF_MAX_FIRST) throw Error{RT_ERR_INVALID_ARGUMENT, "scene too large"};
             return rt_make_leaf(n.first, n.count);
         }
+        const uint32_t id = alloc_node();
+        walk_fill(w, b, id, depth);
+        return id;
+    }
+
+    // Fills wide node `id` from walk node b.  The wide nodes of its inner
+    // children are allocated together before any of their subtrees, so
+    // siblings are adjacent and the top levels form a prefix of the array
+    // (the root is node 0, its inner children nodes 1..k).
+    void walk_fill(const WalkTree& w, int32_t b, uint32_t id, uint32_t depth) {
+        const WalkNode& n = w.nodes[b];
         std::vector<int32_t> kids = collapse_children(w, b, W);
         const int axis = longest_axis(n.mn, n.mx);
         std::stable_sort(kids.begin(), kids.end(), [&](int32_t x, int32_t y) {
             return w.nodes[x].mn[axis] + w.nodes[x].mx[axis] < w.nodes[y].mn[axis] + w.nodes[y].mx[axis];
         });
-        const uint32_t id = alloc_node();
         wide_depth = std::max(wide_depth, depth + 1);
+        std::vector<uint32_t> refs(kids.size());
+        for (size_t c = 0; c < kids.size(); c++)
+            refs[c] = w.nodes[kids[c]].left < 0 ? walk_ref(w, kids[c], depth + 1) : alloc_node();
         for (size_t c = 0; c < kids.size(); c++) {
             float b6[6];
             box32(w.nodes[kids[c]].mn, w.nodes[kids[c]].mx, b6);
-            const uint32_t r = walk_ref(w, kids[c], depth + 1);
-            set_slot(id, (int)c, b6, r);
+            set_slot(id, (int)c, b6, refs[c]);
         }
         uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + (size_t)id * nb);
         p[7] = (uint32_t)axis | ((uint32_t)kids.size() << 2);
-        return id;
+        for (size_t c = 0; c < kids.size(); c++)
+            if (w.nodes[kids[c]].left >= 0) walk_fill(w, kids[c], refs[c], depth + 1);
     }
 
     uint32_t emit_inner(const std::vector<int32_t>& kids, uint32_t depth) {

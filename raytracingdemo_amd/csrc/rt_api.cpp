@@ -301,6 +301,7 @@ void upload_one(rt_scene* s, int device) {
     d.width = f.width;
     d.stack_bound = f.stack_bound;
     d.coord_max = f.coord_max;
+    d.n_wide = (uint32_t)f.n_wide;
     HIP_TRY(hipMalloc(&r.d_counters, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipMemset(r.d_counters, 0, kCounterWords * sizeof(unsigned long long)));
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));

@@ -132,6 +132,8 @@ struct RtDevScene {
     int32_t width;
     uint32_t stack_bound;
     double coord_max;             // max |coordinate| of the scene (slab margins of arbitrary rays)
+    uint32_t n_wide;              // wide nodes
+    uint32_t reserved;
 };
 
 // Per-launch resources of the persistent exact kernel.

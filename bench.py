@@ -297,14 +297,27 @@ def main():
         tris, label = sc
     else:
         tris, label = sponza_scene()
+    # the scene: reference tree on the host, walk tree built on this GPU
+    # (rt_scene_create_on_device), then the replica upload; the stage times
+    # are the reference's dynamic-scene metric (build + traversal,
+    # scripts/bvh_analysis.py:62,543) next to the host walk-tree build
     t_build = time.perf_counter()
-    scene = rt.Scene(tris, a.algo, a.k)
+    scene = rt.Scene(tris, a.algo, a.k, walk_device=local)
     t_upload = time.perf_counter()
     scene.upload([local])
     torch.cuda.synchronize(dev)
     t_ready = time.perf_counter()
+    bt = scene.build_times()
     build_ms = {"scene_create_ms": round((t_upload - t_build) * 1e3, 1),
+                "reference_tree_ms": round(bt["reference_tree_ms"], 1),
+                "walk_tree_device_ms": round(bt["walk_tree_ms"], 1),
+                "flatten_ms": round(bt["flatten_ms"], 1), "soup_ms": round(bt["soup_ms"], 1),
                 "upload_ms": round((t_ready - t_upload) * 1e3, 1)}
+    if world == 1 and not a.paths:
+        hb = rt.Scene(tris, a.algo, a.k).build_times()
+        build_ms["walk_tree_host_ms"] = round(hb["walk_tree_ms"], 1)
+        build_ms["scene_create_host_walk_ms"] = round(sum(hb[k] for k in ("soup_ms", "reference_tree_ms",
+                                                                          "walk_tree_ms", "flatten_ms")), 1)
     if a.paths:
         return run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse)
     st = scene.stats()

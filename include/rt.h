@@ -131,6 +131,16 @@ typedef struct {
                                   recorded around it on the launch stream) */
 } rt_frame_stats_t;
 
+/* Host time of each stage of rt_scene_create (std::chrono, ms). */
+typedef struct {
+    double soup_ms;           /* triangle set-up (triangle.hpp:14-19)                 */
+    double reference_tree_ms; /* StackBVH::build + collapse (stack_bvh.hpp:502-608)   */
+    double walk_tree_ms;      /* the SAH walk tree: host, or device build + copy back */
+    double flatten_ms;        /* wide nodes, records, ranks and chains                */
+    int32_t walk_device;      /* device that built the walk tree, -1 = host           */
+    int32_t reserved;
+} rt_build_times_t;
+
 /* objl::Loader + ObjectLoader::loadFromFile (object_loader.hpp:14-70,
  * lib/OBJ_Loader.h:431-713): N*9 doubles (v0,v1,v2), loader order, each
  * coordinate double(float) * scale.  *tris is malloc'd; free with rt_free. */
@@ -157,6 +167,19 @@ int rt_camera_path(const double scene_center[3], int resolution, int step, doubl
  * 219-221).  algo = RT_ALGO_*, k in {2,4,8,16}.  The tree is identical to the
  * reference's.  The scene is host-only until rt_scene_upload. */
 int rt_scene_create(const double *tri_v, uint64_t n_tris, int algo, int k, int collapse, rt_scene **out);
+
+/* rt_scene_create with the walk tree (the SAH tree the device traverses,
+ * DESIGN.md §3) built on HIP device `device` (the
+ * reference times StackBVH::build as its dynamic-scene metric,
+ * scripts/bvh_analysis.py:62,543).  The splits are the host builder's; only
+ * the order of triangles inside a node may differ, which never changes a
+ * result.  The reference tree itself stays a host build: it fixes the tie
+ * ranks and ancestor chains and its libstdc++ partition order. */
+int rt_scene_create_on_device(const double *tri_v, uint64_t n_tris, int algo, int k, int collapse, int device,
+                              rt_scene **out);
+
+/* Stage times of the scene's creation. */
+int rt_scene_build_times(const rt_scene *s, rt_build_times_t *out);
 
 /* Replicate the flattened scene on each listed HIP device (ordinal).  With
  * more than one device the library also creates an RCCL communicator over

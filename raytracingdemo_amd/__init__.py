@@ -124,13 +124,19 @@ def _camera(pos, d, W, H) -> N.rt_camera:
 class Scene:
     """A scene built into the reference's BVH and flattened for gfx950."""
 
-    def __init__(self, tris: np.ndarray, algorithm: str = "bsah", k: int = 8):
+    def __init__(self, tris: np.ndarray, algorithm: str = "bsah", k: int = 8, walk_device: int | None = None):
+        """walk_device: build the walk tree on that HIP device (rt_scene_create_on_device)
+        instead of the host."""
         algo, collapse = parse_algorithm(algorithm)
         self.tris = np.ascontiguousarray(tris, dtype=np.float64).reshape(-1, 9)
         self.algorithm, self.k = algorithm, int(k)
         h = C.c_void_p()
-        N.check(N.lib().rt_scene_create(self.tris.ctypes.data, len(self.tris), algo, int(k), int(collapse),
-                                        C.byref(h)))
+        if walk_device is None:
+            N.check(N.lib().rt_scene_create(self.tris.ctypes.data, len(self.tris), algo, int(k), int(collapse),
+                                            C.byref(h)))
+        else:
+            N.check(N.lib().rt_scene_create_on_device(self.tris.ctypes.data, len(self.tris), algo, int(k),
+                                                      int(collapse), int(walk_device), C.byref(h)))
         self._h = h
         self.devices: list[int] = []
 
@@ -154,6 +160,12 @@ class Scene:
         N.check(N.lib().rt_scene_upload(self._h, devs, len(devices)))
         self.devices = list(devices)
         return self
+
+    def build_times(self) -> dict:
+        """Stage times of the scene's creation (include/rt.h rt_scene_build_times)."""
+        t = N.rt_build_times_t()
+        N.check(N.lib().rt_scene_build_times(self._h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in t._fields_ if f != "reserved"}
 
     def stats(self) -> dict:
         s = N.rt_scene_stats_t()

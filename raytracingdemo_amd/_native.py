@@ -34,7 +34,7 @@ EXPORTS = [
     "rt_load_obj", "rt_load_obj_cached", "rt_free", "rt_scene_center", "rt_camera_path", "rt_scene_create", "rt_scene_upload",
     "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_render_paths_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
     "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
-    "rt_render_batch_multi", "rt_deinterleave_rows",
+    "rt_render_batch_multi", "rt_deinterleave_rows", "rt_scene_create_on_device", "rt_scene_build_times",
 ]
 
 
@@ -76,6 +76,11 @@ class rt_frame_stats_t(C.Structure):
                 ("wave_tiles", C.c_uint64), ("wave_tris", C.c_uint64), ("redo_rays", C.c_uint64), ("redo_chain", C.c_uint64),
                 ("spilled_rays", C.c_uint64), ("dropped_rays", C.c_uint64), ("empty_node_steps", C.c_uint64),
                 ("reserved", C.c_uint64 * 9), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
+
+
+class rt_build_times_t(C.Structure):
+    _fields_ = [("soup_ms", C.c_double), ("reference_tree_ms", C.c_double), ("walk_tree_ms", C.c_double),
+                ("flatten_ms", C.c_double), ("walk_device", C.c_int32), ("reserved", C.c_int32)]
 
 
 _lib = None
@@ -122,6 +127,9 @@ def lib() -> C.CDLL:
     L.rt_scene_center.argtypes = [C.c_void_p, C.c_uint64, dp]
     L.rt_camera_path.argtypes = [dp, C.c_int, C.c_int, dp, dp]
     L.rt_scene_create.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.rt_scene_create_on_device.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             C.POINTER(C.c_void_p)]
+    L.rt_scene_build_times.argtypes = [C.c_void_p, C.POINTER(rt_build_times_t)]
     L.rt_scene_upload.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
     L.rt_render_frame.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.POINTER(rt_frame_out)]
     L.rt_render_rows_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,

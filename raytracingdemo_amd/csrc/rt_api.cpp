@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -138,6 +139,7 @@ struct rt_scene {
     std::mutex mu;
     uint32_t literal_stack = 0;  // stack bound of the literal (reference-order) traversal
     Group grp;
+    rt_build_times_t times{};    // rt_scene_build_times
 };
 
 namespace {
@@ -762,26 +764,51 @@ int rt_camera_path(const double c[3], int res, int step, double pos[3], double d
     return RT_OK;
 }
 
-int rt_scene_create(const double* tri_v, uint64_t n, int algo, int k, int collapse, rt_scene** out) {
+// rt_scene_create / rt_scene_create_on_device: walk_device < 0 builds the
+// walk tree on the host (walk_tree.cpp), else on that HIP device (walk_build.hip).
+static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int collapse, int walk_device,
+                        rt_scene** out) {
     if (!out || (n && !tri_v)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     *out = nullptr;
     if (algo < 0 || algo > 2) return fail(RT_ERR_OUT_OF_RANGE, "Unknown algorithm");
     if (!(k == 2 || k == 4 || k == 8 || k == 16)) return fail(RT_ERR_INVALID_ARGUMENT, "Unsupported bvh degree");
     if (n > RT_LEAF_MAX_FIRST) return fail(RT_ERR_INVALID_ARGUMENT, "too many triangles");
     try {
+        using clk = std::chrono::steady_clock;
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         std::unique_ptr<rt_scene> s(new rt_scene);
+        const auto t0 = clk::now();
         s->soup = rt::make_soup(tri_v, n);
+        const auto t1 = clk::now();
         s->tree = rt::build_tree(s->soup, algo, k, collapse);
+        const auto t2 = clk::now();
+        auto t3 = t2;
         // the device walks a rebuilt SAH tree (walk_tree.cpp) unless
         // RT_WALK=reference asks for the reference tree's own nodes
         const char* wk = std::getenv("RT_WALK");
+        s->times.walk_device = -1;
         if (wk && wk[0] == 'r') {
             s->flat = rt::flatten(s->soup, s->tree, 0);
         } else {
-            const rt::WalkTree wt = rt::build_walk_tree(s->soup);
+            rt::WalkTree wt;
+            if (walk_device >= 0) {
+                int count = 0;
+                if (hipGetDeviceCount(&count) != hipSuccess || walk_device >= count)
+                    return fail(RT_ERR_NO_DEVICE, "bad device ordinal for the walk-tree build");
+                wt = rt::build_walk_tree_device(s->soup, walk_device, rt::walk_max_leaf(), rt::walk_node_cost());
+                s->times.walk_device = walk_device;
+            } else {
+                wt = rt::build_walk_tree(s->soup);
+            }
+            t3 = clk::now();
             s->flat = rt::flatten(s->soup, s->tree, 0, &wt);
         }
+        const auto t4 = clk::now();
         s->literal_stack = literal_stack_bound(s.get());
+        s->times.soup_ms = ms(t0, t1);
+        s->times.reference_tree_ms = ms(t1, t2);
+        s->times.walk_tree_ms = ms(t2, t3);
+        s->times.flatten_ms = ms(t3, t4);
         *out = s.release();
         return RT_OK;
     } catch (const rt::Error& e) {
@@ -789,6 +816,22 @@ int rt_scene_create(const double* tri_v, uint64_t n, int algo, int k, int collap
     } catch (const std::bad_alloc&) {
         return fail(RT_ERR_RUNTIME, "out of memory");
     }
+}
+
+int rt_scene_create(const double* tri_v, uint64_t n, int algo, int k, int collapse, rt_scene** out) {
+    return scene_create(tri_v, n, algo, k, collapse, -1, out);
+}
+
+int rt_scene_create_on_device(const double* tri_v, uint64_t n, int algo, int k, int collapse, int device,
+                              rt_scene** out) {
+    if (device < 0) return fail(RT_ERR_NO_DEVICE, "bad device ordinal for the walk-tree build");
+    return scene_create(tri_v, n, algo, k, collapse, device, out);
+}
+
+int rt_scene_build_times(const rt_scene* s, rt_build_times_t* out) {
+    if (!s || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out = s->times;
+    return RT_OK;
 }
 
 int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {

@@ -56,6 +56,11 @@ struct WalkTree {
     std::vector<uint32_t> order;  // triangle (loader) index per walk position
 };
 WalkTree build_walk_tree(const Soup& s);
+// The same binned-SAH tree built on a gfx950 device (walk_build.hip): equal
+// splits, device-stable order inside nodes.
+WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node_cost);
+int walk_max_leaf();       // RT_WALK_LEAF (leaf size bound of the walk tree)
+double walk_node_cost();   // RT_WALK_CT (SAH cost of a node visit)
 std::vector<int32_t> collapse_children(const WalkTree& w, int32_t b, int W);
 // 8-bit quantised copy of W = 8 wide nodes (RT_QNODE_BYTES each; walk_tree.cpp).
 std::vector<uint8_t> quantize_wide8(const uint8_t* wide, uint64_t n_nodes);

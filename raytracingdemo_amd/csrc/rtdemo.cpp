@@ -141,7 +141,8 @@ void run_test(const Config& cfg, const std::string& model, double scale, const s
         if (scene) rt_scene_destroy(scene);
         scene = nullptr;
         const auto t0 = std::chrono::steady_clock::now();
-        check(rt_scene_create(tri, n, id, k, collapse, &scene));
+        // reference tree on the host, the walk tree on the first device
+        check(rt_scene_create_on_device(tri, n, id, k, collapse, cfg.devices.front(), &scene));
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         bm.save_data_frame("bvh_build_times.csv", model, scale, full, cam, s);
         std::printf("Time build BVH using %s Split: %f \n", full.c_str(), s);

@@ -77,6 +77,9 @@ double node_cost() {
 
 }  // namespace
 
+int walk_max_leaf() { return max_leaf(); }
+double walk_node_cost() { return node_cost(); }
+
 WalkTree build_walk_tree(const Soup& s) {
     WalkTree w;
     const uint32_t n = (uint32_t)s.n;

@@ -176,3 +176,38 @@ def test_armadillo_config_c3(frames_golden, oracle):
         o = ob.render(pos, d, W, H, want=("id", "rgb"))
         gid = np.where(gg["hit_id"] == rt.RT_MISS, -1, gg["hit_id"].astype(np.int64))
         assert np.array_equal(gid, o["id"]) and np.array_equal(gg["rgb"], o["rgb"]), step
+
+
+@pytest.mark.parametrize("model", ["sponza-proxy", "stanford-bunny.obj", "teapot.obj", "suzanne.obj", "dup-stack"])
+def test_device_walk_tree_build(oracle, model):
+    """The walk tree built on the device (rt_scene_create_on_device) makes the
+    host builder's splits: the same wide-node count and stack bound on scenes
+    without positional splits, and frames identical to the oracle's."""
+    if model == "sponza-proxy":
+        from raytracingdemo_amd.scenes import sponza_proxy_triangles
+        tris, algo = sponza_proxy_triangles(), "bsah"
+    elif model == "dup-stack":
+        tris, algo = _dup_stack(40), "sah"  # coincident centroids: positional splits
+    else:
+        tris, algo = golden_scene(model), "bsah"
+    host = rt.Scene(tris, algo, 8)
+    dev = rt.Scene(tris, algo, 8, walk_device=0)
+    bt = dev.build_times()
+    assert bt["walk_device"] == 0 and host.build_times()["walk_device"] == -1
+    hs, ds = host.stats(), dev.stats()
+    assert ds["walk_tree"] == 1 and ds["triangles"] == hs["triangles"]
+    if model != "dup-stack":
+        assert ds["wide_nodes"] == hs["wide_nodes"] and ds["stack_bound"] == hs["stack_bound"], (hs, ds)
+    dev.upload([0])
+    path = rt.CameraPath(rt.scene_center(tris), 36)
+    W, H = (1920, 1080) if model == "sponza-proxy" else (320, 240)
+    ob = oracle.bvh(tris, algo, 8)
+    for step in (0, 17) if model != "dup-stack" else (0,):
+        pos, d = path.circular_path(step) if model != "dup-stack" else ([0.0, 0.0, 3.0], [0.0, 0.0, -1.0])
+        g = dev.calculate_screen(pos, d, W, H, want=("hit_id", "dist", "rgb"))
+        o = ob.render(pos, d, W, H, want=("id", "dist", "rgb"))
+        gid = np.where(g["hit_id"] == rt.RT_MISS, -1, g["hit_id"].astype(np.int64))
+        assert np.array_equal(gid, o["id"]), (model, step)
+        m = o["id"] >= 0
+        assert np.array_equal(g["dist"][m], o["dist"][m]) and np.array_equal(g["rgb"], o["rgb"]), (model, step)
+    print(f"\n{model}: walk tree host {host.build_times()['walk_tree_ms']:.1f} ms, device {bt['walk_tree_ms']:.1f} ms")

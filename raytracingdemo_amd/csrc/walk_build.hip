@@ -391,8 +391,8 @@ __global__ void k_flags(Tri tr, uint32_t n, const uint32_t* idx, const int32_t* 
 // prefix sum of the flags); elements of leaves and small subtrees keep their
 // place and leave the level loop (seg -1)
 __global__ void k_scatter(uint32_t n, const uint32_t* idx, const int32_t* seg, const uint32_t* task_b,
-                          const Split* split, const uint32_t* flag, const uint32_t* scan, const int32_t* child_task,
-                          uint32_t* idx2, int32_t* seg2) {
+                          const uint32_t* task_e, const Split* split, const uint32_t* flag, const uint32_t* scan,
+                          const int32_t* child_task, uint32_t* idx2, int32_t* seg2) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         const int32_t t = seg[p];
         if (t < 0 || split[t].leaf) {
@@ -403,7 +403,10 @@ __global__ void k_scatter(uint32_t n, const uint32_t* idx, const int32_t* seg, c
         const uint32_t b = task_b[t];
         const uint32_t lb = scan[p] - scan[b];  // left elements before p in the task
         const int c = flag[p] ? 0 : 1;
-        const uint32_t np = c == 0 ? b + lb : b + split[t].nleft + (p - b - lb);
+        // (the left count from the flags themselves: every position stays in
+        // the task's range even if it disagreed with the bins' count)
+        const uint32_t nl = scan[task_e[t]] - scan[b];
+        const uint32_t np = c == 0 ? b + lb : b + nl + (p - b - lb);
         idx2[np] = idx[p];
         seg2[np] = child_task[2 * t + c];
     }
@@ -651,8 +654,8 @@ WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node
         HT(hipMemsetAsync(flag + n, 0, sizeof(uint32_t), st));
         wsb = ws_bytes;
         HT(hipcub::DeviceScan::ExclusiveSum(ws, wsb, flag, scan, n + 1, st));
-        hipLaunchKernelGGL(k_scatter, dim3(egrid), blk, 0, st, n, idx, seg, tb[cur], split, flag, scan, child_task,
-                           idx2, seg2);
+        hipLaunchKernelGGL(k_scatter, dim3(egrid), blk, 0, st, n, idx, seg, tb[cur], te[cur], split, flag, scan,
+                           child_task, idx2, seg2);
         HT(hipGetLastError());
         HT(hipStreamSynchronize(st));  // tot: this level's inner / big / small children
         std::swap(idx, idx2);

@@ -141,9 +141,10 @@ def cpu_baseline(tris, algo, k, cams, W, H, target_s):
             "one_core": {"value": round(one, 4), "cores": 1,
                          "sample": f"{f1} bands of 60 rows x {W} px over the orbit ({rows1 * W} rays, {spent1:.1f} s)"},
             "host": host,
-            "published_O0": "none for Sponza: the reference's only Sponza datum is an old-code run "
-                            "(testruns_2025_12_25/testrun_47, ~99 s per 500x500 frame at -O0, 1 core); "
-                            "BASELINE.md lists the published -O0 figures for the other models"}
+            "published_O0": {"value": None, "note": "no published Sponza figure for the current code; the only "
+                             "Sponza datum is an older-code run (testruns_2025_12_25/testrun_47: 105.58 s mean per "
+                             "500x500 frame, 0.0024 Mrays/s, -O0, 1 core; not comparable). Published -O0 1-core "
+                             "bsah-8 figures of the other models: 0.149-0.200 Mrays/s (BASELINE.md §1)"}}
 
 
 def scene_difficulty(label, algo, k):

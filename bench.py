@@ -88,6 +88,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-dropin", action="store_true", help="skip the rt_render_frame (drop-in path) rate")
+    p.add_argument("--shard-of", type=int, default=1,
+                   help="diagnostic (one process): render only shard 0 of N interleaved row shards — the per-GPU "
+                        "work of an N-rank run without its gather; not the headline")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="committed rocprofv3 PMC summary supplying roofline.traffic")
     p.add_argument("--key-out", default="", help="write this run's workload key (for tools/pmc_traffic.py)")
@@ -332,8 +335,11 @@ def main():
     path = rt.CameraPath(center, 36)
     cams = [path.circular_path(f % 36) for f in range(F)]
 
-    rows = rows_per_rank(H, world)             # rows per rank (padded)
-    my_rows = len(shard_rows(rank, world, H))
+    # row shard of this process: rank of world (--shard-of N at one process:
+    # shard 0 of N, a diagnostic of the per-GPU work at N ranks)
+    srank, sworld = (0, a.shard_of) if (world == 1 and a.shard_of > 1) else (rank, world)
+    rows = rows_per_rank(H, sworld)            # rows per rank (padded)
+    my_rows = len(shard_rows(srank, sworld, H))
     S = a.spp
     # Two buffer sets: step k renders into set k % 2 while set (k - 1) % 2 is
     # still being gathered (the gather of step k overlaps the render of step
@@ -366,7 +372,7 @@ def main():
         if shipped[b] is not None:
             stream.wait_event(shipped[b])  # set b's previous gather has read it
         cnt[b].zero_()
-        scene.render_batch_device(local, cams, W, H, rank, world, my_rows, hit_id=r_ids[b].data_ptr(),
+        scene.render_batch_device(local, cams, W, H, srank, sworld, my_rows, hit_id=r_ids[b].data_ptr(),
                                   dist=dists.data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
                                   stream=stream.cuda_stream, mode=mode, timing=timing, count=count, spp=S)
         if padded:
@@ -474,7 +480,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_rays = a.steps * F * W * H * S
+    total_rays = a.steps * F * W * (H if sworld == world else my_rows) * S
     value = total_rays / elapsed / 1e6
     launches_timed = max(ks["timed_launches"], 1)
     frames_timed = a.steps * F
@@ -526,6 +532,7 @@ def main():
                                    f"{F}-frame camera orbit per step",
                        "width": W, "height": H, "spp": S, "bvh": f"{a.algo}-{a.k}", "frames_per_step": F,
                        "triangles": int(st["triangles"]), "mode": mode,
+                       **({"diagnostic_shard_of": sworld} if sworld != world else {}),
                        "parallelism": f"image rows interleaved x{world}" +
                                       (" + RCCL gather of rgb (overlapped)" if world > 1 else ""),
                        **({"gather_verified": verified} if world > 1 else {}),

@@ -5,8 +5,9 @@ a CPU baseline (the reference's own traversal, compiled, all host cores used).
 
 A *step* is one pass of the reference's camera orbit (runTest's 36-frame path,
 src/main.cpp:234-281): every frame is ray generation + traversal + exact
-resolve + shading on the GPU, rows interleaved over the N GPUs (row j on rank
-j mod N), followed by one RCCL gather of the step's framebuffers (rgb) and hit
+resolve + shading on the GPU, bands of 8 image rows interleaved over the N
+GPUs (band b on rank b mod N: rt_render_shard_device), followed by one RCCL
+gather of the step's framebuffers (rgb) and hit
 counts to rank 0 and the de-interleave there, on a side stream that overlaps
 the next step's render.  Total work per step is fixed (strong scaling).
 
@@ -176,8 +177,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
 
     W, H, S, B, F = a.width, a.height, a.spp, a.bounces, a.frames
     path = rt.CameraPath(rt.scene_center(tris), 36)
-    rows = rows_per_rank(H, world)
-    my_rows = len(shard_rows(rank, world, H))
+    rows = rows_per_rank(H, world, band=1)  # the paths kernel takes single interleaved rows
+    my_rows = len(shard_rows(rank, world, H, band=1))
     rgb = torch.zeros((1, rows, W, 3), dtype=torch.uint8, device=dev)
     cnt = torch.zeros((1,), dtype=torch.int64, device=dev)
     gather_rgb = coll(rgb).new_empty((world,) + tuple(rgb.shape)) if (world > 1 and rank == 0) else None
@@ -190,7 +191,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
                                       rgb=rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
                                       timing=timing, count=count)
         if world > 1:
-            return gather_frames(coll(rgb), H, world, rank, out=gather_rgb)
+            return gather_frames(coll(rgb), H, world, rank, out=gather_rgb, band=1)
         return rgb
 
     for w in range(a.warmup):
@@ -372,7 +373,9 @@ def main():
         if shipped[b] is not None:
             stream.wait_event(shipped[b])  # set b's previous gather has read it
         cnt[b].zero_()
-        scene.render_batch_device(local, cams, W, H, srank, sworld, my_rows, hit_id=r_ids[b].data_ptr(),
+        # the library's multi-GPU partition (rt_render_shard_device: bands of
+        # 8 rows interleaved over the ranks)
+        scene.render_shard_device(local, cams, W, H, srank, sworld, hit_id=r_ids[b].data_ptr(),
                                   dist=dists.data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
                                   stream=stream.cuda_stream, mode=mode, timing=timing, count=count, spp=S)
         if padded:
@@ -533,7 +536,7 @@ def main():
                        "width": W, "height": H, "spp": S, "bvh": f"{a.algo}-{a.k}", "frames_per_step": F,
                        "triangles": int(st["triangles"]), "mode": mode,
                        **({"diagnostic_shard_of": sworld} if sworld != world else {}),
-                       "parallelism": f"image rows interleaved x{world}" +
+                       "parallelism": f"8-row image bands interleaved x{world}" +
                                       (" + RCCL gather of rgb (overlapped)" if world > 1 else ""),
                        **({"gather_verified": verified} if world > 1 else {}),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},

@@ -189,17 +189,33 @@ int rt_scene_upload(rt_scene *s, const int *devices, int n_devices);
 
 /* One whole frame, blocking; replaces calculateScreen + shadeScreen
  * (main.cpp:253-262).  On one device it renders there; on G uploaded devices
- * image rows are interleaved (row j on the (j mod G)-th device), each device
- * renders its rows, and the shards (hit-id + dist + pos + rgb as requested,
+ * image rows are sharded in bands of 8 (band b on the (b mod G)-th device; as
+ * rt_render_shard_device), each device
+ * renders its shard, and the shards (hit-id + dist + pos + rgb as requested,
  * hit counts) are gathered to the first device with RCCL and de-interleaved
- * there before the copy to the host.  seconds: device time
+ * there before the copy to the host (shards as
+ * rt_render_shard_device's).  seconds: device time
  * of the frame on the first device's stream (renders to gather). */
 int rt_render_frame(rt_scene *s, const rt_camera *cam, int mode, rt_frame_out *out);
+
+/* Shard `shard` of `nshards` of every pose's frame (the multi-GPU partition,
+ * SURVEY.md §8(e)): bands of 8 image rows (one row of 8x8 tiles) interleaved
+ * over the shards, band b on shard b mod nshards, so each shard keeps whole
+ * tiles.  Outputs as rt_render_batch_spp_device's with nrows =
+ * rt_shard_height(height, nshards, shard) rows per frame, the shard's rows in
+ * image order.  This is the call of a one-process-per-GPU driver (bench.py);
+ * rt_render_batch_multi uses the same layout inside the library. */
+int rt_render_shard_device(rt_scene *s, int device, const rt_camera *cams, int nframes, int spp, int mode, int shard,
+                           int nshards, const rt_device_out *out, void *stream, uint32_t flags);
+
+/* Rows of shard `shard` of `nshards` of an image `height` rows high (-1 on bad
+ * arguments). */
+int rt_shard_height(int height, int nshards, int shard);
 
 /* rt_render_batch_spp_device over every uploaded device: nframes poses of full
  * frames (row0 = 0, stride 1, nrows = height) into device buffers `out` on the
  * FIRST uploaded device, asynchronous on `stream` (a stream of that device).
- * With G > 1 devices rows are interleaved as in rt_render_frame, each device
+ * With G > 1 devices the frames are sharded as rt_render_shard_device's, each device
  * renders its rows of every pose, and one RCCL gather per call brings the
  * shards to the first device, which de-interleaves them; hit_count[f] adds
  * all shards.  Results are identical to a one-device render.  (Test hook:
@@ -212,8 +228,9 @@ int rt_render_batch_multi(rt_scene *s, const rt_camera *cams, int nframes, int s
  * arithmetic as the device kernel; for tests and host-side gathers):
  * `gathered` holds `shards` blocks of block_bytes; shard g's block holds at
  * section_offset its frames back to back, [frames][rows_g][width] elements
- * of elem_bytes, rows_g = the image rows g, g + shards, ... below height;
- * writes frames_out[frames][height][width] elements. */
+ * of elem_bytes, rows_g = rt_shard_height(height, shards, g) rows in the
+ * layout of rt_render_shard_device; writes frames_out[frames][height][width]
+ * elements. */
 int rt_deinterleave_rows(const void *gathered, uint64_t block_bytes, uint64_t section_offset, int shards, int frames,
                          int height, int width, int elem_bytes, void *frames_out);
 

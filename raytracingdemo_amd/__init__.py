@@ -244,6 +244,20 @@ class Scene:
                                                    (N.RT_FLAG_COUNT if count else 0) |
                                                    (N.RT_FLAG_TIMING if timing else 0)))
 
+    def render_shard_device(self, device: int, cams, W: int, H: int, shard: int, nshards: int, hit_id=0, dist=0,
+                            hit_pos=0, rgb=0, hit_count=0, stream=0, mode: str = "exact", count: bool = False,
+                            timing: bool = False, spp: int = 1):
+        """Shard `shard` of `nshards` of every pose (bands of 8 rows interleaved,
+        include/rt.h rt_render_shard_device) into device pointers: pose f's
+        outputs start f * W * shard_height(H, nshards, shard) pixels in."""
+        n = len(cams)
+        arr = (N.rt_camera * max(n, 1))(*[_camera(p, d, W, H) for p, d in cams])
+        o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
+        m = N.RT_MODE_FP64 if mode in ("fp64", "literal") else N.RT_MODE_EXACT
+        N.check(N.lib().rt_render_shard_device(self._h, int(device), arr, n, int(spp), m, int(shard), int(nshards),
+                                               C.byref(o), C.c_void_p(stream or None),
+                                               (N.RT_FLAG_COUNT if count else 0) | (N.RT_FLAG_TIMING if timing else 0)))
+
     def render_batch_multi(self, cams, W: int, H: int, hit_id=0, dist=0, hit_pos=0, rgb=0, hit_count=0, stream=0,
                            mode: str = "exact", count: bool = False, timing: bool = False, spp: int = 1):
         """Full frames of every pose in ``cams`` over all uploaded devices (rows
@@ -277,6 +291,11 @@ class Scene:
             v = getattr(s, f)
             out[f] = list(v) if isinstance(v, C.Array) else v
         return out
+
+
+def shard_height(H: int, nshards: int, shard: int) -> int:
+    """Rows of one shard of the multi-GPU partition (include/rt.h rt_shard_height)."""
+    return int(N.lib().rt_shard_height(int(H), int(nshards), int(shard)))
 
 
 def deinterleave_rows(gathered: np.ndarray, shards: int, frames: int, H: int, W: int, elem_bytes: int,

@@ -35,6 +35,7 @@ EXPORTS = [
     "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_render_paths_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
     "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
     "rt_render_batch_multi", "rt_deinterleave_rows", "rt_scene_create_on_device", "rt_scene_build_times",
+    "rt_render_shard_device", "rt_shard_height",
 ]
 
 
@@ -141,6 +142,9 @@ def lib() -> C.CDLL:
                                              C.c_uint32]
     L.rt_render_paths_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_int, C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
+    L.rt_render_shard_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
+    L.rt_shard_height.argtypes = [C.c_int, C.c_int, C.c_int]
     L.rt_render_batch_multi.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                         C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
     L.rt_deinterleave_rows.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,

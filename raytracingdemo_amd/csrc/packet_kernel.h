@@ -330,7 +330,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     {
         const RtFrameParams fp = kload(&A->fp);
         const RtFrameCam cam = kload(&A->fp.cam[f]);  // this tile's frame
-        const Ray64 ray = gen_ray(fp, cam, i, fp.row0 + r * fp.row_stride);
+        const Ray64 ray = gen_ray(fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r));
         q = make_ray32(ray, cam.pad);
         tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
         pd = cam.pad;
@@ -534,7 +534,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         const RT_G uint2* ch = spilled ? reinterpret_cast<const RT_G uint2*>(aux.pool) + (size_t)chunk * RT_POOL_CHUNK
                                        : nullptr;
         const uint32_t redo = resolve_list<COUNT>(
-            sc, fp, cam, i, fp.row0 + r * fp.row_stride, nl, nl ? cand[lane] : make_uint2(0u, 0u),
+            sc, fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r), nl, nl ? cand[lane] : make_uint2(0u, 0u),
             [&](uint32_t c) { return cand[c * 64 + lane]; }, ch, dropped, drop, out, sh, rc);
         if (redo) {
             // k_fixup redoes the pixel with the exact per-lane path
@@ -632,7 +632,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
         Best out;
         Shade sh;
         const uint32_t redo = resolve_list<COUNT>(
-            sc, fp, fp.cam[f], i, fp.row0 + r * fp.row_stride, nlist, e0,
+            sc, fp, fp.cam[f], i, rt_image_row(fp.row0, fp.row_stride, fp.band, r), nlist, e0,
             [&](uint32_t c) { return cl[(size_t)c * npix + o]; }, ch, dropped, dropped ? aux.cand_drop[o] : 0.f, out,
             sh, rc);
         if (COUNT) n_redo[redo]++;

@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
         uint32_t hits = 0, segs = 0;  // segs: ray segments traced (RT_FLAG_COUNT)
         if (i < fp.W && r < fp.nrows) {
-            const int j = fp.row0 + r * fp.row_stride;
+            const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
             const size_t pix = (size_t)r * fp.W + i;
             double acc[3] = {0.0, 0.0, 0.0};
             for (int s = 0; s < fp.spp; s++) {

@@ -506,7 +506,7 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
 template <int W, int S, bool COUNT>
 __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
                                             LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
-    const int j = fp.row0 + r * fp.row_stride;
+    const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
     const RtFrameCam& cam = fp.cam[f];
     auto ray_of = [&]() { return gen_ray(fp, cam, opaque(i), j); };
     LaneCounts lc;
@@ -715,7 +715,7 @@ template <int SMAX, bool COUNT>
 __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFrameParams fp) {
     int i, r;
     if (!lane_pixel(fp, i, r)) return;
-    const int j = fp.row0 + r * fp.row_stride;
+    const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
     const size_t po = (size_t)r * fp.W + i;
     uint32_t n_nodes = 0, n_tris = 0, hits = 0;
     double acc[3] = {0.0, 0.0, 0.0};

@@ -429,8 +429,9 @@ float frame_pad(const rt_scene* s, const rt_camera* c) {
 // n x n pattern sits at ((s % n) + 0.5) / n, ((s / n) + 0.5) / n (spp = 1:
 // the reference's pixel centre 0.5, camera.hpp:35-37).
 RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row0, int row_stride, int nrows,
-                           int spp = 1) {
+                           int spp = 1, int band = 1) {
     RtFrameParams fp{};
+    fp.band = band;
     fp.nframes = n * spp;
     fp.spp = spp;
     const int g = spp_grid(spp);
@@ -532,7 +533,8 @@ void launch(const rt_scene* s, Replica& r, const RtFrameParams& fp, int mode, bo
 // `out`, on stream st (scene lock held, r's device current): up to
 // batch_frames() sample frames per launch.
 void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nframes, int spp, int mode, int row0,
-                         int row_stride, int nrows, const rt_device_out* out, hipStream_t st, uint32_t flags) {
+                         int row_stride, int nrows, const rt_device_out* out, hipStream_t st, uint32_t flags,
+                         int band = 1) {
     Replica* r = &rr;
     const rt_camera* cam = &cams[0];
     const uint64_t fpix = (uint64_t)cam->width * (uint64_t)nrows;  // pixels per frame
@@ -557,7 +559,7 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
     order_on(*r, st);
     for (int f0 = 0; f0 < nframes; f0 += per) {
         const int n = std::min(per, nframes - f0);
-        RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows, spp);
+        RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows, spp, band);
         const uint64_t off = (uint64_t)f0 * fpix, soff = off * (uint64_t)spp;
         fp.hit_id = out->hit_id ? out->hit_id + soff : nullptr;
         fp.dist = out->dist ? out->dist + soff : nullptr;
@@ -669,7 +671,8 @@ void render_group(rt_scene* s, const rt_camera* cams, int nframes, int spp, int 
         so.rgb = out->rgb ? b + L.rgb : nullptr;
         so.hit_count = reinterpret_cast<unsigned long long*>(b + L.cnt);
         const int nrows = rt_shard_rows(H, G, g);
-        if (nrows > 0) render_batch_locked(s, r, cams, nframes, spp, mode, g, G, nrows, &so, r.stream, flags);
+        if (nrows > 0)
+            render_batch_locked(s, r, cams, nframes, spp, mode, g, G, nrows, &so, r.stream, flags, RT_SHARD_BAND);
     }
     // gather to the first device: RCCL between distinct devices (one group of
     // ncclGather calls, each on its shard's stream), device copies otherwise
@@ -918,6 +921,39 @@ int rt_render_batch_multi(rt_scene* s, const rt_camera* cams, int nframes, int s
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
     }
+}
+
+int rt_render_shard_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int spp, int mode, int shard,
+                           int nshards, const rt_device_out* out, void* stream, uint32_t flags) {
+    if (!s || !out || (nframes > 0 && !cams)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (nframes < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative frame count");
+    if (spp < 1 || spp > RT_MAX_BATCH || spp_grid(spp) * spp_grid(spp) != spp)
+        return fail(RT_ERR_INVALID_ARGUMENT, "spp must be n*n samples (1, 4, 9 or 16)");
+    if (mode != RT_MODE_EXACT && mode != RT_MODE_FP64) return fail(RT_ERR_INVALID_ARGUMENT, "bad mode");
+    if (nshards < 1 || shard < 0 || shard >= nshards) return fail(RT_ERR_INVALID_ARGUMENT, "bad shard");
+    try {
+        for (int f = 0; f < nframes; f++) {
+            check_camera(s, &cams[f]);
+            if (cams[f].width != cams[0].width || cams[f].height != cams[0].height)
+                return fail(RT_ERR_INVALID_ARGUMENT, "frames of a batch must share the image size");
+        }
+        if (nframes == 0) return RT_OK;
+        const int nrows = rt_shard_rows(cams[0].height, nshards, shard);
+        if (nrows == 0) return RT_OK;
+        std::lock_guard<std::mutex> lk(s->mu);
+        Replica* r = &replica_for(s, device);
+        DevGuard g(device);
+        render_batch_locked(s, *r, cams, nframes, spp, mode, shard, nshards, nrows, out, (hipStream_t)stream, flags,
+                            RT_SHARD_BAND);
+        return RT_OK;
+    } catch (const rt::Error& e) {
+        return fail(e.status, e.msg);
+    }
+}
+
+int rt_shard_height(int height, int nshards, int shard) {
+    if (height < 0 || nshards < 1 || shard < 0 || shard >= nshards) return -1;
+    return rt_shard_rows(height, nshards, shard);
 }
 
 int rt_render_batch_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int mode, int row0,

@@ -76,21 +76,38 @@
 #else
 #define RT_HD
 #endif
-// Row-interleaved image shards (multi-device frames, rt_render_batch_multi;
-// SURVEY.md §8(e)): shard g of G holds image rows g, g + G, g + 2G, ...
-// (rt_shard_rows of them).  Its block holds, per output section, the shard's
-// frames back to back ([F][rows][W] elements, as the row-shard render writes
-// them); blocks are sized for rt_shard_pad(H, G) rows so all have one size.
-// Image row j of frame f is row j / G of frame f in shard j % G.
-static inline RT_HD int rt_shard_rows(int H, int G, int g) { return g < H ? (H - 1 - g) / G + 1 : 0; }
-static inline RT_HD int rt_shard_pad(int H, int G) { return (H + G - 1) / G; }
-// byte offset of image row j of frame f inside the gathered [G][block] buffer
-// (section at sec_off of each block, elements of eb bytes)
+// Image shards for multi-GPU frames: bands of RT_SHARD_BAND
+// rows (one row of 8x8 tiles) interleaved over the shards — band b of a frame
+// goes to shard b mod G, so every shard keeps whole, coherent tiles and the
+// depth-complexity gradient is still spread evenly.  (Single interleaved rows,
+// the round-1 layout, turn a shard's 8x8 tile into 8 columns spread over 64
+// image rows: one GPU's rate on 1/8 of a frame fell to 48% of its full-frame
+// rate.)  A shard's rows, in shard order, are its bands back to back; image
+// row of shard row r: rt_image_row(g, G, RT_SHARD_BAND, r).
+#define RT_SHARD_BAND 8
+static inline RT_HD int rt_image_row(int row0, int row_stride, int band, int r) {
+    return band <= 1 ? row0 + r * row_stride : (row0 + (r / band) * row_stride) * band + r % band;
+}
+static inline RT_HD int rt_shard_rows(int H, int G, int g) {
+    const int nb = (H + RT_SHARD_BAND - 1) / RT_SHARD_BAND;  // bands, the last one possibly partial
+    if (g >= nb) return 0;
+    const int bands = (nb - 1 - g) / G + 1;
+    const int last = H - (nb - 1) * RT_SHARD_BAND;  // rows of the last band
+    return bands * RT_SHARD_BAND - ((nb - 1) % G == g ? RT_SHARD_BAND - last : 0);
+}
+// rows every shard's block is sized for
+static inline RT_HD int rt_shard_pad(int H, int G) {
+    return ((H + RT_SHARD_BAND - 1) / RT_SHARD_BAND + G - 1) / G * RT_SHARD_BAND;
+}
+// Byte offset of image row j of frame f in the gathered [G][block] buffer:
+// shard g's block holds at sec_off its frames back to back ([F][rows_g][W]
+// elements of eb bytes, as its shard render wrote them).
 static inline RT_HD uint64_t rt_gathered_row(int j, int f, int G, int H, int W, int eb, uint64_t block,
                                              uint64_t sec_off) {
-    const int g = j % G;
-    return (uint64_t)g * block + sec_off +
-           ((uint64_t)f * (uint64_t)rt_shard_rows(H, G, g) + (uint64_t)(j / G)) * (uint64_t)W * eb;
+    const int b = j / RT_SHARD_BAND, g = b % G;
+    const int r = (b / G) * RT_SHARD_BAND + j % RT_SHARD_BAND;  // row within the shard
+    return (uint64_t)g * block + sec_off + ((uint64_t)f * (uint64_t)rt_shard_rows(H, G, g) + (uint64_t)r) *
+                                               (uint64_t)W * (uint64_t)eb;
 }
 
 #ifdef __cplusplus
@@ -175,9 +192,11 @@ struct RtFrameParams {
     double cam_iw, cam_ih;        // 1/W, 1/H            (camera.hpp:33-34)
     double cam_half, cam_aspect;  // tan(fov/2), W/H      (camera.hpp:29-30)
     int32_t W, H;
-    int32_t row0, row_stride, nrows;
+    int32_t row0, row_stride, nrows;  // shard row r is image row rt_image_row(row0, row_stride, band, r)
     int32_t nframes;              // 1..RT_MAX_BATCH, a multiple of spp
     int32_t spp;                  // samples per pixel (n x n stratified), >= 1
+    int32_t band;                 // 1: rows (row0, row_stride in rows); RT_SHARD_BAND: banded shard (in bands)
+    int32_t reserved_;
     RT_G uint32_t* hit_id;
     RT_G double* dist;
     RT_G double* hit_pos;

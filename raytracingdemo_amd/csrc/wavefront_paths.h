@@ -33,7 +33,7 @@
 __device__ __forceinline__ Ray64 pw_primary(const RtFrameParams& fp, uint32_t frame, uint32_t idx, uint32_t s,
                                             uint32_t& seed) {
     const int i = (int)(idx % (uint32_t)fp.W), r = (int)(idx / (uint32_t)fp.W);
-    const int j = fp.row0 + r * fp.row_stride;
+    const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
     seed = path_seed(frame, (uint32_t)j * (uint32_t)fp.W + (uint32_t)i, s);
     RtFrameCam c1 = fp.cam[0];
     c1.ox = path_u(seed, 0);

@@ -1,62 +1,93 @@
-"""Row-interleaved image shards for the one-process-per-GPU driver.
+"""Image shards for the one-process-per-GPU driver (bench.py).
 
-Image row j is rendered by rank j mod world (interleaving
-balances the depth-complexity gradient of a frame).  Every rank holds
-`rows_per_rank(H, world)` rows (the last one padding where H % world != 0), so
-the shards gather with one equal-sized collective; rank 0 de-interleaves.
+The partition is the library's (include/rt.h rt_render_shard_device; the
+index arithmetic of rt_device.h rt_shard_rows / rt_gathered_row): bands of
+BAND = 8 image rows — one row of 8x8 tiles — interleaved over the ranks, band
+b of a frame on rank b mod world.  Interleaving spreads the depth-complexity
+gradient of a frame; whole bands keep each rank's tiles
+coherent (single interleaved rows cost a rank half its rate at 8 ranks).
+Every rank holds `rows_per_rank(H, world)` rows (padding where its bands are
+fewer or the last band is partial), so the shards gather with one equal-sized
+collective; rank 0 de-interleaves with one gather kernel.  `band=1` gives
+single interleaved rows (row j on rank j mod world), the layout of the
+row-shard entry points (rt_render_paths_device with row0 = rank, row_stride =
+world).
 """
 from __future__ import annotations
 
-
-def rows_per_rank(H: int, world: int) -> int:
-    return (H + world - 1) // world
+BAND = 8
 
 
-def shard_rows(rank: int, world: int, H: int) -> range:
-    """Image rows of `rank`'s shard, in shard order (row r of the shard is image row rank + r*world)."""
-    return range(rank, H, world)
+def _bands(H: int, band: int) -> int:
+    return (H + band - 1) // band
 
 
-def deinterleave(gathered, H: int):
-    """Full images from gathered shards.
-
-    gathered: tensor [world, F, rows, W, ...] (shard k from rank k, rows =
-    rows_per_rank(H, world)).  Returns [F, H, W, ...] with image row
-    j = r*world + k taken from shard k, row r; padding rows are dropped.
-    """
-    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
-    rest = tuple(gathered.shape[3:])
-    nd = gathered.dim()
-    perm = (1, 2, 0) + tuple(range(3, nd))
-    full = gathered.permute(*perm).reshape((F, rows * world) + rest)
-    return full[:, :H]
+def rows_per_rank(H: int, world: int, band: int = BAND) -> int:
+    """Rows of the tallest shard (every shard's buffer is padded to it)."""
+    return (_bands(H, band) + world - 1) // world * band
 
 
-def deinterleave_into(gathered, H: int, out):
-    """deinterleave() written into `out` ([F, H, W, ...]) with one copy kernel
-    (no temporary when the shards have no padding rows)."""
-    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
-    rest = tuple(gathered.shape[3:])
-    if rows * world == H:
-        perm = (1, 2, 0) + tuple(range(3, gathered.dim()))
-        out.view((F, rows, world) + rest).copy_(gathered.permute(*perm))
-    else:
-        out.copy_(deinterleave(gathered, H))
+def shard_rows(rank: int, world: int, H: int, band: int = BAND) -> list[int]:
+    """Image rows of `rank`'s shard, in shard order (its bands back to back)."""
+    return [b * band + k for b in range(rank, _bands(H, band), world) for k in range(band) if b * band + k < H]
+
+
+def source_rows(H: int, world: int, rows: int, band: int = BAND) -> list[int]:
+    """For every image row j: its position in the [world * rows] stack of
+    padded shards (shard g = (j // band) % world, row ((j // band) // world) *
+    band + j % band of it)."""
+    out = []
+    for j in range(H):
+        b = j // band
+        out.append((b % world) * rows + (b // world) * band + j % band)
     return out
 
 
-def gather_frames(shard, H: int, world: int, rank: int, dst: int = 0, out=None):
+_IDX: dict = {}
+
+
+def _index(H: int, world: int, rows: int, device, band: int):
+    import torch
+    key = (H, world, rows, str(device), band)
+    if key not in _IDX:
+        _IDX[key] = torch.tensor(source_rows(H, world, rows, band), dtype=torch.long, device=device)
+    return _IDX[key]
+
+
+def deinterleave(gathered, H: int, band: int = BAND):
+    """Full images from gathered shards.
+
+    gathered: tensor [world, F, rows, W, ...] (shard k from rank k, rows =
+    rows_per_rank(H, world), padding rows last).  Returns [F, H, W, ...] with
+    image row j taken from its shard (source_rows)."""
+    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+    rest = tuple(gathered.shape[3:])
+    stack = gathered.transpose(0, 1).reshape((F, world * rows) + rest)
+    return stack.index_select(1, _index(H, world, rows, gathered.device, band))
+
+
+def deinterleave_into(gathered, H: int, out, band: int = BAND):
+    """deinterleave() written into `out` ([F, H, W, ...]) with one gather kernel."""
+    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+    rest = tuple(gathered.shape[3:])
+    stack = gathered.transpose(0, 1).reshape((F, world * rows) + rest)
+    import torch
+    torch.index_select(stack, 1, _index(H, world, rows, gathered.device, band), out=out)
+    return out
+
+
+def gather_frames(shard, H: int, world: int, rank: int, dst: int = 0, out=None, band: int = BAND):
     """Gather every rank's [F, rows, W, ...] shard to `dst` and de-interleave there.
 
     The shards land in one [world, F, rows, W, ...] buffer (`out`, allocated
     once by the caller, or here) through views of it, so the collective writes
-    straight into the layout `deinterleave` reads: one copy in all.  Returns
-    [F, H, W, ...] on `dst`, None elsewhere.
+    straight into the layout `deinterleave` reads.  Returns [F, H, W, ...] on
+    `dst`, None elsewhere.
     """
     import torch.distributed as dist
     if rank == dst:
         buf = out if out is not None else shard.new_empty((world,) + tuple(shard.shape))
         dist.gather(shard, list(buf.unbind(0)), dst=dst)
-        return deinterleave(buf, H)
+        return deinterleave(buf, H, band)
     dist.gather(shard, None, dst=dst)
     return None

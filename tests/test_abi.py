@@ -117,21 +117,23 @@ def test_batch_render_rejects_mixed_sizes_and_needs_a_device():
                                         (5, 4, 3, 2, 1)])
 def test_deinterleave_rows_matches_row_interleaving(G, F, H, W, eb):
     """rt_deinterleave_rows (the host twin of the device kernel that
-    rt_render_batch_multi runs after the RCCL gather): shard g holds image
-    rows g, g + G, ... of every frame; the
-    de-interleave puts row j of frame f back from shard j % G, row j // G
-    (each shard's frames back to back in its block, as its row-shard render
-    wrote them)."""
+    rt_render_batch_multi runs after the RCCL gather): shard g holds the bands
+    of 8 image rows b = g, g + G, ... of every frame; the de-interleave puts
+    row j of frame f back from shard (j // 8) % G (each shard's frames back to
+    back in its block, as its shard render wrote them)."""
     import numpy as np
     import raytracingdemo_amd as rt
     rng = np.random.default_rng(G * 1000 + H)
     frames = rng.integers(0, 256, size=(F, H, W * eb), dtype=np.uint8)
-    R = -(-H // G)
+    R = -(-(-(-H // 8)) // G) * 8  # rows of the tallest shard
     sec_off, pad = 256, 64  # a section inside each block, as the library lays it out
     block = sec_off + F * R * W * eb + pad  # sized for the tallest shard
     gathered = rng.integers(0, 256, size=(G, block), dtype=np.uint8)  # the unused tail stays garbage
+    from raytracingdemo_amd.shards import shard_rows
     for g in range(G):
-        rows = np.ascontiguousarray(frames[:, g::G]).reshape(-1)  # [F, rows_g, W*eb], frames back to back
+        mine = shard_rows(g, G, H)  # bands of 8 rows, band b on shard b % G
+        assert len(mine) == rt.shard_height(H, G, g)
+        rows = np.ascontiguousarray(frames[:, mine]).reshape(-1)  # [F, rows_g, W*eb], frames back to back
         gathered[g, sec_off:sec_off + len(rows)] = rows
     out = rt.deinterleave_rows(gathered, G, F, H, W, eb, block_bytes=block, section_offset=sec_off)
     assert np.array_equal(out, frames)

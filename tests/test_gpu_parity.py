@@ -531,3 +531,38 @@ def test_sharded_frames_through_the_abi_equal_one_device(monkeypatch, shards):
     assert np.array_equal(g["hit_id"], ref["id"].cpu().numpy().view(np.uint32).reshape(F, -1)[2])
     assert np.array_equal(g["rgb"].reshape(-1), ref["rgb"].cpu().numpy().reshape(F, -1)[2])
     assert g["hits"] == int(ref_cnt[2])
+
+
+def test_band_shards_reassemble_to_full_frame():
+    """rt_render_shard_device (bands of 8 rows interleaved over the shards, the
+    multi-GPU partition bench.py uses) reassembles through shards.py into the
+    one-device frame bit for bit, for even and uneven shard counts."""
+    torch = pytest.importorskip("torch")
+    from raytracingdemo_amd.shards import deinterleave_into, rows_per_rank
+    tris = golden_scene("stanford-bunny.obj")
+    s = scene("stanford-bunny.obj", "bsah", 8)
+    path = rt.CameraPath(rt.scene_center(tris), 36)
+    cams = [path.circular_path(f) for f in (2, 19)]
+    W, H, F = 150, 101, 2
+    full = [s.calculate_screen(p, d, W, H) for p, d in cams]
+    st = torch.cuda.current_stream().cuda_stream
+    for G in (1, 2, 3, 8):
+        R = rows_per_rank(H, G)
+        ids = torch.full((G, F, R, W), -7, dtype=torch.int32, device="cuda:0")
+        rgb = torch.zeros((G, F, R, W, 3), dtype=torch.uint8, device="cuda:0")
+        cnt = torch.zeros((G, F), dtype=torch.int64, device="cuda:0")
+        for g in range(G):
+            n = rt.shard_height(H, G, g)
+            t_id = torch.empty((F, n, W), dtype=torch.int32, device="cuda:0")
+            t_rgb = torch.empty((F, n, W, 3), dtype=torch.uint8, device="cuda:0")
+            s.render_shard_device(0, cams, W, H, g, G, hit_id=t_id.data_ptr(), rgb=t_rgb.data_ptr(),
+                                  hit_count=cnt[g].data_ptr(), stream=st)
+            ids[g, :, :n] = t_id
+            rgb[g, :, :n] = t_rgb
+        torch.cuda.synchronize()
+        img_id = deinterleave_into(ids, H, torch.empty((F, H, W), dtype=torch.int32, device="cuda:0"))
+        img_rgb = deinterleave_into(rgb, H, torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda:0"))
+        for f in range(F):
+            assert np.array_equal(img_id[f].cpu().numpy().view(np.uint32).reshape(-1), full[f]["hit_id"]), (G, f)
+            assert np.array_equal(img_rgb[f].cpu().numpy().reshape(-1, 3), full[f]["rgb"]), (G, f)
+            assert int(cnt[:, f].sum()) == full[f]["hits"], (G, f)

@@ -93,9 +93,25 @@ def test_deinterleave_single_process():
         # the bench's single-copy form (padded and unpadded shards)
         out = torch.empty_like(full)
         assert torch.equal(deinterleave_into(sh, H, out), full)
-    H = 12  # rows * world == H: the strided-view copy
+    H = 16  # whole bands of 8 rows: no padding for 1 or 2 ranks
     full = torch.arange(F * H * W * 3, dtype=torch.int32).reshape(F, H, W, 3)
-    for world in (1, 2, 3, 4, 6, 12):
+    for world in (1, 2, 3, 4):
         rows = rows_per_rank(H, world)
-        sh = torch.stack([full[:, list(shard_rows(r, world, H))] for r in range(world)])
+        sh = torch.zeros((world, F, rows, W, 3), dtype=torch.int32)
+        for r in range(world):
+            idx = shard_rows(r, world, H)
+            sh[r, :, : len(idx)] = full[:, idx]
         assert torch.equal(deinterleave_into(sh, H, torch.empty_like(full)), full)
+
+
+def test_python_shards_match_the_library_layout():
+    """shards.py (bench.py's partition) and the library's rt_shard_height /
+    rt_deinterleave_rows (rt_render_shard_device's layout) agree."""
+    import raytracingdemo_amd as rt
+    for H in (1, 7, 8, 9, 37, 1080, 2160, 1081):
+        for world in (1, 2, 3, 4, 7, 8):
+            rows = [shard_rows(r, world, H) for r in range(world)]
+            assert sorted(j for rr in rows for j in rr) == list(range(H))
+            assert [len(rr) for rr in rows] == [rt.shard_height(H, world, r) for r in range(world)]
+            assert max(len(rr) for rr in rows) <= rows_per_rank(H, world)
+            assert all(rr == sorted(rr) for rr in rows)

@@ -72,7 +72,10 @@ def deinterleave_into(gathered, H: int, out, band: int = BAND):
     rest = tuple(gathered.shape[3:])
     stack = gathered.transpose(0, 1).reshape((F, world * rows) + rest)
     import torch
-    torch.index_select(stack, 1, _index(H, world, rows, gathered.device, band), out=out)
+    if out.device != gathered.device:  # (host-side gathers: one copy across)
+        out.copy_(stack.index_select(1, _index(H, world, rows, gathered.device, band)))
+    else:
+        torch.index_select(stack, 1, _index(H, world, rows, gathered.device, band), out=out)
     return out
 
 

@@ -29,6 +29,8 @@ for s in $STEPS; do
         quick) run bench_quick 300 python bench.py --no-cpu --steps 10 ;;
         split) RT_RESOLVE=split run bench_split 300 python bench.py --no-cpu --steps 10 ;;
         shards) for n in 2 4 8; do run bench_shard$n 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of $n || exit 1; done ;;
+        rehearse) RT_BENCH_REHEARSE=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                      --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu ;;
         spp4)  run bench_spp4 300 python bench.py --no-cpu --steps 5 --spp 4 ;;
         paths) run bench_paths 300 python bench.py --no-cpu --paths --steps 3 --warmup 1 ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \

@@ -247,8 +247,8 @@ int rt_render_rows_device(rt_scene *s, int device, const rt_camera *cam, int mod
  * with calculateScreen + shadeScreen per pose, main.cpp:253-262).  Frame f's
  * outputs start f * width * nrows pixels into every buffer of `out` (rgb and
  * pos: 3 values per pixel), and its hit counter is out->hit_count[f].  The
- * library launches up to 18 frames at a time (one persistent traversal launch,
- * one resolve launch, one fix-up launch), so per-launch ramp-up, tail and
+ * library launches up to 36 frames at a time (one persistent traversal launch
+ * with the resolve fused in, one fix-up launch), so per-launch ramp-up, tail and
  * launch gaps are paid once per batch.  Results are identical to per-frame
  * calls. */
 int rt_render_batch_device(rt_scene *s, int device, const rt_camera *cams, int nframes, int mode, int row0,

@@ -683,6 +683,15 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
 // Persistent waves over 8x8 tiles; the stack bound of the tree must fit SP
 // (the host falls back to the per-lane kernel otherwise), so no push can drop.
 // FUSED (spp = 1): each tile is resolved, shaded and stored by its own wave.
+// Waves per workgroup of the packet kernel.  7 (448 threads): four
+// workgroups fill a CU at 7 waves/SIMD, and the argument block in LDS is
+// shared by 7 waves instead of 4 — which leaves room for 36 poses of cameras
+// per launch (RT_MAX_BATCH) at full occupancy.
+#ifndef RT_PACKET_WAVES
+#define RT_PACKET_WAVES 7
+#endif
+constexpr int kPacketWaves = RT_PACKET_WAVES;
+
 // Occupancy target of the packet kernel in waves per SIMD (0: the compiler's
 // choice).  The fused resolve's fp64 set-up raises the kernel's VGPR peak
 // above the walk's (91 VGPRs, 5 waves); 7 waves (72 VGPRs, 28 B of spills
@@ -698,9 +707,9 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
 #endif
 
 template <int W, int SP, int K, bool COUNT, bool FUSED>
-__global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs args) {
-    __shared__ uint32_t stacks[4][SP];
-    __shared__ uint2 cands[4][K * 64];
+__global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_packet(PacketArgs args) {
+    __shared__ uint32_t stacks[kPacketWaves][SP];
+    __shared__ uint2 cands[kPacketWaves][K * 64];
     __shared__ PacketArgs s_args;
     {
         const __attribute__((address_space(4))) uint32_t* src =
@@ -721,7 +730,7 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
     // frame's spread counters when the wave moves on to another frame
     uint32_t hacc = 0;
     int hf = -1;
-    const uint32_t hslot = (blockIdx.x * 4 + (uint32_t)wv) % RT_HIT_SLOTS;
+    const uint32_t hslot = (blockIdx.x * kPacketWaves + (uint32_t)wv) % RT_HIT_SLOTS;
     for (;;) {
         A = launder(A);
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
@@ -734,9 +743,9 @@ __global__ void __launch_bounds__(256) RT_PACKET_ATTR k_trace_packet(PacketArgs 
             // whole grid starting at once would serialise on the 8 counters
             // for ~10 us); the counter hands out the slots after the XCD's waves
             first = false;
-            t = (int)(xq + RT_QUEUES * ((blockIdx.x / RT_QUEUES) * 4 + wv));
+            t = (int)(xq + RT_QUEUES * ((blockIdx.x / RT_QUEUES) * kPacketWaves + wv));
         } else if (lane == 0) {
-            const uint32_t nwq = 4u * ((gridDim.x + RT_QUEUES - 1 - xq) / RT_QUEUES);  // waves of queue xq
+            const uint32_t nwq = kPacketWaves * ((gridDim.x + RT_QUEUES - 1 - xq) / RT_QUEUES);  // waves of queue xq
             t = (int)(xq + RT_QUEUES * (nwq + atomicAdd(kload(&A->aux.tile_ctr) + xq * RT_QUEUE_STRIDE, 1u)));
         }
         const int tile = __builtin_amdgcn_readlane(t, 0);  // wave-uniform: a uniform loop exit

@@ -790,7 +790,7 @@ bool split_resolve(int spp) {
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
                         hipStream_t s, const hipEvent_t* ev) {
-    const dim3 grid((unsigned)aux.grid), blk(256);
+    const dim3 grid((unsigned)aux.grid), blk(256), pgrid((unsigned)aux.pgrid), pblk(64 * kPacketWaves);
     // RT_FLAG_TIMING: two markers bracket the traversal kernel only (the
     // rest of the pipeline is timed as frame minus traversal by the caller)
     if (ev) (void)hipEventRecord(ev[0], s);
@@ -798,10 +798,10 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
         const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
         if (!split_resolve(fp.spp)) {
             if (count)
-                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, true>), grid, blk, 0, s,
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, true>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             else
-                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true>), grid, blk, 0, s,
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
         } else {
@@ -809,10 +809,10 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
             const uint64_t rt8 = (((uint64_t)(fp.W + 15) / 16) * ((uint64_t)(fp.nrows + 15) / 16) + 7) / 8;
             const dim3 rgrid((unsigned)(8 * rt8 * (uint64_t)(fp.nframes / fp.spp)));
             if (count)
-                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, false>), grid, blk, 0, s,
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, false>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             else
-                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, false>), grid, blk, 0, s,
+                hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, false>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
             if (count) hipLaunchKernelGGL((k_resolve<true>), rgrid, blk, 0, s, sc, fp, aux);
@@ -837,13 +837,22 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     return hipGetLastError();
 }
 
+// Resident 256-thread workgroups per CU of the per-lane persistent kernels
+// (exact traversal, fix-up, paths): the larger of their occupancies.
 template <int W>
 int blocks_per_cu_w(uint32_t stack_bound) {
+    int n = 0, m = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<W, kLdsStack, false, 3>, 256, 0) != hipSuccess)
+        n = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_paths<W, kPathStack>, 256, 0) != hipSuccess) m = 1;
+    (void)stack_bound;
+    return n > m ? n : m;
+}
+template <int W>
+int packet_blocks_per_cu_w() {
     int n = 0;
-    hipError_t e = use_packet(stack_bound)
-                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                                 &n, k_trace_packet<W, kPacketStack, kCandidates, false, true>, 256, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<W, kLdsStack, false, 3>, 256, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, k_trace_packet<W, kPacketStack, kCandidates, false, true>, 64 * kPacketWaves, 0);
     return e == hipSuccess ? n : 1;
 }
 
@@ -866,6 +875,15 @@ int exact_blocks_per_cu(int width, uint32_t stack_bound) {
                          : blocks_per_cu_w<16>(stack_bound);
     if (n < 1) n = 1;
     return n < 8 ? n : 8;
+}
+
+// Workgroups per CU of the packet kernel (64 * kPacketWaves threads each).
+int packet_blocks_per_cu(int width) {
+    int n = width == 2   ? packet_blocks_per_cu_w<2>()
+            : width == 4 ? packet_blocks_per_cu_w<4>()
+            : width == 8 ? packet_blocks_per_cu_w<8>()
+                         : packet_blocks_per_cu_w<16>();
+    return n < 1 ? 1 : n;
 }
 
 // the smallest LDS ring of the per-lane kernels (spill sizing)
@@ -911,7 +929,8 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     // the redo list must hold every pixel of the shard; the split resolve
     // needs candidate lists for every pixel of the batch
     const uint64_t bpix = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.nframes;  // pixels of the batch
-    if (use_packet(sc.stack_bound) && (!aux.redo || aux.redo_cap < bpix / (uint64_t)fp.spp || !aux.pool))
+    if (use_packet(sc.stack_bound) &&
+        (!aux.redo || aux.redo_cap < bpix / (uint64_t)fp.spp || !aux.pool || aux.pgrid <= 0))
         return hipErrorInvalidValue;
     if (use_packet(sc.stack_bound) && split_resolve(fp.spp) &&
         (!aux.cand || !aux.cand_cnt || !aux.cand_drop || !aux.cand_ovf || aux.cand_cap < bpix))

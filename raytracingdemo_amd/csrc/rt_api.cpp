@@ -23,6 +23,7 @@ namespace rt {
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
                         hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after);
 int exact_blocks_per_cu(int width, uint32_t stack_bound);
+int packet_blocks_per_cu(int width);
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
                         int bounces, hipStream_t s, const hipEvent_t* ev);
 hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
@@ -93,7 +94,8 @@ struct Replica {
     uint32_t* d_tiles = nullptr;
     uint64_t* d_spill = nullptr;
     uint32_t spill_cap = 0;
-    int grid = 0;
+    int grid = 0;                // per-lane kernels: 256-thread workgroups
+    int pgrid = 0;               // packet kernel: 64 * kPacketWaves-thread workgroups
     uint32_t* d_redo = nullptr;  // packet pipeline -> fix-up kernel pixel list
     uint64_t redo_cap = 0;
     uint64_t* d_pool = nullptr;  // candidate overflow pool (pool_chunks x RT_POOL_CHUNK entries)
@@ -317,6 +319,7 @@ void upload_one(rt_scene* s, int device) {
         if (v >= 1 && v < bpc) bpc = v;
     }
     r.grid = prop.multiProcessorCount * bpc;
+    r.pgrid = prop.multiProcessorCount * rt::packet_blocks_per_cu(f.width);
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
     HIP_TRY(hipMalloc(&r.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
@@ -489,6 +492,7 @@ RtLaunchAux aux_of(Replica& r) {
     a.spill = r.d_spill;
     a.spill_cap = r.spill_cap;
     a.grid = r.grid;
+    a.pgrid = r.pgrid;
     a.redo = r.d_redo;
     a.redo_cap = r.redo_cap;
     a.pool = r.d_pool;

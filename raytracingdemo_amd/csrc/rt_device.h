@@ -54,7 +54,7 @@
 // traversal kernel's ramp-up and tail, and the launch gaps, are paid once per
 // batch instead of once per frame.
 #ifndef RT_MAX_BATCH
-#define RT_MAX_BATCH 18
+#define RT_MAX_BATCH 36
 #endif
 #define RT_QUEUE_WORDS (RT_HIT_BASE + RT_MAX_BATCH * RT_HIT_SLOTS * RT_QUEUE_STRIDE)
 // Candidate lists of the packet walk, per pixel: RT_CAND_LDS entries kept in
@@ -163,7 +163,7 @@ struct RtLaunchAux {
     uint64_t redo_cap;    // entries (>= pixels of the launch)
     RT_G uint64_t* pool;       // candidate overflow pool: pool_chunks x RT_POOL_CHUNK entries
     uint32_t pool_chunks;
-    uint32_t reserved;
+    int32_t pgrid;             // workgroups of the packet kernel (64 * kPacketWaves threads each)
     // spp > 1 (packet kernel -> k_resolve) and the wavefront path tracer:
     RT_G uint64_t* cand;       // {tri, t lower bound} per entry, [K][pixels]
     RT_G uint8_t* cand_cnt;    // entries per pixel | kCandSpilled | kCandDropped (wavefront: 0xFF = overflow)

@@ -157,6 +157,29 @@ __device__ __forceinline__ int tri_classify(const float4 A, const float4 B, cons
     return 2;
 }
 
+// Pose of sample frame f with its sub-pixel offset: sample q = f mod spp of
+// an n x n pattern at ((q mod n) + 0.5) / n, ((q div n) + 0.5) / n — the
+// host's expressions (rt_api.cpp frame_params), so the doubles are the same;
+// spp = 1: 0.5, the reference's pixel centre (camera.hpp:35-37).
+__device__ __forceinline__ RtFrameCam frame_cam_of(const RtPose& p, const RtFrameParams& fp, int f) {
+    RtFrameCam c;
+    for (int a = 0; a < 3; a++) {
+        c.pos[a] = p.pos[a];
+        c.dir[a] = p.dir[a];
+        c.right[a] = p.right[a];
+        c.up[a] = p.up[a];
+    }
+    c.pad = p.pad;
+    c.reserved = 0;
+    const int q = f % fp.spp, g = fp.spp_n;
+    c.ox = ((double)(q % g) + 0.5) / (double)g;
+    c.oy = ((double)(q / g) + 0.5) / (double)g;
+    return c;
+}
+__device__ __forceinline__ RtFrameCam frame_cam(const RtFrameParams& fp, int f) {
+    return frame_cam_of(fp.pose[f / fp.spp], fp, f);
+}
+
 // Camera pixel caches (camera.hpp:35-37), evaluated per pixel in the same
 // operation order as the host's pixel_caches (no contraction): bit-identical.
 // ox / oy: the sample's offset inside the pixel; the reference's pixel centre

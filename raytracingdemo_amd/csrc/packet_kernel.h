@@ -329,7 +329,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     uint32_t ob;
     {
         const RtFrameParams fp = kload(&A->fp);
-        const RtFrameCam cam = kload(&A->fp.cam[f]);  // this tile's frame
+        const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f / fp.spp]), fp, f);  // this tile's frame
         const Ray64 ray = gen_ray(fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r));
         q = make_ray32(ray, cam.pad);
         tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
@@ -527,7 +527,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
             if (__uint_as_float(e.y) <= tcull) cand[nl++ * 64 + lane] = e;
         }
         const RtDevScene sc = kload(&A->sc);
-        const RtFrameCam cam = kload(&A->fp.cam[f]);
+        const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f]), fp, f);  // (spp = 1: pose f)
         Best out;
         Shade sh;
         ResolveCounts rc;
@@ -632,7 +632,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
         Best out;
         Shade sh;
         const uint32_t redo = resolve_list<COUNT>(
-            sc, fp, fp.cam[f], i, rt_image_row(fp.row0, fp.row_stride, fp.band, r), nlist, e0,
+            sc, fp, frame_cam(fp, f), i, rt_image_row(fp.row0, fp.row_stride, fp.band, r), nlist, e0,
             [&](uint32_t c) { return cl[(size_t)c * npix + o]; }, ch, dropped, dropped ? aux.cand_drop[o] : 0.f, out,
             sh, rc);
         if (COUNT) n_redo[redo]++;
@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
         if (active && !redo) {
             store_sample(fp, pix * (size_t)spp + k, out, sh);
             double c[3];
-            shade_color(fp.cam[f], out, sh, c);
+            shade_color(frame_cam(fp, f), out, sh, c);
             acc[0] = acc[0] + c[0];
             acc[1] = acc[1] + c[1];
             acc[2] = acc[2] + c[2];
@@ -683,12 +683,12 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
 // Persistent waves over 8x8 tiles; the stack bound of the tree must fit SP
 // (the host falls back to the per-lane kernel otherwise), so no push can drop.
 // FUSED (spp = 1): each tile is resolved, shaded and stored by its own wave.
-// Waves per workgroup of the packet kernel.  7 (448 threads): four
-// workgroups fill a CU at 7 waves/SIMD, and the argument block in LDS is
-// shared by 7 waves instead of 4 — which leaves room for 36 poses of cameras
-// per launch (RT_MAX_BATCH) at full occupancy.
+// Waves per workgroup of the packet kernel (4: seven workgroups per CU at 7
+// waves/SIMD).  7-wave workgroups (4 per CU, the LDS argument block shared by
+// 7 waves) measured 5% slower: a workgroup's waves land unevenly on the 4
+// SIMDs.
 #ifndef RT_PACKET_WAVES
-#define RT_PACKET_WAVES 7
+#define RT_PACKET_WAVES 4
 #endif
 constexpr int kPacketWaves = RT_PACKET_WAVES;
 

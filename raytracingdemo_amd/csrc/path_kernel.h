@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
     st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
     st.tid = tid;
     st.top = 0;
-    const RtFrameCam& cam = fp.cam[0];
+    const RtFrameCam cam = frame_cam(fp, 0);
     for (;;) {
         int tile = 0;
         if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);

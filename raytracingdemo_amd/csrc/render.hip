@@ -507,7 +507,7 @@ template <int W, int S, bool COUNT>
 __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
                                             LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
     const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
-    const RtFrameCam& cam = fp.cam[f];
+    const RtFrameCam cam = frame_cam(fp, f);
     auto ray_of = [&]() { return gen_ray(fp, cam, opaque(i), j); };
     LaneCounts lc;
     const Win best = trace_core<W, S, COUNT>(sc, ray_of, cam.pad, st, pass0, lc);
@@ -558,7 +558,7 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
         const Shade sh = shade_of(sc, b.tri);
         store_sample(fp, po * (size_t)fp.spp + k, b, sh);
         double c[3];
-        shade_color(fp.cam[f], b, sh, c);
+        shade_color(frame_cam(fp, f), b, sh, c);
         acc[0] = acc[0] + c[0];
         acc[1] = acc[1] + c[1];
         acc[2] = acc[2] + c[2];
@@ -720,12 +720,13 @@ __global__ void __launch_bounds__(256) k_trace_literal(RtDevScene sc, RtFramePar
     uint32_t n_nodes = 0, n_tris = 0, hits = 0;
     double acc[3] = {0.0, 0.0, 0.0};
     for (int k = 0; k < fp.spp; k++) {
-        const Ray64 ray = gen_ray(fp, fp.cam[k], i, j);
+        const RtFrameCam cam = frame_cam(fp, k);
+        const Ray64 ray = gen_ray(fp, cam, i, j);
         const Best best = trace_literal<SMAX, COUNT>(sc, ray, n_nodes, n_tris);
         const Shade sh = shade_of(sc, best.tri);
         store_sample(fp, po * (size_t)fp.spp + k, best, sh);
         double c[3];
-        shade_color(fp.cam[k], best, sh, c);
+        shade_color(cam, best, sh, c);
         acc[0] = acc[0] + c[0];
         acc[1] = acc[1] + c[1];
         acc[2] = acc[2] + c[2];
@@ -768,7 +769,7 @@ RtFrameParams single_pose(const RtFrameParams& fp, int p) {
     const size_t off = (size_t)p * (size_t)fp.W * (size_t)fp.nrows;  // pixels before pose p
     const size_t soff = off * (size_t)fp.spp;                         // samples before pose p
     o.nframes = fp.spp;
-    for (int k = 0; k < fp.spp; k++) o.cam[k] = fp.cam[p * fp.spp + k];
+    o.pose[0] = fp.pose[p];
     if (o.hit_id) o.hit_id += soff;
     if (o.dist) o.dist += soff;
     if (o.hit_pos) o.hit_pos += 3 * soff;

@@ -437,20 +437,18 @@ RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row
     fp.band = band;
     fp.nframes = n * spp;
     fp.spp = spp;
-    const int g = spp_grid(spp);
+    // sample q of each pose sits at ((q % g) + 0.5) / g, ((q / g) + 0.5) / g
+    // (computed in-kernel by frame_cam with these same expressions)
+    fp.spp_n = spp_grid(spp);
     for (int p = 0; p < n; p++) {
-        RtFrameCam k{};
+        RtPose k{};
         k.pad = frame_pad(s, &c[p]);
         for (int a = 0; a < 3; a++) {
             k.pos[a] = c[p].pos[a];
             k.dir[a] = c[p].dir[a];
         }
         rt::camera_basis(c[p].dir, k.right, k.up);
-        for (int q = 0; q < spp; q++) {
-            k.ox = ((double)(q % g) + 0.5) / (double)g;
-            k.oy = ((double)(q / g) + 0.5) / (double)g;
-            fp.cam[p * spp + q] = k;
-        }
+        fp.pose[p] = k;
     }
     rt::pixel_constants(c->width, c->height, fp.cam_iw, fp.cam_ih, fp.cam_half, fp.cam_aspect);
     fp.W = c->width;

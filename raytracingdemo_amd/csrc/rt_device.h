@@ -174,17 +174,23 @@ struct RtLaunchAux {
 
 // One camera pose of a launch (Camera, camera.hpp:20-38: position, view
 // direction and the basis main.cpp:325-329 derives from it).
-struct RtFrameCam {
+struct RtPose {
     double pos[3], dir[3], right[3], up[3];
-    double ox, oy;                 // sub-pixel sample offset (0.5, 0.5 = the reference's pixel centre)
     float pad;                     // world-space slab margin of the fp32 traversal (per pose)
     uint32_t reserved;
 };
+// A pose with the sub-pixel offset of one sample (kernel side: frame_cam).
+struct RtFrameCam {
+    double pos[3], dir[3], right[3], up[3];
+    float pad;
+    uint32_t reserved;
+    double ox, oy;                 // sub-pixel sample offset (0.5, 0.5 = the reference's pixel centre)
+};
 
-// One launch: `nframes` frames (cam[0..nframes-1]) of the same image
-// geometry and row shard.  With spp samples per pixel a pose is spp
-// consecutive frames (sample s of pose p = frame p * spp + s, its own
-// sub-pixel offset); outputs are per pose: per-sample values (hit_id, dist,
+// One launch: `nframes` sample frames of the same image geometry and row
+// shard, poses pose[0 .. nframes / spp - 1].  With spp samples per pixel a
+// pose is spp consecutive frames (sample s of pose p = frame p * spp + s, its
+// own sub-pixel offset, computed in-kernel: frame_cam); outputs are per pose: per-sample values (hit_id, dist,
 // hit_pos) of pose p, pixel o, sample s at (p * W * nrows + o) * spp + s, the
 // averaged colour (rgb) at p * W * nrows + o, the hit counter (samples hit)
 // at hit_count[p].  spp = 1 is the reference's one ray per pixel centre.
@@ -196,14 +202,14 @@ struct RtFrameParams {
     int32_t nframes;              // 1..RT_MAX_BATCH, a multiple of spp
     int32_t spp;                  // samples per pixel (n x n stratified), >= 1
     int32_t band;                 // 1: rows (row0, row_stride in rows); RT_SHARD_BAND: banded shard (in bands)
-    int32_t reserved_;
+    int32_t spp_n;                // n of the n x n sample pattern (spp = n * n)
     RT_G uint32_t* hit_id;
     RT_G double* dist;
     RT_G double* hit_pos;
     RT_G uint8_t* rgb;
     RT_G unsigned long long* hit_count;
     RT_G unsigned long long* counters;  // [rays, node_fetches, tri_tests, chain_checks, hits, chain_nodes] or NULL
-    RtFrameCam cam[RT_MAX_BATCH];
+    RtPose pose[RT_MAX_BATCH];    // pose f / spp of sample frame f (104 B each: 36 fit the LDS copy)
 };
 
 // Workspace of the wavefront path tracer (wavefront_paths.h), per replica.

@@ -35,7 +35,7 @@ __device__ __forceinline__ Ray64 pw_primary(const RtFrameParams& fp, uint32_t fr
     const int i = (int)(idx % (uint32_t)fp.W), r = (int)(idx / (uint32_t)fp.W);
     const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
     seed = path_seed(frame, (uint32_t)j * (uint32_t)fp.W + (uint32_t)i, s);
-    RtFrameCam c1 = fp.cam[0];
+    RtFrameCam c1 = frame_cam(fp, 0);
     c1.ox = path_u(seed, 0);
     c1.oy = path_u(seed, 1);
     return gen_ray<false>(fp, c1, i, j);
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256) k_pw_shade(RtDevScene sc, RtFrameParams f
     st.top = 0;
     const uint32_t n = b == 0 ? ws.P : ws.ctl[b & 1];
     const size_t P = ws.P;
-    const RtFrameCam& cam = fp.cam[0];
+    const RtFrameCam cam = frame_cam(fp, 0);
     const double w = __builtin_ldexp(1.0, -b);  // 0.5^b: k_paths' repeated halving, exactly
     const uint32_t stride = gridDim.x * 256u;
     // every lane of a wave runs the same number of iterations (ballots below)

@@ -43,7 +43,10 @@ for s in $STEPS; do
                    gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}" 300 \
-                          python bench.py --no-cpu --steps 10 || exit 1; done ;;
+                          python bench.py --no-cpu --no-dropin --steps 10 || exit 1; done ;;
+        vshards) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
+                      n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}_s8" 300 \
+                          python bench.py --no-cpu --no-dropin --steps 10 --shard-of 8 || exit 1; done ;;
         sq)    for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
                            "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD" \
                            "SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_TC_DATA_READ_REQ SQC_TC_STALL SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \

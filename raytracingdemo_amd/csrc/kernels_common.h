@@ -171,6 +171,10 @@ __device__ __forceinline__ RtFrameCam frame_cam_of(const RtPose& p, const RtFram
     }
     c.pad = p.pad;
     c.reserved = 0;
+    if (fp.spp_n == 1) {  // (0 + 0.5) / 1, without the divisions
+        c.ox = c.oy = 0.5;
+        return c;
+    }
     const int q = f % fp.spp, g = fp.spp_n;
     c.ox = ((double)(q % g) + 0.5) / (double)g;
     c.oy = ((double)(q / g) + 0.5) / (double)g;

@@ -36,9 +36,9 @@ for s in $STEPS; do
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
                    -- python bench.py --steps 3 --warmup 1 --no-cpu --no-dropin ;;
         pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
-                   -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu --no-dropin --key-out gpurun_out/pmc_key.txt && \
+                   -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin --key-out gpurun_out/pmc_key.txt && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
-                   -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu --no-dropin && \
+                   -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin && \
                python tools/pmc_traffic.py gpurun_out/pmc/fetch_counter_collection.csv \
                    gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
@@ -53,7 +53,7 @@ for s in $STEPS; do
                            "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
                    pn=$((${pn:-0}+1))
                    run sq$pn 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq -o sq$pn \
-                       -- python bench.py --steps 1 --warmup 0 --frames 18 --no-cpu --no-dropin --key-out gpurun_out/pmc_key.txt || exit 1
+                       -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin --key-out gpurun_out/pmc_key.txt || exit 1
                done
                python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt
                python tools/pmc_valu.py gpurun_out/pmc_key.txt gpurun_out/pmc_valu.json gpurun_out/sq/sq*_counter_collection.csv ;;

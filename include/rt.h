@@ -103,6 +103,9 @@ typedef struct {
     uint32_t walk_tree;       /* 1: device nodes from the rebuilt SAH walk tree
                                  (results unchanged), 0: from the
                                  reference tree itself (RT_WALK=reference) */
+    uint64_t layout_digest;   /* 64-bit FNV-style digest of the device scene
+                                 sections (host copy): equal digests = the same
+                                 device scene, byte for byte (build tests) */
 } rt_scene_stats_t;
 
 typedef struct {

@@ -67,7 +67,7 @@ class rt_scene_stats_t(C.Structure):
                 ("real_leaves", C.c_uint64), ("depth", C.c_uint32), ("max_children", C.c_uint32),
                 ("max_leaf_size", C.c_uint32), ("wide_width", C.c_uint32), ("wide_nodes", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("stack_bound", C.c_uint32), ("node_bytes", C.c_double),
-                ("walk_tree", C.c_uint32)]
+                ("walk_tree", C.c_uint32), ("layout_digest", C.c_uint64)]
 
 
 class rt_frame_stats_t(C.Structure):

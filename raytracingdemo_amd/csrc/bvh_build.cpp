@@ -14,6 +14,9 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <cstdlib>
+#include <exception>
+#include <thread>
 
 #include "rt_internal.h"
 
@@ -61,9 +64,56 @@ struct Builder {
         }
         return b;
     }
+    // std::sort of the range by centre.  Large ranges run the same introsort
+    // with the right side of the top partitions on threads (par_introsort):
+    // the permutation is std::sort's, ties included.
+    bool threads = true;
     void sort_range(int64_t lo, int64_t hi, int axis) {
         const double* c = s.c[axis].data();
-        std::sort(order.begin() + lo, order.begin() + hi, [c](uint32_t p, uint32_t q) { return c[p] < c[q]; });
+        auto less = [c](uint32_t p, uint32_t q) { return c[p] < c[q]; };
+        auto first = order.begin() + lo, last = order.begin() + hi;
+        if (!threads || hi - lo < 65536) { std::sort(first, last, less); return; }
+        const int64_t n = hi - lo;
+        par_introsort(first, last, 2 * (63 - __builtin_clzll((uint64_t)n)), less, std::max<int64_t>(16384, n / 32));
+        // std::sort's closing pass: insertion sort of the whole range (every
+        // element is at most 16 places from home, inside its partition)
+        for (auto i = first + 1; i < last; ++i) {
+            const uint32_t v = *i;
+            auto j = i;
+            for (; j > first && less(v, *(j - 1)); --j) *j = *(j - 1);
+            *j = v;
+        }
+    }
+    // The introsort loop of libstdc++'s std::sort (bits/stl_algo.h:
+    // median-of-three of first + 1, middle, last - 1 moved to first, Hoare
+    // partition about it, recursion on the right side, loop on the left, heap
+    // sort past 2 log2(n) levels, stop at 16 elements).  The two sides of a
+    // partition are disjoint and each is processed the same way wherever it
+    // runs, so right sides of at least par_min elements go to threads.
+    template <class It, class C>
+    static void par_introsort(It first, It last, int depth, C less, int64_t par_min) {
+        std::vector<std::thread> th;
+        while (last - first > 16) {
+            if (depth == 0) { std::partial_sort(first, last, last, less); break; }
+            --depth;
+            It a = first + 1, b = first + (last - first) / 2, c = last - 1;
+            It med = less(*a, *b) ? (less(*b, *c) ? b : (less(*a, *c) ? c : a))
+                                  : (less(*a, *c) ? a : (less(*b, *c) ? c : b));
+            std::iter_swap(first, med);
+            It lo = first + 1, hi = last;
+            for (;;) {
+                while (less(*lo, *first)) ++lo;
+                --hi;
+                while (less(*first, *hi)) --hi;
+                if (!(lo < hi)) break;
+                std::iter_swap(lo, hi);
+                ++lo;
+            }
+            if (last - lo >= par_min) th.emplace_back([=] { par_introsort(lo, last, depth, less, par_min); });
+            else par_introsort(lo, last, depth, less, par_min);
+            last = lo;
+        }
+        for (auto& x : th) x.join();
     }
     static bool leaf(int64_t n, int k) { return n <= (int64_t)k || k < 2; }  // isLeaf :71-76
 
@@ -193,15 +243,32 @@ int longest_axis(const double mn[3], const double mx[3]) {
     return 0;
 }
 
+// Runs fn(lo, hi) over [0, n) in contiguous chunks on up to 16 threads (each
+// chunk writes only its own outputs, so the result does not depend on the
+// split).  Small ranges run inline.
+template <class F>
+void parallel_for(uint64_t n, F fn) {
+    const uint64_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t T = std::min<uint64_t>(hw, n / 16384);
+    if (T <= 1) { fn(uint64_t(0), n); return; }
+    std::vector<std::thread> th;
+    const uint64_t per = (n + T - 1) / T;
+    for (uint64_t c = 1; c < T; c++) th.emplace_back(fn, std::min(n, c * per), std::min(n, (c + 1) * per));
+    fn(uint64_t(0), std::min(n, per));
+    for (auto& x : th) x.join();
+}
+
 }  // namespace
 
 Soup make_soup(const double* tri_v, uint64_t n) {
     Soup s;
     s.n = n;
-    s.v.assign(tri_v, tri_v + n * 9);
+    s.v.resize(n * 9);
     for (int a = 0; a < 3; a++) { s.c[a].resize(n); s.lo[a].resize(n); s.hi[a].resize(n); }
     s.normal.resize(n * 3);
-    for (uint64_t i = 0; i < n; i++) {
+    parallel_for(n, [&](uint64_t lo, uint64_t hi) {
+    std::memcpy(s.v.data() + lo * 9, tri_v + lo * 9, (hi - lo) * 9 * sizeof(double));
+    for (uint64_t i = lo; i < hi; i++) {
         const double* p = tri_v + i * 9;
         for (int a = 0; a < 3; a++) {
             double x0 = p[a], x1 = p[3 + a], x2 = p[6 + a];
@@ -221,8 +288,119 @@ Soup make_soup(const double* tri_v, uint64_t n) {
         if (len == 0) { nx = ny = nz = 0; } else { nx = nx / len; ny = ny / len; nz = nz / len; }
         s.normal[i * 3] = nx; s.normal[i * 3 + 1] = ny; s.normal[i * 3 + 2] = nz;
     }
+    });
     return s;
 }
+
+namespace {
+
+// Splits node n (index ni of its vector) with the reference's partition and
+// returns its children (:520-568): bounds per child range, parent = ni.  An
+// empty result is a leaf.
+std::vector<RNode> split_node(Builder& B, int algo, int pk, const RNode& n, int32_t ni) {
+    const int64_t lo = n.begin, hi = n.end;
+    if (hi - lo <= 1) return {};
+    const int axis = longest_axis(n.mn, n.mx);
+    std::vector<size_t> sp = algo == RT_ALGO_MEDIAN ? B.median(lo, hi, axis, pk)
+                             : algo == RT_ALGO_SAH  ? B.sah(lo, hi, axis, pk)
+                                                     : B.binned(lo, hi, axis, pk);
+    if (sp.empty()) return {};
+    std::sort(sp.begin(), sp.end());
+    std::vector<RNode> kids;
+    int64_t from = lo;
+    auto add_child = [&](int64_t a, int64_t b) {
+        RNode c;
+        c.begin = a;
+        c.end = b;
+        c.parent = ni;
+        Box bx = B.bounds(a, b);
+        std::memcpy(c.mn, bx.mn, sizeof bx.mn);
+        std::memcpy(c.mx, bx.mx, sizeof bx.mx);
+        kids.push_back(std::move(c));
+    };
+    for (size_t x : sp) {
+        if (x == 0 || x >= (size_t)(hi - lo)) throw Error{RT_ERR_OUT_OF_RANGE, "invalid split position"};
+        int64_t to = lo + (int64_t)x;
+        if (from >= to) throw Error{RT_ERR_OUT_OF_RANGE, "Invalid iterator range"};
+        add_child(from, to);
+        from = to;
+    }
+    add_child(from, hi);
+    return kids;
+}
+
+// The reference's build loop (work stack, :520-568) below nodes[0].  Node ids
+// follow its numbering: a node's children are appended when it is split, and
+// the stack is LIFO, so the descendants of a node's last child come next,
+// then those of the child before it, and so on.
+void grow(Builder& B, int algo, int pk, std::vector<RNode>& nodes) {
+    std::vector<int32_t> work{0};
+    while (!work.empty()) {
+        int32_t ni = work.back();
+        work.pop_back();
+        std::vector<RNode> kids = split_node(B, algo, pk, nodes[ni], ni);
+        for (RNode& c : kids) {
+            nodes[ni].kids.push_back((int32_t)nodes.size());
+            nodes.push_back(std::move(c));
+        }
+        for (int32_t c : nodes[ni].kids) work.push_back(c);
+    }
+}
+
+// The same tree with the subtrees of large nodes built on threads.  Every
+// split reads and permutes only its own range of B.order, so subtrees are
+// independent; the numbering above makes the descendants of child j one
+// contiguous id range, so the subtrees built apart (each numbered from its own
+// root = 0) are spliced in with an offset: children at 1..k, then child k's
+// descendants, then child k-1's, ...  The result equals grow()'s node for node.
+std::vector<RNode> grow_parallel(Builder& B, int algo, int pk, RNode root, int64_t par_min) {
+    std::vector<RNode> out;
+    if (root.end - root.begin < par_min) {
+        out.push_back(std::move(root));
+        grow(B, algo, pk, out);
+        return out;
+    }
+    std::vector<RNode> kids = split_node(B, algo, pk, root, 0);
+    const size_t k = kids.size();
+    std::vector<std::vector<RNode>> sub(k);
+    std::vector<std::exception_ptr> err(k);
+    std::vector<std::thread> th;
+    auto run = [&](size_t j) {
+        try {
+            RNode c = kids[j];
+            c.parent = -1;
+            sub[j] = grow_parallel(B, algo, pk, std::move(c), par_min);
+        } catch (...) { err[j] = std::current_exception(); }
+    };
+    for (size_t j = 0; j + 1 < k; j++) th.emplace_back(run, j);
+    if (k) run(k - 1);
+    for (auto& x : th) x.join();
+    for (auto& e : err) if (e) std::rethrow_exception(e);
+    // splice: base[j] = id of child j's first descendant
+    std::vector<int32_t> base(k);
+    int32_t next = (int32_t)(1 + k);
+    for (size_t j = k; j-- > 0;) { base[j] = next; next += (int32_t)sub[j].size() - 1; }
+    out.reserve((size_t)next);
+    out.push_back(std::move(root));
+    for (size_t j = 0; j < k; j++) out[0].kids.push_back((int32_t)(1 + j));
+    auto remap = [&](size_t j, int32_t x) { return x == 0 ? (int32_t)(1 + j) : base[j] + x - 1; };
+    for (size_t j = 0; j < k; j++) {  // the children themselves (ids 1..k)
+        RNode c = std::move(sub[j][0]);
+        c.parent = 0;
+        for (int32_t& q : c.kids) q = remap(j, q);
+        out.push_back(std::move(c));
+    }
+    for (size_t j = k; j-- > 0;)
+        for (size_t x = 1; x < sub[j].size(); x++) {
+            RNode c = std::move(sub[j][x]);
+            c.parent = remap(j, c.parent);
+            for (int32_t& q : c.kids) q = remap(j, q);
+            out.push_back(std::move(c));
+        }
+    return out;
+}
+
+}  // namespace
 
 Tree build_tree(const Soup& s, int algo, int k, int collapse) {
     if (algo < 0 || algo > 2) throw Error{RT_ERR_OUT_OF_RANGE, "Unknown algorithm"};
@@ -245,43 +423,14 @@ Tree build_tree(const Soup& s, int algo, int k, int collapse) {
         std::memcpy(root.mn, b.mn, sizeof b.mn);
         std::memcpy(root.mx, b.mx, sizeof b.mx);
     }
-    t.nodes.push_back(root);
-    std::vector<int32_t> work{0};  // build work stack (:520-568)
-    while (!work.empty()) {
-        int32_t ni = work.back();
-        work.pop_back();
-        const int64_t lo = t.nodes[ni].begin, hi = t.nodes[ni].end;
-        if (hi - lo <= 1) continue;
-        const int axis = longest_axis(t.nodes[ni].mn, t.nodes[ni].mx);
-        std::vector<size_t> sp = algo == RT_ALGO_MEDIAN ? B.median(lo, hi, axis, pk)
-                                 : algo == RT_ALGO_SAH  ? B.sah(lo, hi, axis, pk)
-                                                         : B.binned(lo, hi, axis, pk);
-        if (sp.empty()) continue;
-        std::sort(sp.begin(), sp.end());
-        std::vector<int32_t> kids;
-        int64_t from = lo;
-        auto add_child = [&](int64_t a, int64_t b) {
-            RNode c;
-            c.begin = a;
-            c.end = b;
-            c.parent = ni;
-            Box bx = B.bounds(a, b);
-            std::memcpy(c.mn, bx.mn, sizeof bx.mn);
-            std::memcpy(c.mx, bx.mx, sizeof bx.mx);
-            kids.push_back((int32_t)t.nodes.size());
-            t.nodes.push_back(std::move(c));
-        };
-        for (size_t x : sp) {
-            if (x == 0 || x >= (size_t)(hi - lo)) throw Error{RT_ERR_OUT_OF_RANGE, "invalid split position"};
-            int64_t to = lo + (int64_t)x;
-            if (from >= to) throw Error{RT_ERR_OUT_OF_RANGE, "Invalid iterator range"};
-            add_child(from, to);
-            from = to;
-        }
-        add_child(from, hi);
-        t.nodes[ni].kids = kids;
-        for (int32_t c : kids) work.push_back(c);
-    }
+    // subtrees of at least par_min primitives go to threads (RT_BUILD_THREADS=1:
+    // the serial loop, for A/B)
+    const char* bt = std::getenv("RT_BUILD_THREADS");
+    const bool serial = bt && std::atoi(bt) == 1;
+    B.threads = !serial;
+    const int64_t par_min = std::max<int64_t>(4096, (int64_t)s.n / 256);
+    t.nodes = serial ? std::vector<RNode>{root} : grow_parallel(B, algo, pk, root, par_min);
+    if (serial) grow(B, algo, pk, t.nodes);
     if (collapse) {
         // collapse (:574-608), log2(k)-1 passes (main.cpp:208)
         const int passes = static_cast<int>(std::log2(k)) - 1;
@@ -433,6 +582,75 @@ struct Flattener {
             if (w.nodes[kids[c]].left >= 0) walk_fill(w, kids[c], refs[c], depth + 1);
     }
 
+    // walk_ref(w, 0, 0) for an inner root, with the subtrees of the root's
+    // inner children filled on threads.  walk_fill numbers depth first: the
+    // root 0, its inner children 1..m, then child 1's descendants, child 2's,
+    // ... — each a contiguous id range.  Every child's subtree is filled into
+    // a Flat of its own (the child = local node 0) and copied to its range,
+    // inner-node refs shifted; the array equals the serial fill byte for byte.
+    uint32_t walk_root(const WalkTree& w) {
+        const uint32_t id = alloc_node();
+        std::vector<int32_t> kids = collapse_children(w, 0, W);
+        const WalkNode& n = w.nodes[0];
+        const int axis = longest_axis(n.mn, n.mx);
+        std::stable_sort(kids.begin(), kids.end(), [&](int32_t x, int32_t y) {
+            return w.nodes[x].mn[axis] + w.nodes[x].mx[axis] < w.nodes[y].mn[axis] + w.nodes[y].mx[axis];
+        });
+        wide_depth = std::max(wide_depth, 1u);
+        std::vector<uint32_t> refs(kids.size());
+        std::vector<size_t> inner;
+        for (size_t c = 0; c < kids.size(); c++) {
+            if (w.nodes[kids[c]].left < 0) refs[c] = walk_ref(w, kids[c], 1);
+            else { refs[c] = alloc_node(); inner.push_back(c); }
+        }
+        for (size_t c = 0; c < kids.size(); c++) {
+            float b6[6];
+            box32(w.nodes[kids[c]].mn, w.nodes[kids[c]].mx, b6);
+            set_slot(id, (int)c, b6, refs[c]);
+        }
+        uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + (size_t)id * nb);
+        p[7] = (uint32_t)axis | ((uint32_t)kids.size() << 2);
+        const size_t m = inner.size();
+        std::vector<Flat> sub(m);
+        std::vector<uint32_t> sub_depth(m, 0);
+        std::vector<std::exception_ptr> err(m);
+        auto run = [&](size_t j) {
+            try {
+                sub[j].width = W;
+                Flattener L(s, t, sub[j]);
+                const uint32_t root = L.alloc_node();
+                L.walk_fill(w, kids[inner[j]], root, 1);
+                sub_depth[j] = L.wide_depth;
+            } catch (...) { err[j] = std::current_exception(); }
+        };
+        std::vector<std::thread> th;
+        for (size_t j = 0; j + 1 < m; j++) th.emplace_back(run, j);
+        if (m) run(m - 1);
+        for (auto& x : th) x.join();
+        for (auto& e : err) if (e) std::rethrow_exception(e);
+        uint64_t total = f.n_wide;
+        std::vector<uint64_t> base(m);
+        for (size_t j = 0; j < m; j++) { base[j] = total; total += sub[j].n_wide - 1; }
+        f.wide.resize(total * nb, 0);
+        for (size_t j = 0; j < m; j++) {
+            wide_depth = std::max(wide_depth, sub_depth[j]);
+            const uint32_t self = refs[inner[j]];
+            auto remap = [&](uint32_t r) -> uint32_t {
+                if (r == RT_INVALID_REF || (r & RT_LEAF_BIT)) return r;
+                return r == 0 ? self : (uint32_t)(base[j] + r - 1);
+            };
+            for (uint64_t x = 0; x < sub[j].n_wide; x++) {
+                const uint64_t g = x == 0 ? self : base[j] + x - 1;
+                uint8_t* dst = f.wide.data() + g * nb;
+                std::memcpy(dst, sub[j].wide.data() + x * nb, nb);
+                uint32_t* q = reinterpret_cast<uint32_t*>(dst);
+                for (int c = 0; c < W; c++) q[8 * c + RT_CHILD_REF] = remap(q[8 * c + RT_CHILD_REF]);
+            }
+        }
+        f.n_wide = total;
+        return id;
+    }
+
     uint32_t emit_inner(const std::vector<int32_t>& kids, uint32_t depth) {
         uint32_t id = alloc_node();
         wide_depth = std::max(wide_depth, depth + 1);
@@ -523,11 +741,13 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
     const uint64_t n = s.n;
     const std::vector<uint32_t>& worder = walk ? walk->order : t.order;
     f.tri64.resize(n * RT_TRI64_DOUBLES);
-    f.tri32.resize((n + RT_TRI32_PAD) * 12, 0.0f);  // + padding records (packet kernel leaf chunks)
+    f.tri32.resize((n + RT_TRI32_PAD) * 12);  // + zeroed padding records (packet kernel leaf chunks)
+    std::fill(f.tri32.begin() + (ptrdiff_t)(n * 12), f.tri32.end(), 0.0f);
     f.tri_id.resize(n);
     f.tri_rank.resize(n);
     f.tri_leaf.resize(n);
-    for (uint64_t i = 0; i < n; i++) {
+    parallel_for(n, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; i++) {
         uint32_t id = worder[i];
         const double* p = s.v.data() + (size_t)id * 9;
         double* q = f.tri64.data() + i * RT_TRI64_DOUBLES;
@@ -549,6 +769,7 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
         r[11] = up(std::max({std::fabs(q[0]), std::fabs(q[1]), std::fabs(q[2])}));
         f.tri_id[i] = id;
     }
+    });
     // --- real nodes (fp64 box + parent) and reference visit ranks
     const size_t R = t.nodes.size();
     f.rbox.resize(R * 6);
@@ -603,7 +824,8 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
         if ((double)v < x) v = std::nextafter(v, std::numeric_limits<float>::infinity());
         return v;
     };
-    for (uint64_t i = 0; i < n; i++) {
+    parallel_for(n, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; i++) {
         double* q = f.tri64.data() + i * RT_TRI64_DOUBLES;
         const uint32_t id = f.tri_id[i], leaf = f.tri_leaf[i];
         // shadeScreen's normal.normalize() (main.cpp:361, vector3.hpp), done
@@ -624,12 +846,15 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
             b[3 + a] = down(f.rbox[(size_t)leaf * 6 + 3 + a]);
         }
     }
+    });
     // --- wide nodes
     Flattener F(s, t, f);
     F.box32(t.nodes[0].mn, t.nodes[0].mx, f.root_box);
     if (walk && n > 0) {
         F.box32(walk->nodes[0].mn, walk->nodes[0].mx, f.root_box);
-        f.root_ref = F.walk_ref(*walk, 0, 0);
+        const char* bt = std::getenv("RT_BUILD_THREADS");  // 1: the serial fill (A/B, tests)
+        const bool serial = (bt && std::atoi(bt) == 1) || walk->nodes[0].left < 0;
+        f.root_ref = serial ? F.walk_ref(*walk, 0, 0) : F.walk_root(*walk);
         if (f.n_wide == 0) F.alloc_node();
     } else if (n == 0) {
         f.root_ref = RT_INVALID_REF;

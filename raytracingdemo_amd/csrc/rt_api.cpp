@@ -278,10 +278,8 @@ void upload_one(rt_scene* s, int device) {
     }
     r.blob_bytes = off;
     HIP_TRY(hipMalloc(&r.blob, off));
-    std::vector<uint8_t> host(off, 0);
-    for (auto& sc : secs)
-        if (sc.bytes) std::memcpy(host.data() + sc.off, sc.src, sc.bytes);
-    HIP_TRY(hipMemcpy(r.blob, host.data(), off, hipMemcpyHostToDevice));
+    for (auto& sc : secs)  // straight from the flat arrays: no host staging copy
+        if (sc.bytes) HIP_TRY(hipMemcpy(static_cast<uint8_t*>(r.blob) + sc.off, sc.src, sc.bytes, hipMemcpyHostToDevice));
     auto at = [&](int k) { return static_cast<uint8_t*>(r.blob) + secs[k].off; };
     RtDevScene& d = r.dev;
     d.nodes = at(0);
@@ -1175,6 +1173,25 @@ int rt_scene_stats(const rt_scene* s, rt_scene_stats_t* o) {
     o->device_bytes = f.wide.size() + f.tri32.size() * 4 + f.tri64.size() * 8 + f.tri_id.size() * 12 +
                       f.rbox.size() * 8 + f.rparent.size() * 4 + s->soup.normal.size() * 8 +
                       (f.rkid_off.size() + f.rkid.size() + f.rrange.size() + f.ref2walk.size()) * 4;
+    uint64_t h = 0xcbf29ce484222325ull;
+    auto mix = [&](const void* p, size_t bytes) {
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        h = (h ^ bytes) * 0x100000001b3ull;
+        size_t i = 0;
+        for (; i + 8 <= bytes; i += 8) {
+            uint64_t w;
+            std::memcpy(&w, b + i, 8);
+            h = (h ^ w) * 0x100000001b3ull;
+        }
+        for (; i < bytes; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+    };
+    auto vec = [&](const auto& v) { mix(v.data(), v.size() * sizeof(v[0])); };
+    vec(f.wide); vec(f.tri32); vec(f.tri64); vec(f.tri_id); vec(f.tri_rank); vec(f.tri_leaf); vec(f.rbox);
+    vec(f.rparent); vec(f.rkid_off); vec(f.rkid); vec(f.rrange); vec(f.ref2walk);
+    mix(&f.root_ref, sizeof f.root_ref);
+    mix(f.root_box, sizeof f.root_box);
+    mix(&f.stack_bound, sizeof f.stack_bound);
+    o->layout_digest = h;
     return RT_OK;
 }
 

@@ -2,6 +2,8 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "rt_device.h"
@@ -15,14 +17,28 @@ struct Error {
     std::string msg;
 };
 
+// std::vector storage whose resize() leaves elements uninitialised: arrays
+// that a parallel loop fills completely are first touched by the threads that
+// write them, not zero-filled by one thread beforehand.
+template <class T>
+struct UninitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = UninitAlloc<U>; };
+    UninitAlloc() = default;
+    template <class U> UninitAlloc(const UninitAlloc<U>&) noexcept {}
+    template <class U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+template <class T>
+using uvector = std::vector<T, UninitAlloc<T>>;
+
 // Triangle soup in loader order with the per-triangle values the reference
 // precomputes (triangle.hpp:14-19, getMin/getMax :27-38), stored SoA.
 struct Soup {
     uint64_t n = 0;
-    std::vector<double> v;           // n*9: v0, v1, v2
-    std::vector<double> c[3];        // centre per axis
-    std::vector<double> lo[3], hi[3];// per-triangle box
-    std::vector<double> normal;      // n*3
+    uvector<double> v;               // n*9: v0, v1, v2
+    uvector<double> c[3];            // centre per axis
+    uvector<double> lo[3], hi[3];    // per-triangle box
+    uvector<double> normal;          // n*3
 };
 Soup make_soup(const double* tri_v, uint64_t n);
 
@@ -73,9 +89,9 @@ struct Flat {
     double pad = 0, coord_max = 0;        // max |coordinate| (sizes the per-frame margin)
     std::vector<uint8_t> wide;            // wide nodes, node_bytes(W) each
     uint64_t n_wide = 0;
-    std::vector<double> tri64;            // BVH order: v0, e1, e2 (9 doubles)
-    std::vector<float> tri32;             // BVH order: v0, e1, e2 (fp32, 12 floats padded)
-    std::vector<uint32_t> tri_id, tri_rank, tri_leaf;
+    uvector<double> tri64;                // BVH order: v0, e1, e2 (9 doubles)
+    uvector<float> tri32;                 // BVH order: v0, e1, e2 (fp32, 12 floats padded)
+    uvector<uint32_t> tri_id, tri_rank, tri_leaf;
     std::vector<double> rbox;             // real nodes: 6 doubles
     std::vector<int32_t> rparent;         // real nodes: parent
     std::vector<uint32_t> rkid_off, rkid, rrange;  // real tree in CSR form

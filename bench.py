@@ -523,6 +523,10 @@ def main():
             if pv.get("workload_key") == key:
                 valu = {"busy": pv["valu_busy"], "insts_per_launch": pv["valu_insts_per_launch"],
                         "salu_insts_per_launch": pv["salu_insts_per_launch"],
+                        # SURVEY §8(d) asks for VALU ops per ray: every lane of a
+                        # wave64 instruction is one ray's op (a tile's 64 rays share
+                        # the wave's node and triangle tests)
+                        "lane_ops_per_ray": round(64 * pv["valu_insts_per_launch"] / (frames_per_launch * W * H * S), 1),
                         "wave_cycles_split": pv["wave_cycles_split"], "source": "profiles/pmc_valu.json"}
         except (OSError, ValueError, KeyError):
             pass
@@ -586,19 +590,23 @@ def dropin_rate(scene, cams, W, H, mode):
     call into host buffers, blocking, as runTest's calculateScreen call,
     src/main.cpp:253-255): hit ids, distances and PPM bytes for every pose of
     the orbit, D2H copies included.  Reported beside the headline, never as it."""
+    # one set of host arrays reused frame after frame, as runTest reuses its
+    # global ray_hits (src/main.cpp:39)
+    g = None
     for p, d in cams[:2]:
-        scene.calculate_screen(p, d, W, H, mode=mode, want=("hit_id", "dist", "rgb"))
+        g = scene.calculate_screen(p, d, W, H, mode=mode, want=("hit_id", "dist", "rgb"), out=g)
     t0 = time.perf_counter()
     dev_s = 0.0
     for p, d in cams:
-        g = scene.calculate_screen(p, d, W, H, mode=mode, want=("hit_id", "dist", "rgb"))
+        g = scene.calculate_screen(p, d, W, H, mode=mode, out=g)
         dev_s += g["seconds"]
     wall = time.perf_counter() - t0
     n = len(cams) * W * H
     return {"value": round(n / wall / 1e6, 2), "unit": "Mrays/s", "entry_point": "rt_render_frame",
             "frames": len(cams), "ms_per_frame": round(wall / len(cams) * 1e3, 3),
             "device_ms_per_frame": round(dev_s / len(cams) * 1e3, 3),
-            "note": "one pose per call, host buffers (hit_id + dist + rgb D2H), blocking"}
+            "note": "one pose per call into one reused set of pageable host arrays (hit_id + dist + rgb D2H), "
+                    "blocking"}
 
 
 if __name__ == "__main__":

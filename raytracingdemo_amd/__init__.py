@@ -186,13 +186,25 @@ class Scene:
         return TreeDump(boxes, meta, order)
 
     def calculate_screen(self, pos, d, W: int, H: int, mode: str = "exact",
-                         want=("hit_id", "dist", "pos", "rgb")) -> dict:
-        """One whole frame: calculateScreen + shadeScreen on the first device."""
+                         want=("hit_id", "dist", "pos", "rgb"), out: dict | None = None) -> dict:
+        """One whole frame: calculateScreen + shadeScreen (rt_render_frame).
+
+        out: the dict a previous call returned, to write this frame into the
+        same host arrays (runTest fills one global ray_hits vector frame after
+        frame, src/main.cpp:39,322-349); `want` is then taken from it."""
         npx = int(W) * int(H)
-        out = {"hit_id": np.empty(npx, np.uint32) if "hit_id" in want else None,
-               "dist": np.empty(npx) if "dist" in want else None,
-               "pos": np.empty((npx, 3)) if "pos" in want else None,
-               "rgb": np.empty((npx, 3), np.uint8) if "rgb" in want else None}
+        if out is not None:
+            spec = {"hit_id": ((npx,), np.uint32), "dist": ((npx,), np.float64), "pos": ((npx, 3), np.float64),
+                    "rgb": ((npx, 3), np.uint8)}
+            for k, (shp, dt) in spec.items():
+                a = out.get(k)
+                if a is not None and (a.shape != shp or a.dtype != dt or not a.flags.c_contiguous):
+                    raise ValueError(f"out[{k!r}] must be a C-contiguous {np.dtype(dt).name} array of shape {shp}")
+        else:
+            out = {"hit_id": np.empty(npx, np.uint32) if "hit_id" in want else None,
+                   "dist": np.empty(npx) if "dist" in want else None,
+                   "pos": np.empty((npx, 3)) if "pos" in want else None,
+                   "rgb": np.empty((npx, 3), np.uint8) if "rgb" in want else None}
         fo = N.rt_frame_out()
         if out["hit_id"] is not None:
             fo.hit_id = out["hit_id"].ctypes.data_as(C.POINTER(C.c_uint32))

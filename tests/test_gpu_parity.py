@@ -43,14 +43,16 @@ def compare_with_oracle(oracle, s, tris, pos, d, W, H, algo, k, mode="exact"):
 @pytest.mark.parametrize("mode", ["exact", "fp64"])
 @pytest.mark.parametrize("model", MODELS)
 def test_reference_frames_bit_exact(frames_golden, model, mode):
-    """500x500 frames 0,9,17,27 == testruns_final PPM bytes and hit counts."""
+    """500x500 frames 0,9,17,27 == testruns_final PPM bytes and hit counts
+    (one set of host arrays reused across the frames, as runTest does)."""
     g = frames_golden[model]
     tris = golden_scene(model)
     s = scene(model, "bsah", 2)
     c = rt.scene_center(tris)
+    out = None
     for step in (0, 9, 17, 27):
         pos, d = rt.CameraPath(c, 36).circular_path(step)
-        out = s.calculate_screen(pos, d, 500, 500, mode=mode, want=("rgb",))
+        out = s.calculate_screen(pos, d, 500, 500, mode=mode, want=("rgb",), out=out)
         assert hashlib.sha256(rt.ppm_bytes(out["rgb"], 500, 500)).hexdigest() == g["frames"][step]["sha256"], step
         assert out["hits"] == g["frames"][step]["hits"]
 

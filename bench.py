@@ -202,6 +202,13 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
     segs_per_pose = cs["rays"] / F
+    # algorithmic bytes of one pose (the counting pass, W = 8): per segment the
+    # lane's own node steps on the 96-B quantised nodes (walk_tree.cpp
+    # quantize_wide8), 48-B fp32 triangle records through the pre-filter,
+    # 72-B fp64 Moller-Trumbore records, 52 B per ancestor-chain check and the
+    # winner's 56-B record; 3 B of colour per pixel
+    alg_pose = (cs["node_fetches"] * 96 + cs["tri_prefilter"] * 48 + cs["tri_tests"] * 72
+                + cs["chain_checks"] * 52 + cs["rays"] * 56) / F + my_rows * W * 3
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -221,10 +228,23 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
         dist.all_reduce(sg, op=dist.ReduceOp.SUM)
         segs_per_pose = float(sg.item())
     nominal = a.steps * F * W * H * S * (1 + B)
+    kernel_s = ks["trace_ms"] / max(ks["timed_launches"], 1) / 1e3
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu:
             cpu = paths_cpu_baseline(tris, a, path, W, H, S, B)
+        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|paths|spp{S}|b{B}|n{world}"
+        if a.key_out:
+            with open(a.key_out, "w") as fh:
+                fh.write(key + "\n")
+        traffic = None
+        try:
+            pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic_paths.json")))
+            if pm.get("workload_key") == key:
+                traffic = round(float(pm["hbm_bytes_per_launch"]))
+        except (OSError, ValueError, KeyError):
+            pass
+        achieved = alg_pose / kernel_s / 1e9 if kernel_s > 0 else 0.0
         line = {
             "metric": f"Mrays/sec (primary + {B} diffuse bounces, {S}spp) on Sponza {W}x{H}",
             "value": round(nominal / elapsed / 1e6, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
@@ -239,6 +259,14 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
             "segments_traced_per_s_M": round(segs_per_pose * a.steps * F / elapsed / 1e6, 2),
             "segments_per_sample": round(segs_per_pose / (W * H * S), 3),
             "kernel_ms_avg": round(ks["trace_ms"] / max(ks["timed_launches"], 1), 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_paths",
+                         "alg_bytes_per_launch": round(alg_pose),
+                         "per_segment": {k: round(cs[c] / max(cs["rays"], 1), 3) for k, c in
+                                         (("node_fetches", "node_fetches"), ("tri_prefilter", "tri_prefilter"),
+                                          ("tri_tests_fp64", "tri_tests"), ("chain_checks", "chain_checks"))},
+                         "bytes": "node steps x 96 (quantised) + pre-filter x 48 + fp64 tests x 72 + chain checks "
+                                  "x 52 + segments x 56 + 3 per pixel"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -428,16 +428,26 @@ __device__ __forceinline__ bool chain_fast_ok32(const float (&b)[6], const Ray64
 
 // Per-lane traversal stack: the top S entries live in LDS (one column per
 // lane: entry e of lane t at lds[e % S][t], conflict-free for ds_read_b64),
-// older entries spill to the lane's slice of a global buffer.
+// older entries spill to a global buffer interleaved over the lanes of the
+// grid (spill entry e of lane g at spill[e * stride + g]), so lanes of a wave
+// at the same depth share cache lines instead of each dirtying its own.
 template <int S>
 struct LaneStack {
     uint2 (*lds)[256];
-    uint2* spill;
+    uint2* spill;     // this lane's column: aux.spill + global lane index
+    uint32_t stride;  // lanes of the grid (aux.grid * 256)
     int tid;
     int top;
+    __device__ __forceinline__ void attach(uint2 (*l)[256], const RtLaunchAux& aux, int t) {
+        lds = l;
+        spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + (size_t)t);
+        stride = (uint32_t)aux.grid * 256u;
+        tid = t;
+        top = 0;
+    }
     __device__ __forceinline__ void push(uint32_t ref, float t) {
         const int slot = top & (S - 1);
-        if (top >= S) spill[top - S] = lds[slot][tid];
+        if (top >= S) spill[(size_t)(top - S) * stride] = lds[slot][tid];
         lds[slot][tid] = make_uint2(ref, __float_as_uint(t));
         top++;
     }
@@ -445,7 +455,7 @@ struct LaneStack {
         top--;
         const int slot = top & (S - 1);
         const uint2 e = lds[slot][tid];
-        if (top >= S) lds[slot][tid] = spill[top - S];
+        if (top >= S) lds[slot][tid] = spill[(size_t)(top - S) * stride];
         return e;
     }
 };

@@ -142,7 +142,10 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
 #ifndef RT_QNODES
 #define RT_QNODES 1
 #endif
-template <int W, int S>
+// COUNT (the counting pass, RT_FLAG_COUNT, W = 8 only): per-lane node steps,
+// triangle pre-filter and fp64 tests summed into the fetch counters for the
+// roofline's algorithmic bytes (bench.py --paths).
+template <int W, int S, bool COUNT = false>
 __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
                                                int bounces) {
     __shared__ uint2 lds[S][256];
@@ -154,10 +157,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
     const int tiles_x = (fp.W + 7) >> 3;
     const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
     LaneStack<S> st;
-    st.lds = lds;
-    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
-    st.tid = tid;
-    st.top = 0;
+    st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
     for (;;) {
         int tile = 0;
@@ -167,6 +167,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         const int i = (tile % tiles_x) * 8 + (lane & 7);
         const int r = (tile / tiles_x) * 8 + (lane >> 3);
         uint32_t hits = 0, segs = 0;  // segs: ray segments traced (RT_FLAG_COUNT)
+        LaneCounts tot;               // COUNT: the lane's fetch counts over its paths
         if (i < fp.W && r < fp.nrows) {
             const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
             const size_t pix = (size_t)r * fp.W + i;
@@ -185,13 +186,19 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                 for (int b = 0; b <= bounces; b++) {
                     LaneCounts lc;
 #if RT_PATHS_DEFER
-                    const Win win = trace_deferred<W, S, RT_PATHS_K, false, W == 8 && RT_QNODES>(
+                    const Win win = trace_deferred<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES>(
                         sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, pcand, lc);
 #else
                     const Win win =
-                        trace_core<W, S, false>(sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, 0, lc);
+                        trace_core<W, S, COUNT>(sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, 0, lc);
 #endif
                     segs++;
+                    if (COUNT) {
+                        tot.nodes += lc.nodes;
+                        tot.pre += lc.pre;
+                        tot.tris += lc.tris;
+                        tot.chain += lc.chain;
+                    }
                     Best hb;
                     hb.dist = win.dist;
                     hb.rank = win.rank;
@@ -229,5 +236,11 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         }
         wave_add<13>(fp.hit_count, hits);
         if (fp.counters) wave_add<20>(fp.counters, segs);
+        if (COUNT && fp.counters) {
+            wave_add<24>(fp.counters + 1, tot.nodes);
+            wave_add<24>(fp.counters + 6, tot.pre);
+            wave_add<24>(fp.counters + 2, tot.tris);
+            wave_add<24>(fp.counters + 3, tot.chain);
+        }
     }
 }

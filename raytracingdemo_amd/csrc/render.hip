@@ -615,10 +615,7 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
     const uint32_t n = n_sh;
     if (n == 0) return;
     LaneStack<S> st;
-    st.lds = lds;
-    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
-    st.tid = tid;
-    st.top = 0;
+    st.attach(lds, aux, tid);
     const uint32_t npix = (uint32_t)fp.W * (uint32_t)fp.nrows;
     // (grid-stride over the redo list; every thread reaches the exit test)
     for (uint32_t e = blockIdx.x * 256u + (uint32_t)tid; e < n; e += gridDim.x * 256u) {
@@ -641,10 +638,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace_exact(RtDevScene sc, RtFram
     const int tiles_x = (fp.W + 7) >> 3;
     const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
     LaneStack<S> st;
-    st.lds = lds;
-    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
-    st.tid = tid;
-    st.top = 0;
+    st.attach(lds, aux, tid);
     for (;;) {
         int tile = 0;
         if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);
@@ -1015,7 +1009,12 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     switch (sc.width) {
         case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
-        case 8: hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 8:
+            if (fp.counters)  // the counting pass: fetch counts too
+                hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+            else
+                hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+            break;
         case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         default: return hipErrorInvalidValue;
     }

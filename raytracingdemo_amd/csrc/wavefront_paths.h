@@ -72,10 +72,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(RtDevScene sc, RtFrameParams fp
     // the next stage's queue count (walk b and shade b - 1 are done with it)
     if (blockIdx.x == 0 && tid == 0) ws.ctl[(b + 1) & 1] = 0;
     LaneStack<S> st;
-    st.lds = lds;
-    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
-    st.tid = tid;
-    st.top = 0;
+    st.attach(lds, aux, tid);
     const uint32_t n = b == 0 ? ws.P : ws.ctl[b & 1];
     const size_t P = ws.P;
     for (;;) {
@@ -116,10 +113,7 @@ __global__ void __launch_bounds__(256) k_pw_shade(RtDevScene sc, RtFrameParams f
     // walk b + 1 starts its cursor from zero (walk b is done with it)
     if (blockIdx.x == 0 && tid == 0) ws.ctl[2] = 0;
     LaneStack<S> st;
-    st.lds = lds;
-    st.spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + tid) * aux.spill_cap;
-    st.tid = tid;
-    st.top = 0;
+    st.attach(lds, aux, tid);
     const uint32_t n = b == 0 ? ws.P : ws.ctl[b & 1];
     const size_t P = ws.P;
     const RtFrameCam cam = frame_cam(fp, 0);

@@ -32,7 +32,7 @@ for s in $STEPS; do
         rehearse) RT_BENCH_REHEARSE=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                       --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu ;;
         spp4)  run bench_spp4 300 python bench.py --no-cpu --steps 5 --spp 4 ;;
-        paths) run bench_paths 300 python bench.py --no-cpu --paths --steps 3 --warmup 1 ;;
+        paths) run bench_paths 300 python bench.py --paths --steps 3 --warmup 1 ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
                    -- python bench.py --steps 3 --warmup 1 --no-cpu --no-dropin ;;
         pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
@@ -41,6 +41,14 @@ for s in $STEPS; do
                    -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin && \
                python tools/pmc_traffic.py gpurun_out/pmc/fetch_counter_collection.csv \
                    gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
+        pmcpaths) run pmcp 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmcp -o fetch \
+                   -- python bench.py --paths --steps 1 --warmup 0 --no-cpu --key-out gpurun_out/pmcp_key.txt && \
+               run pmcpw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcp -o write \
+                   -- python bench.py --paths --steps 1 --warmup 0 --no-cpu && \
+               python tools/pmc_traffic.py gpurun_out/pmcp/fetch_counter_collection.csv \
+                   gpurun_out/pmcp/write_counter_collection.csv gpurun_out/pmcp_key.txt gpurun_out/pmc_traffic_paths.json k_paths ;;
+        profpaths) run profp 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profp -o paths \
+                   -- python bench.py --paths --steps 3 --warmup 1 --no-cpu ;;
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}" 300 \
                           python bench.py --no-cpu --no-dropin --steps 10 || exit 1; done ;;

@@ -10,7 +10,8 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports
 half of the bytes of wide coalesced reads (128-B requests tallied at 64 B), so
 read bytes = 2 x FETCH_SIZE; WRITE_SIZE is taken as is.
 
-Usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV KEY_FILE OUT_JSON
+Usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV KEY_FILE OUT_JSON [KERNEL]
+(KERNEL: k_trace_packet, the default, or k_paths for config c5)
 """
 import collections
 import csv
@@ -21,9 +22,9 @@ import sys
 
 
 def counting(name):
-    """k_trace_packet<W, SP, K, COUNT, FUSED>: the COUNT instantiation is the
-    counting pass, not the timed kernel."""
-    m = re.search(r"k_trace_packet<\d+, \d+, \d+, (true|false)", name)
+    """k_trace_packet<W, SP, K, COUNT, FUSED> / k_paths<W, S, COUNT>: the COUNT
+    instantiation is the counting pass, not the timed kernel."""
+    m = re.search(r"k_trace_packet<\d+, \d+, \d+, (true|false)", name) or re.search(r"k_paths<\d+, \d+, (true|false)", name)
     return bool(m and m.group(1) == "true")
 
 
@@ -40,7 +41,7 @@ def per_dispatch(path, kernel_sub):
 def main():
     fetch_csv, write_csv, key_file, out = sys.argv[1:5]
     key = open(key_file).read().strip()
-    kern = "k_trace_packet"
+    kern = sys.argv[5] if len(sys.argv) > 5 else "k_trace_packet"
     f = per_dispatch(fetch_csv, kern)
     w = per_dispatch(write_csv, kern)
     if not f or not w:

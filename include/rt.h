@@ -20,6 +20,12 @@
  * std::out_of_range "Unknown algorithm"; object_loader.hpp:17
  * std::runtime_error "Failed to load OBJ file") the same message text is
  * returned with the matching status.  Nothing crosses the ABI as an exception.
+ *
+ * Threading: a scene's geometry is immutable after rt_scene_create.  Any
+ * number of host threads may call the render and stats entry points on one
+ * scene; the scene's lock serialises the calls that touch its per-device
+ * buffers (a caller stream still runs its launches asynchronously).
+ * rt_scene_destroy must not race with other calls on the same scene.
  */
 #ifndef RT_MI355X_H
 #define RT_MI355X_H

@@ -259,9 +259,9 @@ def test_row_shards_reassemble_to_full_frame():
 
 @pytest.mark.parametrize("mode", ["exact", "fp64"])
 def test_batched_frames_equal_single_frames(mode):
-    """rt_render_batch_device over 27 poses (two launches: 18 + 9 frames)
-    of a row shard equals 27 single-frame renders: ids, distances, positions,
-    colours and per-frame hit counts, bit for bit."""
+    """rt_render_batch_device over 27 poses (one launch; up to 36 poses fit
+    one) of a row shard equals 27 single-frame renders: ids, distances,
+    positions, colours and per-frame hit counts, bit for bit."""
     torch = pytest.importorskip("torch")
     tris = golden_scene("stanford-bunny.obj")
     s = scene("stanford-bunny.obj", "bsah", 8)
@@ -568,3 +568,54 @@ def test_band_shards_reassemble_to_full_frame():
             assert np.array_equal(img_id[f].cpu().numpy().view(np.uint32).reshape(-1), full[f]["hit_id"]), (G, f)
             assert np.array_equal(img_rgb[f].cpu().numpy().reshape(-1, 3), full[f]["rgb"]), (G, f)
             assert int(cnt[:, f].sum()) == full[f]["hits"], (G, f)
+
+
+def test_concurrent_callers_on_one_scene():
+    """Two host threads drive one scene at once (rt_render_frame, blocking,
+    and rt_render_batch_device on their own streams; ctypes drops the GIL in
+    the calls): the library serialises them on the scene's lock and every
+    result equals the sequential one (include/rt.h threading note)."""
+    import threading
+
+    torch = pytest.importorskip("torch")
+    tris = golden_scene("stanford-bunny.obj")
+    s = scene("stanford-bunny.obj", "bsah", 8)
+    path = rt.CameraPath(rt.scene_center(tris), 36)
+    cams = [path.circular_path(f) for f in range(12)]
+    W, H = 200, 120
+    ref = [s.calculate_screen(p, d, W, H, want=("hit_id", "rgb")) for p, d in cams]
+    errors: list = []
+
+    def frames(k):
+        try:
+            out = None
+            for it in range(3):
+                for f in range(k, len(cams), 2):
+                    out = s.calculate_screen(*cams[f], W, H, want=("hit_id", "rgb"), out=out)
+                    assert np.array_equal(out["hit_id"], ref[f]["hit_id"]), (k, it, f)
+                    assert np.array_equal(out["rgb"], ref[f]["rgb"]), (k, it, f)
+        except BaseException as e:  # reported by the main thread
+            errors.append(e)
+
+    def batches():
+        try:
+            st = torch.cuda.Stream()
+            t_id = torch.empty(len(cams) * W * H, dtype=torch.int32, device="cuda:0")
+            for it in range(3):
+                s.render_batch_device(0, cams, W, H, 0, 1, H, hit_id=t_id.data_ptr(), stream=st.cuda_stream)
+                st.synchronize()
+                got = t_id.cpu().numpy().view(np.uint32).reshape(len(cams), -1)
+                for f in range(len(cams)):
+                    assert np.array_equal(got[f], ref[f]["hit_id"]), ("batch", it, f)
+        except BaseException as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=frames, args=(0,)), threading.Thread(target=frames, args=(1,)),
+          threading.Thread(target=batches)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a caller thread hung"
+    if errors:
+        raise errors[0]

@@ -176,3 +176,18 @@ def test_scene_cache_returns_the_loader_output(tmp_path):
     assert not hit_e and len(e) == len(c) + 1
     with pytest.raises(rt.RTError, match="Failed to load OBJ file"):
         rt.load_obj_cached(str(tmp_path / "missing.obj"), 1.0, str(cache))
+
+
+def test_calculate_screen_rejects_mismatched_output_arrays():
+    """calculate_screen(out=...) reuses the caller's host arrays (runTest's
+    reused ray_hits); a wrong shape or dtype is refused before any device call."""
+    s = rt.Scene(golden_scene("teapot.obj"), "bsah", 2)
+    W, H = 16, 8
+    ok = {"hit_id": np.empty(W * H, np.uint32), "dist": np.empty(W * H), "pos": None,
+          "rgb": np.empty((W * H, 3), np.uint8)}
+    for key, bad in [("hit_id", np.empty(W * H, np.int64)), ("dist", np.empty(W * H + 1)),
+                     ("rgb", np.empty((W * H, 3), np.uint8)[:, ::-1])]:
+        out = dict(ok)
+        out[key] = bad
+        with pytest.raises(ValueError, match=key):
+            s.calculate_screen([0, 0, 5], [0, 0, -1], W, H, out=out)

@@ -140,7 +140,10 @@ typedef struct {
                                   recorded around it on the launch stream) */
 } rt_frame_stats_t;
 
-/* Host time of each stage of rt_scene_create (std::chrono, ms). */
+/* Host time of each stage of rt_scene_create (std::chrono, ms).  With the
+ * walk tree built on a device (rt_scene_create_on_device) the two trees are
+ * built at the same time (the reference tree on host threads), so their times
+ * overlap: total_ms = soup + max(reference tree, walk tree) + flatten. */
 typedef struct {
     double soup_ms;           /* triangle set-up (triangle.hpp:14-19)                 */
     double reference_tree_ms; /* StackBVH::build + collapse (stack_bvh.hpp:502-608)   */
@@ -148,6 +151,7 @@ typedef struct {
     double flatten_ms;        /* wide nodes, records, ranks and chains                */
     int32_t walk_device;      /* device that built the walk tree, -1 = host           */
     int32_t reserved;
+    double total_ms;          /* wall time of the whole rt_scene_create               */
 } rt_build_times_t;
 
 /* objl::Loader + ObjectLoader::loadFromFile (object_loader.hpp:14-70,

@@ -81,7 +81,8 @@ class rt_frame_stats_t(C.Structure):
 
 class rt_build_times_t(C.Structure):
     _fields_ = [("soup_ms", C.c_double), ("reference_tree_ms", C.c_double), ("walk_tree_ms", C.c_double),
-                ("flatten_ms", C.c_double), ("walk_device", C.c_int32), ("reserved", C.c_int32)]
+                ("flatten_ms", C.c_double), ("walk_device", C.c_int32), ("reserved", C.c_int32),
+                ("total_ms", C.c_double)]
 
 
 _lib = None

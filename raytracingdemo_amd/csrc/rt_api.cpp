@@ -12,7 +12,9 @@
 #include <cstring>
 #include <limits>
 #include <memory>
+#include <exception>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <array>
 #include <vector>
@@ -783,35 +785,60 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
         const auto t0 = clk::now();
         s->soup = rt::make_soup(tri_v, n);
         const auto t1 = clk::now();
-        s->tree = rt::build_tree(s->soup, algo, k, collapse);
-        const auto t2 = clk::now();
-        auto t3 = t2;
         // the device walks a rebuilt SAH tree (walk_tree.cpp) unless
         // RT_WALK=reference asks for the reference tree's own nodes
         const char* wk = std::getenv("RT_WALK");
         s->times.walk_device = -1;
+        auto t2 = t1, t3 = t1;
         if (wk && wk[0] == 'r') {
+            s->tree = rt::build_tree(s->soup, algo, k, collapse);
+            t2 = t3 = clk::now();
             s->flat = rt::flatten(s->soup, s->tree, 0);
         } else {
-            rt::WalkTree wt;
             if (walk_device >= 0) {
                 int count = 0;
                 if (hipGetDeviceCount(&count) != hipSuccess || walk_device >= count)
                     return fail(RT_ERR_NO_DEVICE, "bad device ordinal for the walk-tree build");
-                wt = rt::build_walk_tree_device(s->soup, walk_device, rt::walk_max_leaf(), rt::walk_node_cost());
-                s->times.walk_device = walk_device;
-            } else {
-                wt = rt::build_walk_tree(s->soup);
             }
-            t3 = clk::now();
+            rt::WalkTree wt;
+            if (walk_device >= 0) {
+                // the two trees are independent (both read only the soup): the
+                // reference tree builds on host threads while this thread
+                // drives the device build of the walk tree (mostly waiting)
+                std::exception_ptr tree_err;
+                std::thread ref([&] {
+                    try {
+                        s->tree = rt::build_tree(s->soup, algo, k, collapse);
+                    } catch (...) { tree_err = std::current_exception(); }
+                    t2 = clk::now();
+                });
+                try {
+                    wt = rt::build_walk_tree_device(s->soup, walk_device, rt::walk_max_leaf(), rt::walk_node_cost());
+                } catch (...) {
+                    ref.join();
+                    throw;
+                }
+                s->times.walk_device = walk_device;
+                t3 = clk::now();
+                ref.join();
+                if (tree_err) std::rethrow_exception(tree_err);
+            } else {
+                // host walk build: one after the other (both want the host's
+                // cores and memory bandwidth)
+                s->tree = rt::build_tree(s->soup, algo, k, collapse);
+                t2 = clk::now();
+                wt = rt::build_walk_tree(s->soup);
+                t3 = clk::now();
+            }
             s->flat = rt::flatten(s->soup, s->tree, 0, &wt);
         }
         const auto t4 = clk::now();
         s->literal_stack = literal_stack_bound(s.get());
         s->times.soup_ms = ms(t0, t1);
         s->times.reference_tree_ms = ms(t1, t2);
-        s->times.walk_tree_ms = ms(t2, t3);
-        s->times.flatten_ms = ms(t3, t4);
+        s->times.walk_tree_ms = walk_device >= 0 ? ms(t1, t3) : ms(t2, t3);
+        s->times.flatten_ms = ms(std::max(t2, t3), t4);
+        s->times.total_ms = ms(t0, t4);
         *out = s.release();
         return RT_OK;
     } catch (const rt::Error& e) {

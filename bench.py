@@ -103,13 +103,18 @@ def parse():
     return a
 
 
-def cpu_baseline(tris, algo, k, cams, W, H, target_s):
+def cpu_baseline(tris, algo, k, cams, W, H, target_s, gpu=None):
     """Reference traversal (oracle/_ref: the reference's own headers compiled -O3,
     OpenMP over pixel columns; the timed scope of runTest, src/main.cpp:253-255)
     or, without it, the oracle restatement, in two legs: every host core this
     process may use (the cgroup quota on the GPU box) and one core.  Bounded
     samples: whole frames of the same camera orbit until ~target_s of CPU time
-    (all cores), ~target_s / 3 (one core: whole rows, a frame is ~3 s there)."""
+    (all cores), ~target_s / 3 (one core: whole rows, a frame is ~3 s there).
+
+    gpu: the timed step's outputs (numpy hit ids, distances, colours and hit
+    counts per pose, N = 1): every whole frame the reference renders here is
+    compared with them — hit mask, |hit - o| from its fp64 hit point (the
+    stack_bvh.hpp:631 expression), PPM bytes and hit count."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     host = host_cores()
@@ -120,13 +125,28 @@ def cpu_baseline(tris, algo, k, cams, W, H, target_s):
         lib, kind = pyoracle.Oracle(), "port"
     b = lib.bvh(tris, algo, k)
     frames, rays, spent = 0, 0, 0.0
+    check = {"frames": 0, "pixels": 0, "hit_mask_diff": 0, "dist_diff": 0, "rgb_diff": 0, "count_diff": 0}
     while spent < target_s and frames < len(cams) * 4:
-        pos, d = cams[frames % len(cams)]
+        f = frames % len(cams)
+        pos, d = cams[f]
         t0 = time.perf_counter()
-        b.render(pos, d, W, H, threads=threads)
+        o = b.render(pos, d, W, H, threads=threads)
         spent += time.perf_counter() - t0
         frames += 1
         rays += W * H
+        if gpu is not None and frames <= len(cams):  # (outside the timed CPU work)
+            hit = o["hit"] if "hit" in o else o["id"] >= 0
+            g_hit = gpu["ids"][f] != -1
+            p = np.asarray(pos, dtype=np.float64)
+            dx, dy, dz = (o["pos"][:, a] - p[a] for a in range(3))
+            rdist = np.sqrt(dx * dx + dy * dy + dz * dz)
+            check["frames"] += 1
+            check["pixels"] += W * H
+            check["hit_mask_diff"] += int(np.count_nonzero(hit != g_hit))
+            both = hit & g_hit
+            check["dist_diff"] += int(np.count_nonzero(rdist[both] != gpu["dist"][f][both]))
+            check["rgb_diff"] += int(np.count_nonzero(np.any(o["rgb"] != gpu["rgb"][f], axis=1)))
+            check["count_diff"] += int(o["hits"] != int(gpu["cnt"][f]))
     # one core: bands of 60 rows spread over the orbit's frames
     rows1, spent1, f1 = 0, 0.0, 0
     while spent1 < target_s / 3 and f1 < len(cams) * (H // 60):
@@ -145,6 +165,9 @@ def cpu_baseline(tris, algo, k, cams, W, H, target_s):
             "one_core": {"value": round(one, 4), "cores": 1,
                          "sample": f"{f1} bands of 60 rows x {W} px over the orbit ({rows1 * W} rays, {spent1:.1f} s)"},
             "host": host,
+            **({"verified_timed_frames": dict(check, equal=not any(v for kk, v in check.items()
+                                                                     if kk.endswith("_diff")))}
+               if gpu is not None else {}),
             "published_O0": {"value": None, "note": "no published Sponza figure for the current code; the only "
                              "Sponza datum is an older-code run (testruns_2025_12_25/testrun_47: 105.58 s mean per "
                              "500x500 frame, 0.0024 Mrays/s, -O0, 1 core; not comparable). Published -O0 1-core "
@@ -562,7 +585,14 @@ def main():
         if world == 1 and not a.no_dropin and S == 1:
             dropin = dropin_rate(scene, cams, W, H, mode)
         if world == 1 and not a.no_cpu:
-            cpu = cpu_baseline(tris, a.algo, a.k, cams, W, H, a.cpu_seconds)
+            # the timed step's frames (buffer set 0, the last step at N = 1)
+            # checked against the reference frames the baseline renders
+            gpu = None
+            if S == 1 and sworld == 1 and F <= 36:
+                gpu = {"ids": ids[0][:, :H, :, 0].reshape(F, H * W).cpu().numpy(),
+                       "dist": dists[:, :H, :, 0].reshape(F, H * W).cpu().numpy(),
+                       "rgb": rgb[0][:, :H].reshape(F, H * W, 3).cpu().numpy(), "cnt": cnt[0].cpu().numpy()}
+            cpu = cpu_baseline(tris, a.algo, a.k, cams, W, H, a.cpu_seconds, gpu=gpu)
         line = {
             "metric": METRIC if S == 1 else METRIC.replace("1spp", f"{S}spp"), "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,

@@ -425,7 +425,7 @@ def main():
 
     def render(b, timing=False, count=False):
         # the whole camera orbit in one batched call (the library launches up
-        # to 18 frames per traversal / resolve / fix-up launch)
+        # to 36 frames per walk / fix-up launch)
         if shipped[b] is not None:
             stream.wait_event(shipped[b])  # set b's previous gather has read it
         cnt[b].zero_()
@@ -545,7 +545,7 @@ def main():
     frames_timed = a.steps * F
     frame_s = elapsed / frames_timed
     # dominant (traversal) kernel, HIP events around each of its launches
-    # (one launch = up to 18 frames); without library timing, whole frames
+    # (one launch = up to 36 frames); without library timing, whole frames
     trace_s = ks["trace_ms"] * 1e-3 if ks["timed_launches"] else elapsed
     avg_kernel_s = trace_s / launches_timed if ks["timed_launches"] else frame_s
     frames_per_launch = frames_timed / launches_timed if ks["timed_launches"] else 1.0

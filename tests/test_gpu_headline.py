@@ -1,6 +1,6 @@
 """GPU parity at the benchmarked sizes: the exact workload bench.py times
 (sponza proxy, 1920x1080, bsah-8, the 36-pose orbit of runTest in one
-rt_render_batch_device call, 18 poses per launch) against the oracle on full
+rt_render_batch_device call, 36 poses per launch) against the oracle on full
 frames, pixel for pixel; config c4 (4 spp) on full frames; config c3
 (armadillo) where its geometry is supplied; and the candidate-overflow pool
 running dry.  Reference: StackBVH::traverse (src/stack_bvh.hpp:611-644),

@@ -40,6 +40,7 @@ WIN_BYTES = 56         # the winner's normal, {id, leaf} and leaf box, once per 
 CHAIN_BYTES = 52       # fp64 box (48 B) + parent (4 B) per re-verified ancestor
 OUT_BYTES = 15         # u32 hit-id + f64 distance + 3 B rgb written per ray
 CAND_BYTES = 8         # one candidate entry {triangle, t bound} handed to the resolve kernel
+SAMPLE_BYTES = 37      # spp > 1, fused: u32 hit-id + f64 distance + the sample's f64 colour + status byte
 
 
 def host_cores():
@@ -483,15 +484,17 @@ def main():
     # SURVEY.md 8(d)'s per-ray figure: what each ray's own traversal touches
     survey_bytes_per_ray = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
                             cs["rays"] * OUT_BYTES) / max(cs["rays"], 1)
-    fused = cs["wave_tiles"] and S == 1 and os.environ.get("RT_RESOLVE", "")[:1] != "s"
+    fused = cs["wave_tiles"] and os.environ.get("RT_RESOLVE", "")[:1] != "s"
     if fused:
         # packet traversal kernel with the fused resolve (the dominant kernel):
         # a node or triangle record is fetched once per wave for its 64 rays;
         # per ray the Moller-Trumbore part of each exact test, the winner's
         # shading fields, the ancestor boxes re-verified and the outputs
         # (rays are generated in-kernel: no camera reads)
+        # (spp > 1: per sample its outputs, colour and status for k_average)
         trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES + cs["tri_tests"] * MT64_BYTES +
-                       cs["hits"] * WIN_BYTES + cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * OUT_BYTES)
+                       cs["hits"] * WIN_BYTES + cs["chain_nodes"] * CHAIN_BYTES +
+                       cs["rays"] * (OUT_BYTES if S == 1 else SAMPLE_BYTES))
     elif cs["wave_tiles"]:
         # packet traversal kernel, split resolve: the walk plus the candidate
         # lists it writes

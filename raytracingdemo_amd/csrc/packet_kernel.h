@@ -96,6 +96,10 @@ constexpr int kLeafChunk = 2;
 constexpr uint32_t kCandDropped = 0x80;  // cand_cnt flag: candidates were dropped (bound in cand_drop)
 constexpr uint32_t kCandSpilled = 0x40;  // cand_cnt flag: entries in an overflow pool chunk (cand_ovf)
 constexpr uint32_t kCandCount = 0x3F;    // cand_cnt: entries in slots [0, count)
+// spp > 1 with the fused resolve: cand_cnt holds each sample's status for
+// k_average (bit 0: a hit; kSampRedo: not resolved, the pixel goes to k_fixup)
+// and cand the sample's colour (3 doubles at 3 * sample pixel)
+constexpr uint32_t kSampRedo = 0x80;
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;   // lane has no overflow chunk (yet)
 constexpr uint32_t kPoolDry = 0xFFFFFFFEu;   // the pool ran out: drop with a certified bound
 static_assert(kLeafChunk <= RT_TRI32_PAD, "tri32 padding must cover a leaf chunk");
@@ -518,16 +522,18 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         reinterpret_cast<RT_G uint2*>(aux.pool)[(size_t)chunk * RT_POOL_CHUNK + nsp] = make_uint2(~0u, 0u);
     const bool spilled = chunk != kNoChunk && chunk != kPoolDry && nsp > 0;
     if constexpr (FUSED) {
-        // the tile's own lanes resolve their lists (spp = 1: frame f = pose
-        // f), compacted against the final culling distance first (an entry
-        // beyond it cannot beat a certain hit)
+        // the tile's own lanes resolve their lists (frame f = sample f % spp
+        // of pose f / spp), compacted against the final culling distance
+        // first (an entry beyond it cannot beat a certain hit)
         uint32_t nl = 0;
         for (int c = 0; c < nc; c++) {
             const uint2 e = cand[c * 64 + lane];
             if (__uint_as_float(e.y) <= tcull) cand[nl++ * 64 + lane] = e;
         }
         const RtDevScene sc = kload(&A->sc);
-        const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f]), fp, f);  // (spp = 1: pose f)
+        const int spp = fp.spp;
+        const int pose = f / spp;
+        const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[pose]), fp, f);
         Best out;
         Shade sh;
         ResolveCounts rc;
@@ -536,23 +542,44 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         const uint32_t redo = resolve_list<COUNT>(
             sc, fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r), nl, nl ? cand[lane] : make_uint2(0u, 0u),
             [&](uint32_t c) { return cand[c * 64 + lane]; }, ch, dropped, drop, out, sh, rc);
-        if (redo) {
-            // k_fixup redoes the pixel with the exact per-lane path
-            const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-            aux.redo[slot] = ob | (redo == 2u ? kRedoPass1 : 0u);
+        const bool hit_s = !redo && out.tri >= 0;
+        if (spp == 1) {
+            if (redo) {
+                // k_fixup redoes the pixel with the exact per-lane path
+                const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
+                aux.redo[slot] = ob | (redo == 2u ? kRedoPass1 : 0u);
+            } else {
+                store_sample(fp, ob, out, sh);
+                double c[3];
+                shade_color(cam, out, sh, c);
+                store_rgb(fp, ob, c);
+                res.hit = hit_s;
+            }
         } else {
-            store_sample(fp, ob, out, sh);
-            double c[3];
-            shade_color(cam, out, sh, c);
-            store_rgb(fp, ob, c);
-            res.hit = out.tri >= 0;
+            // one sample of a pixel: its outputs at sample index pix * spp + k
+            // (k_resolve's layout), its colour and status for k_average,
+            // which sums the pixel's samples in order and counts its hits
+            if (redo) {
+                aux.cand_cnt[ob] = (uint8_t)kSampRedo;
+            } else {
+                const size_t fpix = (size_t)fp.W * (size_t)fp.nrows;
+                const size_t po = (size_t)ob - (size_t)f * fpix;
+                store_sample(fp, out_index(fp, pose, po) * (size_t)spp + (size_t)(f - pose * spp), out, sh);
+                double c[3];
+                shade_color(cam, out, sh, c);
+                RT_G double* const col = reinterpret_cast<RT_G double*>(aux.cand) + (size_t)ob * 3;
+                col[0] = c[0];
+                col[1] = c[1];
+                col[2] = c[2];
+                aux.cand_cnt[ob] = (uint8_t)(hit_s ? 1u : 0u);
+            }
         }
         if (COUNT && fp.counters) {
             atomicAdd(&fp.counters[0], 1ull);
             atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
             atomicAdd(&fp.counters[2], (unsigned long long)rc.tris);
             atomicAdd(&fp.counters[3], (unsigned long long)rc.chain);
-            if (res.hit) atomicAdd(&fp.counters[4], 1ull);
+            if (hit_s) atomicAdd(&fp.counters[4], 1ull);
             atomicAdd(&fp.counters[5], (unsigned long long)rc.chain_nodes);
             atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
             if (redo == 1) atomicAdd(&fp.counters[10], 1ull);
@@ -680,9 +707,60 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
     }
 }
 
+// spp > 1 behind the fused walk: one thread per pixel of a pose sums its
+// samples' colours in sample order (k_resolve's order, so the bytes are the
+// same), stores the PPM bytes and counts the samples hit; a pixel with a
+// sample the walk kernel could not resolve goes to k_fixup whole (its hits are
+// counted there).  Blocks never straddle poses.
+__global__ void __launch_bounds__(256) k_average(RtFrameParams fp, RtLaunchAux aux) {
+    __shared__ uint32_t wave_hits[4];
+    const uint32_t fpix = (uint32_t)fp.W * (uint32_t)fp.nrows;
+    const uint32_t bpf = (fpix + 255u) >> 8;  // blocks per pose
+    const int p = (int)(blockIdx.x / bpf);
+    const uint32_t fb = blockIdx.x - (uint32_t)p * bpf;
+    const uint32_t po = fb * 256u + threadIdx.x;
+    const int spp = fp.spp;
+    uint32_t hits = 0;
+    if (po < fpix) {
+        bool redo = false;
+        double acc[3] = {0.0, 0.0, 0.0};
+        for (int k = 0; k < spp; k++) {
+            const size_t o = out_index(fp, p * spp + k, po);
+            const uint32_t st = aux.cand_cnt[o];
+            if (st & kSampRedo) {
+                redo = true;
+                continue;
+            }
+            const RT_G double* const col = reinterpret_cast<const RT_G double*>(aux.cand) + o * 3;
+            acc[0] = acc[0] + col[0];
+            acc[1] = acc[1] + col[1];
+            acc[2] = acc[2] + col[2];
+            hits += st & 1u;
+        }
+        const size_t pix = out_index(fp, p, po);
+        if (redo) {
+            const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
+            aux.redo[slot] = (uint32_t)pix;
+            hits = 0;
+        } else {
+            store_rgb(fp, pix, acc);
+        }
+    }
+    uint32_t wsum = 0;
+#pragma unroll
+    for (int b = 0; b < 7; b++) wsum += (uint32_t)__builtin_popcountll(__ballot((hits >> b) & 1u)) << b;
+    if ((threadIdx.x & 63) == 0) wave_hits[threadIdx.x >> 6] = wsum;
+    __syncthreads();
+    if (threadIdx.x == 0 && fp.hit_count) {
+        const uint32_t sum = wave_hits[0] + wave_hits[1] + wave_hits[2] + wave_hits[3];
+        if (sum) atomicAdd(aux.tile_ctr + RT_HIT_BASE + (p * RT_HIT_SLOTS + fb % RT_HIT_SLOTS) * RT_QUEUE_STRIDE, sum);
+    }
+}
+
 // Persistent waves over 8x8 tiles; the stack bound of the tree must fit SP
 // (the host falls back to the per-lane kernel otherwise), so no push can drop.
-// FUSED (spp = 1): each tile is resolved, shaded and stored by its own wave.
+// FUSED: each tile is resolved, shaded and stored by its own wave (spp > 1:
+// each sample; k_average then forms the pixels).
 // Waves per workgroup of the packet kernel (4: seven workgroups per CU at 7
 // waves/SIMD).  7-wave workgroups (4 per CU, the LDS argument block shared by
 // 7 waves) measured 5% slower: a workgroup's waves land unevenly on the 4

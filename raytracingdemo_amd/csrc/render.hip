@@ -776,11 +776,16 @@ RtFrameParams single_pose(const RtFrameParams& fp, int p) {
 // kernel's tile epilogue (default) or, with RT_RESOLVE=split, the separate
 // k_resolve pass over candidate lists in HBM (the spp > 1 path; kept for
 // A/B measurement).  Read per call (tests switch it in-process).
+// RT_RESOLVE=split: the walk hands candidate lists to k_resolve through HBM
+// (the A/B reference for the fused resolve), for any spp
 bool split_resolve(int spp) {
-    if (spp > 1) return true;
+    (void)spp;
     const char* e = getenv("RT_RESOLVE");
     return e && e[0] == 's';
 }
+// the packet pipeline needs the candidate buffers: the split resolve's lists,
+// or spp > 1 with the fused resolve (each sample's colour and status)
+bool needs_cand(int spp) { return spp > 1 || split_resolve(spp); }
 
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
@@ -799,6 +804,11 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
                 hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
+            if (fp.spp > 1) {
+                const uint64_t bpf = ((uint64_t)fp.W * (uint64_t)fp.nrows + 255) / 256;
+                hipLaunchKernelGGL(k_average, dim3((unsigned)(bpf * (uint64_t)(fp.nframes / fp.spp))), blk, 0, s, fp,
+                                   aux);
+            }
         } else {
             // k_resolve: one block per 16x16 tile, 8 XCD bands of T8 tiles per pose
             const uint64_t rt8 = (((uint64_t)(fp.W + 15) / 16) * ((uint64_t)(fp.nrows + 15) / 16) + 7) / 8;
@@ -887,7 +897,7 @@ int exact_lds_stack() {
     return a < RT_PW_STACK ? a : RT_PW_STACK;
 }
 int packet_candidates() { return RT_CAND_LDS; }  // HBM list entries per pixel (spp > 1, wavefront paths)
-bool packet_split(int spp) { return split_resolve(spp); }
+bool packet_split(int spp) { return needs_cand(spp); }
 uint32_t params_bytes() { return (uint32_t)sizeof(RtFrameParams); }
 
 // Host entry: validates the launch geometry against what the kernels assume
@@ -927,7 +937,7 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     if (use_packet(sc.stack_bound) &&
         (!aux.redo || aux.redo_cap < bpix / (uint64_t)fp.spp || !aux.pool || aux.pgrid <= 0))
         return hipErrorInvalidValue;
-    if (use_packet(sc.stack_bound) && split_resolve(fp.spp) &&
+    if (use_packet(sc.stack_bound) && needs_cand(fp.spp) &&
         (!aux.cand || !aux.cand_cnt || !aux.cand_drop || !aux.cand_ovf || aux.cand_cap < bpix))
         return hipErrorInvalidValue;
     const bool packet = use_packet(sc.stack_bound);

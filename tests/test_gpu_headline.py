@@ -93,9 +93,10 @@ def test_headline_orbit_full_size_matches_oracle(oracle, monkeypatch):
 
 
 def test_config_c4_spp4_full_frames_match_oracle(oracle):
-    """Config c4 (2x2 stratified samples) on full 1080p frames of 6 poses (two
-    launches of 4 poses x 4 sample frames and 2 x 4): per-sample ids and
-    distances, averaged colours, per-pose sample hit counts."""
+    """Config c4 (2x2 stratified samples) on full 1080p frames of 6 poses (one
+    launch of 24 sample frames: each sample resolved in the walk kernel,
+    k_average forming the pixels): per-sample ids and distances, averaged
+    colours, per-pose sample hit counts."""
     tris, s = proxy()
     cams = orbit(tris)[::6]
     ids, dist, rgb, cnt = render_orbit(s, cams, spp=4)
@@ -146,6 +147,20 @@ def test_overflow_pool_and_dry_pool(oracle, monkeypatch, chunks):
     assert fs["dropped_rays"] > 0
     if chunks:
         assert fs["spilled_rays"] == 1  # the one chunk; every other lane dropped straight away
+    # 4 spp through the fused resolve: samples that overflow or cannot be
+    # certified send their whole pixel to k_fixup via k_average
+    sp = torch.empty(96 * 72 * 4, dtype=torch.int32, device="cuda:0")
+    rgb = torch.empty(96 * 72 * 3, dtype=torch.uint8, device="cuda:0")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    cam = [([0.0, 0.0, 3.0], [0.0, 0.0, -1.0])]
+    s.render_batch_device(0, cam, 96, 72, 0, 1, 72, hit_id=sp.data_ptr(), rgb=rgb.data_ptr(),
+                          hit_count=cnt.data_ptr(), stream=torch.cuda.current_stream().cuda_stream, spp=4)
+    torch.cuda.synchronize()
+    o = oracle.bvh(tris, "sah", 8).render_spp([0.0, 0.0, 3.0], [0.0, 0.0, -1.0], 96, 72, 4)
+    g4 = sp.cpu().numpy().view(np.uint32).reshape(-1, 4)
+    assert np.array_equal(np.where(g4 == rt.RT_MISS, -1, g4.astype(np.int64)), o["id"])
+    assert np.array_equal(rgb.cpu().numpy().reshape(-1, 3), o["rgb"])
+    assert int(cnt[0]) == o["hits"] > 0
 
 
 ARMADILLO = os.environ.get("RT_ARMADILLO_OBJ")

@@ -343,12 +343,17 @@ def _spp_render(s, cams, W, H, spp, row0=0, stride=1, nrows=None, mode="exact"):
             "rgb": t_rgb.cpu().numpy().reshape(F, npx, 3), "hits": t_cnt.cpu().numpy()}
 
 
-@pytest.mark.parametrize("mode", ["exact", "fp64"])
+@pytest.mark.parametrize("mode", ["exact", "fp64", "split"])
 @pytest.mark.parametrize("spp", [4, 9])
-def test_stratified_spp_matches_oracle(oracle, spp, mode):
+def test_stratified_spp_matches_oracle(oracle, spp, mode, monkeypatch):
     """spp = n*n stratified samples per pixel (config c4's 2x2 and a 3x3): every
     sample's hit id, distance and position, the averaged colour and the per-pose
-    hit count against the oracle; 5 poses span launch boundaries."""
+    hit count against the oracle; 5 poses span launch boundaries.  "exact" is
+    the fused resolve (each sample resolved in the walk kernel, k_average
+    forming the pixels), "split" the candidate lists handed to k_resolve."""
+    if mode == "split":
+        monkeypatch.setenv("RT_RESOLVE", "split")
+        mode = "exact"
     tris = golden_scene("stanford-bunny.obj")
     s = scene("stanford-bunny.obj", "bsah", 8)
     b = oracle.bvh(tris, "bsah", 8)

@@ -52,6 +52,10 @@ for s in $STEPS; do
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}" 300 \
                           python bench.py --no-cpu --no-dropin --steps 10 || exit 1; done ;;
+        pvariants) run bench_paths_base 300 python bench.py --paths --no-cpu --steps 3 --warmup 1 || exit 1
+                   for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
+                      n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_paths_${n#librtmi355x_}" 300 \
+                          python bench.py --paths --no-cpu --steps 3 --warmup 1 || exit 1; done ;;
         vshards) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}_s8" 300 \
                           python bench.py --no-cpu --no-dropin --steps 10 --shard-of 8 || exit 1; done ;;

@@ -538,6 +538,23 @@ def test_sharded_frames_through_the_abi_equal_one_device(monkeypatch, shards):
     assert np.array_equal(g["hit_id"], ref["id"].cpu().numpy().view(np.uint32).reshape(F, -1)[2])
     assert np.array_equal(g["rgb"].reshape(-1), ref["rgb"].cpu().numpy().reshape(F, -1)[2])
     assert g["hits"] == int(ref_cnt[2])
+    # 4 spp (config c4's multi-GPU case): per-sample outputs, averaged colours
+    # and sample hit counts through the same shards
+    monkeypatch.delenv("RT_VIRTUAL_SHARDS")
+    r4 = {"id": torch.empty(F * H * W * 4, dtype=torch.int32, device="cuda:0"),
+          "rgb": torch.empty(F * H * W * 3, dtype=torch.uint8, device="cuda:0")}
+    c4 = torch.zeros(F, dtype=torch.int64, device="cuda:0")
+    s.render_batch_device(0, cams, W, H, 0, 1, H, hit_id=r4["id"].data_ptr(), rgb=r4["rgb"].data_ptr(),
+                          hit_count=c4.data_ptr(), stream=st, spp=4)
+    monkeypatch.setenv("RT_VIRTUAL_SHARDS", str(shards))
+    g4 = {k: torch.full_like(v, 7) for k, v in r4.items()}
+    g4c = torch.zeros(F, dtype=torch.int64, device="cuda:0")
+    s.render_batch_multi(cams, W, H, hit_id=g4["id"].data_ptr(), rgb=g4["rgb"].data_ptr(), hit_count=g4c.data_ptr(),
+                         stream=st, spp=4)
+    torch.cuda.synchronize()
+    for k in r4:
+        assert torch.equal(g4[k], r4[k]), (shards, "spp4", k)
+    assert torch.equal(g4c, c4)
 
 
 def test_band_shards_reassemble_to_full_frame():

@@ -37,7 +37,9 @@
 // Work-queue block (RtLaunchAux::tile_ctr, RT_QUEUE_WORDS u32, zeroed per
 // launch): RT_QUEUES tile queues RT_QUEUE_STRIDE words apart (one per XCD,
 // separate cache lines), the redo-list length, and the hit-count partials.
+#ifndef RT_QUEUES
 #define RT_QUEUES 8
+#endif
 #define RT_QUEUE_STRIDE 16
 #define RT_REDO_COUNT (RT_QUEUES * RT_QUEUE_STRIDE)
 // chunks of the candidate overflow pool handed out so far

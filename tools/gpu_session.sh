@@ -28,6 +28,7 @@ for s in $STEPS; do
         bench) run bench 600 python bench.py ;;
         quick) run bench_quick 300 python bench.py --no-cpu --steps 10 ;;
         split) RT_RESOLVE=split run bench_split 300 python bench.py --no-cpu --steps 10 ;;
+        shard8) run bench_shard8 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of 8 ;;
         shards) for n in 2 4 8; do run bench_shard$n 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of $n || exit 1; done ;;
         rehearse) RT_BENCH_REHEARSE=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                       --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu ;;

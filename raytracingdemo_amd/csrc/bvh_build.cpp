@@ -16,6 +16,7 @@
 #include <numeric>
 #include <cstdlib>
 #include <exception>
+#include <system_error>
 #include <thread>
 
 #include "rt_internal.h"
@@ -40,6 +41,17 @@ struct Box {
 inline double area(const Box& b) {
     double ex = b.mx[0] - b.mn[0], ey = b.mx[1] - b.mn[1], ez = b.mx[2] - b.mn[2];
     return 2.0 * (ex * ey + ey * ez + ez * ex);
+}
+
+// Runs f on a new thread kept in `th`, or here when no thread can be made
+// (the result is the same either way).
+template <class F>
+void spawn(std::vector<std::thread>& th, F&& f) {
+    try {
+        th.emplace_back(f);
+    } catch (const std::system_error&) {
+        f();
+    }
 }
 
 struct Builder {
@@ -109,7 +121,7 @@ struct Builder {
                 std::iter_swap(lo, hi);
                 ++lo;
             }
-            if (last - lo >= par_min) th.emplace_back([=] { par_introsort(lo, last, depth, less, par_min); });
+            if (last - lo >= par_min) spawn(th, [=] { par_introsort(lo, last, depth, less, par_min); });
             else par_introsort(lo, last, depth, less, par_min);
             last = lo;
         }
@@ -253,7 +265,10 @@ void parallel_for(uint64_t n, F fn) {
     if (T <= 1) { fn(uint64_t(0), n); return; }
     std::vector<std::thread> th;
     const uint64_t per = (n + T - 1) / T;
-    for (uint64_t c = 1; c < T; c++) th.emplace_back(fn, std::min(n, c * per), std::min(n, (c + 1) * per));
+    for (uint64_t c = 1; c < T; c++) {
+        const uint64_t a = std::min(n, c * per), b = std::min(n, (c + 1) * per);
+        spawn(th, [&fn, a, b] { fn(a, b); });
+    }
     fn(uint64_t(0), std::min(n, per));
     for (auto& x : th) x.join();
 }
@@ -372,7 +387,7 @@ std::vector<RNode> grow_parallel(Builder& B, int algo, int pk, RNode root, int64
             sub[j] = grow_parallel(B, algo, pk, std::move(c), par_min);
         } catch (...) { err[j] = std::current_exception(); }
     };
-    for (size_t j = 0; j + 1 < k; j++) th.emplace_back(run, j);
+    for (size_t j = 0; j + 1 < k; j++) spawn(th, [&run, j] { run(j); });
     if (k) run(k - 1);
     for (auto& x : th) x.join();
     for (auto& e : err) if (e) std::rethrow_exception(e);
@@ -624,7 +639,7 @@ struct Flattener {
             } catch (...) { err[j] = std::current_exception(); }
         };
         std::vector<std::thread> th;
-        for (size_t j = 0; j + 1 < m; j++) th.emplace_back(run, j);
+        for (size_t j = 0; j + 1 < m; j++) spawn(th, [&run, j] { run(j); });
         if (m) run(m - 1);
         for (auto& x : th) x.join();
         for (auto& e : err) if (e) std::rethrow_exception(e);

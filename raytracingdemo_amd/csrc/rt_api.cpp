@@ -814,6 +814,7 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
                 });
                 try {
                     wt = rt::build_walk_tree_device(s->soup, walk_device, rt::walk_max_leaf(), rt::walk_node_cost());
+                    rt::plan_wide_collapse(wt, 8);
                 } catch (...) {
                     ref.join();
                     throw;
@@ -828,6 +829,7 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
                 s->tree = rt::build_tree(s->soup, algo, k, collapse);
                 t2 = clk::now();
                 wt = rt::build_walk_tree(s->soup);
+                rt::plan_wide_collapse(wt, 8);
                 t3 = clk::now();
             }
             s->flat = rt::flatten(s->soup, s->tree, 0, &wt);

@@ -70,8 +70,19 @@ struct WalkNode {
 struct WalkTree {
     std::vector<WalkNode> nodes;  // nodes[0] = root
     std::vector<uint32_t> order;  // triangle (loader) index per walk position
+    // Planned W-wide collapse (plan_wide_collapse): for a binary node that
+    // becomes a wide node, its slots are wide_kids[wide_off[b] ..
+    // wide_off[b] + wide_cnt[b]); empty = the greedy collapse.
+    std::vector<uint32_t> wide_off;
+    std::vector<uint8_t> wide_cnt;
+    std::vector<int32_t> wide_kids;
 };
 WalkTree build_walk_tree(const Soup& s);
+// SAH-optimal W-wide collapse of the binary walk tree (dynamic programme over
+// slot counts; subtrees of <= RT_WALK_PMAX triangles may become one leaf).
+// Rewrites the chosen subtrees as leaves in place and records the slots of
+// every wide node.  RT_WALK_COLLAPSE=greedy leaves the tree untouched.
+void plan_wide_collapse(WalkTree& w, int W);
 // The same binned-SAH tree built on a gfx950 device (walk_build.hip): equal
 // splits, device-stable order inside nodes.
 WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node_cost);

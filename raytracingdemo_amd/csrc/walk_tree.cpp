@@ -179,9 +179,149 @@ WalkTree build_walk_tree(const Soup& s) {
     return w;
 }
 
-// Children of binary node b for one W-wide node: open the inner child of
-// largest surface area until W children (or only leaves) remain.
+namespace {
+
+double env_cost(const char* name, double dflt) {
+    const char* e = std::getenv(name);
+    const double v = e ? std::atof(e) : dflt;
+    return v >= 0.0 && v < 100.0 ? v : dflt;
+}
+
+}  // namespace
+
+// The collapse as a dynamic programme (the SAH-optimal wide-BVH conversion of
+// Ylitie, Karras and Laine, HPG 2017), costs in the packet kernel's units:
+//   leaf(n)        = A(n) (c_leaf + c_tri cnt(n))        cnt(n) <= P
+//   inner(n)       = A(n) c_node + split(n, W)
+//   split(n, i)    = min_k  C(left, k) + C(right, i - k)
+//   C(n, 1)        = min(leaf(n), inner(n))
+//   C(n, i > 1)    = min(C(n, i - 1), split(n, i))
+// C(n, i) is the cheapest way to stand for n's subtree with at most i slots of
+// a parent wide node.  Any subtree of the binary tree is a contiguous range
+// of `order`, so "this subtree is one leaf" only relabels the node.
+void plan_wide_collapse(WalkTree& w, int W) {
+    w.wide_off.clear();
+    w.wide_cnt.clear();
+    w.wide_kids.clear();
+    const char* mode = std::getenv("RT_WALK_COLLAPSE");
+    if (mode && mode[0] == 'g') return;
+    const size_t N = w.nodes.size();
+    if (N < 3 || w.nodes[0].left < 0 || W < 2 || W > 16) return;
+    const double cN = env_cost("RT_WALK_CN", 1.0);
+    const double cL = env_cost("RT_WALK_CLV", 0.25);
+    const double cT = env_cost("RT_WALK_CTRI", 0.5);
+    const uint32_t P = (uint32_t)std::min(16.0, std::max(1.0, env_cost("RT_WALK_PMAX", 8.0)));
+
+    // post-order of the binary tree (children before parents)
+    std::vector<int32_t> post;
+    post.reserve(N);
+    {
+        std::vector<std::pair<int32_t, bool>> st{{0, false}};
+        while (!st.empty()) {
+            auto [b, done] = st.back();
+            st.pop_back();
+            const WalkNode& n = w.nodes[b];
+            if (done || n.left < 0) { post.push_back(b); continue; }
+            st.push_back({b, true});
+            st.push_back({n.right, false});
+            st.push_back({n.left, false});
+        }
+    }
+    const int S = W + 1;
+    std::vector<double> C(N * S, std::numeric_limits<double>::infinity());
+    std::vector<uint8_t> pick(N * S, 0);  // [0] inner split k; [1] leaf flag; [i] split k or 0 (= C(n, i-1))
+    std::vector<uint32_t> rb(N), re(N);   // the subtree's range of `order`
+    std::vector<double> dist(S);
+    std::vector<uint8_t> dk(S);
+    for (int32_t b : post) {
+        const WalkNode& n = w.nodes[b];
+        BBox bb;
+        for (int a = 0; a < 3; a++) { bb.mn[a] = n.mn[a]; bb.mx[a] = n.mx[a]; }
+        const double A = bb.area();
+        double* c = &C[(size_t)b * S];
+        uint8_t* p = &pick[(size_t)b * S];
+        if (n.left < 0) {
+            rb[b] = n.first;
+            re[b] = n.first + n.count;
+            const double leaf = A * (cL + cT * n.count);
+            for (int i = 1; i <= W; i++) c[i] = leaf;
+            p[1] = 1;
+            continue;
+        }
+        const int32_t l = n.left, r = n.right;
+        bool contiguous = true;
+        if (re[l] == rb[r]) { rb[b] = rb[l]; re[b] = re[r]; }
+        else if (re[r] == rb[l]) { rb[b] = rb[r]; re[b] = re[l]; }
+        else { rb[b] = std::min(rb[l], rb[r]); re[b] = std::max(re[l], re[r]); contiguous = false; }
+        const double* cl = &C[(size_t)l * S];
+        const double* cr = &C[(size_t)r * S];
+        for (int i = 2; i <= W; i++) {
+            double best = std::numeric_limits<double>::infinity();
+            int bk = 1;
+            for (int k = 1; k < i; k++) {
+                const double v = cl[k] + cr[i - k];
+                if (v < best) { best = v; bk = k; }
+            }
+            dist[i] = best;
+            dk[i] = (uint8_t)bk;
+        }
+        const double inner = A * cN + dist[W];
+        p[0] = dk[W];
+        const uint32_t cnt = re[b] - rb[b];
+        const double leaf = contiguous && cnt <= P && b != 0 ? A * (cL + cT * cnt) : std::numeric_limits<double>::infinity();
+        if (leaf <= inner) { c[1] = leaf; p[1] = 1; }
+        else { c[1] = inner; p[1] = 0; }
+        for (int i = 2; i <= W; i++) {
+            if (dist[i] < c[i - 1]) { c[i] = dist[i]; p[i] = dk[i]; }
+            else { c[i] = c[i - 1]; p[i] = 0; }
+        }
+    }
+
+    // top-down: the slots of each wide node; slots that chose "leaf" become leaves
+    w.wide_off.assign(N, UINT32_MAX);
+    w.wide_cnt.assign(N, 0);
+    std::vector<int32_t> slots;
+    auto expand = [&](auto&& self, int32_t m, int i) -> void {
+        const WalkNode& n = w.nodes[m];
+        while (i > 1 && n.left >= 0 && pick[(size_t)m * S + i] == 0) i--;
+        if (i == 1 || n.left < 0) { slots.push_back(m); return; }
+        const int k = pick[(size_t)m * S + i];
+        self(self, n.left, k);
+        self(self, n.right, i - k);
+    };
+    std::vector<int32_t> todo{0};
+    while (!todo.empty()) {
+        const int32_t b = todo.back();
+        todo.pop_back();
+        slots.clear();
+        const int k = pick[(size_t)b * S];
+        expand(expand, w.nodes[b].left, k);
+        expand(expand, w.nodes[b].right, W - k);
+        w.wide_off[b] = (uint32_t)w.wide_kids.size();
+        w.wide_cnt[b] = (uint8_t)slots.size();
+        for (int32_t m : slots) {
+            w.wide_kids.push_back(m);
+            WalkNode& n = w.nodes[m];
+            if (n.left < 0) continue;
+            if (pick[(size_t)m * S + 1]) {
+                n.left = n.right = -1;
+                n.first = rb[m];
+                n.count = re[m] - rb[m];
+            } else {
+                todo.push_back(m);
+            }
+        }
+    }
+}
+
+// Children of binary node b for one W-wide node: the planned slots
+// (plan_wide_collapse), or greedily: open the inner child of largest surface
+// area until W children (or only leaves) remain.
 std::vector<int32_t> collapse_children(const WalkTree& w, int32_t b, int W) {
+    if (!w.wide_off.empty() && w.wide_off[b] != UINT32_MAX) {
+        const int32_t* k = w.wide_kids.data() + w.wide_off[b];
+        return std::vector<int32_t>(k, k + w.wide_cnt[b]);
+    }
     std::vector<int32_t> kids{w.nodes[b].left, w.nodes[b].right};
     while ((int)kids.size() < W) {
         int pick = -1;

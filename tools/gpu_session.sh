@@ -70,6 +70,14 @@ for s in $STEPS; do
                done
                python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt
                python tools/pmc_valu.py gpurun_out/pmc_key.txt gpurun_out/pmc_valu.json gpurun_out/sq/sq*_counter_collection.csv ;;
+        ab)    # A/B over environment settings: AB_ENVS="A=1 B=2;A=3;..." (one bench per entry)
+               i=0; IFS=';' read -ra cfgs <<< "${AB_ENVS:-}"
+               for c in "${cfgs[@]}"; do i=$((i+1))
+                   echo "--- ab$i: $c"
+                   env $c timeout -k 10 300 python bench.py --no-cpu --no-dropin --steps 10 > gpurun_out/ab$i.log 2>&1
+                   rc=$?; echo "ab$i exit=$rc"; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/ab$i.log; exit $rc; }
+                   python -c "import json; l=[x for x in open('gpurun_out/ab$i.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']; q=r['per_ray']; print('RESULT', '$c', d['value'], r['kernel_ms_avg'], q['wave_nodes_per_tile'], q['wave_leaves_per_tile'], q['wave_tris_per_tile'], q['tri_tests_fp64'])" || true
+               done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

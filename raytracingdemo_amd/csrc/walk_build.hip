@@ -35,7 +35,10 @@
 
 namespace {
 
-constexpr int kBins = 32;
+#ifndef RT_WALK_BINS
+#define RT_WALK_BINS 32  // centroid bins per axis (host and device builds must agree)
+#endif
+constexpr int kBins = RT_WALK_BINS;
 constexpr uint32_t kSmall = 16;  // a subtree of at most this many triangles: one thread (16: 64 measured 13 ms in k_small)
 
 static_assert(sizeof(rt::WalkNode) == 64, "device nodes are copied straight into WalkNode");

@@ -13,9 +13,10 @@
 // along one axis from 16 bins (stack_bvh.hpp:241-449): long thin children
 // that overlap a tile's rays far more than needed.  This builder makes a
 // binary SAH tree over all three axes (32 centroid bins, leaves of at most
-// kMaxLeaf triangles: one scalar-load chunk of the packet kernel), then
-// collapses it into W-wide nodes by repeatedly opening the child with the
-// largest surface area (the usual greedy wide-BVH collapse).
+// RT_WALK_LEAF triangles), then collapses it into W-wide nodes by a dynamic
+// programme over the SAH cost (plan_wide_collapse; the greedy collapse, which
+// repeatedly opens the child of largest surface area, with
+// RT_WALK_COLLAPSE=greedy).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -26,7 +27,10 @@
 namespace rt {
 namespace {
 
-constexpr int kBins = 32;
+#ifndef RT_WALK_BINS
+#define RT_WALK_BINS 32  // centroid bins per axis (host and device builds must agree)
+#endif
+constexpr int kBins = RT_WALK_BINS;
 
 struct BBox {
     double mn[3], mx[3];
@@ -55,24 +59,19 @@ struct BBox {
     }
 };
 
+// (read at every scene build, so a process can build trees of both kinds)
 int max_leaf() {
-    static const int m = [] {
-        const char* e = std::getenv("RT_WALK_LEAF");
-        const int v = e ? std::atoi(e) : 4;
-        return v >= 1 && v <= 16 ? v : 4;
-    }();
-    return m;
+    const char* e = std::getenv("RT_WALK_LEAF");
+    const int v = e ? std::atoi(e) : 4;
+    return v >= 1 && v <= 16 ? v : 4;
 }
 
 // SAH cost of one inner-node visit relative to one triangle test (the packet
 // kernel's 8-child step and a triangle test cost about the same: DESIGN.md §7)
 double node_cost() {
-    static const double c = [] {
-        const char* e = std::getenv("RT_WALK_CT");
-        const double v = e ? std::atof(e) : 1.0;
-        return v > 0.0 && v < 100.0 ? v : 1.0;
-    }();
-    return c;
+    const char* e = std::getenv("RT_WALK_CT");
+    const double v = e ? std::atof(e) : 1.0;
+    return v > 0.0 && v < 100.0 ? v : 1.0;
 }
 
 }  // namespace
@@ -87,6 +86,7 @@ WalkTree build_walk_tree(const Soup& s) {
     for (uint32_t i = 0; i < n; i++) w.order[i] = i;
     if (n == 0) return w;
     const int LMAX = max_leaf();
+    const double CT = node_cost();
     std::vector<BBox> tb(n);
     std::vector<double> cen(3 * (size_t)n);
     for (uint32_t i = 0; i < n; i++) {
@@ -154,7 +154,7 @@ WalkTree build_walk_tree(const Soup& s) {
             }
         }
         // a leaf costs cnt triangle tests; an inner node one more box test
-        if (cnt <= (uint32_t)LMAX && (best_axis < 0 || (double)cnt <= node_cost() + best)) { make_leaf(); continue; }
+        if (cnt <= (uint32_t)LMAX && (best_axis < 0 || (double)cnt <= CT + best)) { make_leaf(); continue; }
         uint32_t mid;
         if (best_axis < 0) {
             mid = j.b + cnt / 2;  // coincident centroids: split the range in half

@@ -137,6 +137,29 @@ def test_sponza_proxy_bands_vs_oracle(oracle):
             assert np.array_equal(g["rgb"][sl], o["rgb"])
 
 
+@pytest.mark.parametrize("env", [{"RT_WALK_COLLAPSE": "greedy"}, {"RT_WALK_CN": "2"}, {"RT_WALK_LEAF": "1"}])
+def test_walk_tree_collapse_variants_give_identical_frames(env, monkeypatch):
+    """Results never depend on the walk tree (walk_tree.cpp): the greedy
+    collapse, a costlier node visit in the collapse and one-triangle binary leaves render
+    the headline scene's frames bit for bit like the default planned collapse
+    (the full-size test in test_gpu_headline.py pins the default to the oracle)."""
+    from raytracingdemo_amd.scenes import sponza_proxy_triangles
+    tris = sponza_proxy_triangles()
+    c = rt.scene_center(tris)
+    base = rt.Scene(tris, "bsah", 8).upload([0])
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    alt = rt.Scene(tris, "bsah", 8).upload([0])
+    assert alt.stats()["layout_digest"] != base.stats()["layout_digest"]
+    for step in (3, 21):
+        pos, d = rt.CameraPath(c, 36).circular_path(step)
+        x = base.calculate_screen(pos, d, 960, 540)
+        y = alt.calculate_screen(pos, d, 960, 540)
+        for f in ("hit_id", "pos", "dist", "rgb"):
+            assert np.array_equal(x[f], y[f]), (env, step, f)
+        assert x["hits"] == y["hits"]
+
+
 def test_exact_and_literal_modes_agree_on_sponza_proxy():
     from raytracingdemo_amd.scenes import sponza_proxy_triangles
     tris = sponza_proxy_triangles(60000)

@@ -18,9 +18,12 @@
 // repeatedly opens the child of largest surface area, with
 // RT_WALK_COLLAPSE=greedy).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <limits>
+#include <system_error>
+#include <thread>
 
 #include "rt_internal.h"
 
@@ -212,28 +215,12 @@ void plan_wide_collapse(WalkTree& w, int W) {
     const double cT = env_cost("RT_WALK_CTRI", 0.5);
     const uint32_t P = (uint32_t)std::min(16.0, std::max(1.0, env_cost("RT_WALK_PMAX", 8.0)));
 
-    // post-order of the binary tree (children before parents)
-    std::vector<int32_t> post;
-    post.reserve(N);
-    {
-        std::vector<std::pair<int32_t, bool>> st{{0, false}};
-        while (!st.empty()) {
-            auto [b, done] = st.back();
-            st.pop_back();
-            const WalkNode& n = w.nodes[b];
-            if (done || n.left < 0) { post.push_back(b); continue; }
-            st.push_back({b, true});
-            st.push_back({n.right, false});
-            st.push_back({n.left, false});
-        }
-    }
     const int S = W + 1;
-    std::vector<double> C(N * S, std::numeric_limits<double>::infinity());
-    std::vector<uint8_t> pick(N * S, 0);  // [0] inner split k; [1] leaf flag; [i] split k or 0 (= C(n, i-1))
-    std::vector<uint32_t> rb(N), re(N);   // the subtree's range of `order`
-    std::vector<double> dist(S);
-    std::vector<uint8_t> dk(S);
-    for (int32_t b : post) {
+    uvector<double> C(N * S);        // every row is written before it is read
+    uvector<uint8_t> pick(N * S);    // [0] inner split k; [1] leaf flag; [i] split k or 0 (= C(n, i-1))
+    uvector<uint32_t> rb(N), re(N);  // the subtree's range of `order`
+    // one row of the programme; the children's rows are complete
+    auto row = [&](int32_t b) {
         const WalkNode& n = w.nodes[b];
         BBox bb;
         for (int a = 0; a < 3; a++) { bb.mn[a] = n.mn[a]; bb.mx[a] = n.mx[a]; }
@@ -244,9 +231,9 @@ void plan_wide_collapse(WalkTree& w, int W) {
             rb[b] = n.first;
             re[b] = n.first + n.count;
             const double leaf = A * (cL + cT * n.count);
-            for (int i = 1; i <= W; i++) c[i] = leaf;
+            for (int i = 0; i <= W; i++) { c[i] = leaf; p[i] = 0; }
             p[1] = 1;
-            continue;
+            return;
         }
         const int32_t l = n.left, r = n.right;
         bool contiguous = true;
@@ -255,6 +242,8 @@ void plan_wide_collapse(WalkTree& w, int W) {
         else { rb[b] = std::min(rb[l], rb[r]); re[b] = std::max(re[l], re[r]); contiguous = false; }
         const double* cl = &C[(size_t)l * S];
         const double* cr = &C[(size_t)r * S];
+        double dist[17];
+        uint8_t dk[17];
         for (int i = 2; i <= W; i++) {
             double best = std::numeric_limits<double>::infinity();
             int bk = 1;
@@ -275,7 +264,46 @@ void plan_wide_collapse(WalkTree& w, int W) {
             if (dist[i] < c[i - 1]) { c[i] = dist[i]; p[i] = dk[i]; }
             else { c[i] = c[i - 1]; p[i] = 0; }
         }
+    };
+    // rows of one subtree, children before parents (explicit post-order)
+    auto subtree = [&](int32_t root) {
+        std::vector<std::pair<int32_t, bool>> st{{root, false}};
+        while (!st.empty()) {
+            auto [b, done] = st.back();
+            st.pop_back();
+            const WalkNode& n = w.nodes[b];
+            if (done || n.left < 0) { row(b); continue; }
+            st.push_back({b, true});
+            st.push_back({n.right, false});
+            st.push_back({n.left, false});
+        }
+    };
+    // The top levels breadth-first until there are enough subtrees for the
+    // threads; the subtrees run on threads, then the top levels bottom-up.
+    std::vector<int32_t> top, front{0};
+    for (int level = 0; level < 7 && !front.empty(); level++) {
+        std::vector<int32_t> next;
+        for (int32_t b : front) {
+            const WalkNode& n = w.nodes[b];
+            top.push_back(b);
+            if (n.left >= 0) { next.push_back(n.left); next.push_back(n.right); }
+        }
+        front.swap(next);
     }
+    {
+        std::atomic<size_t> take{0};
+        auto work = [&] {
+            for (size_t t; (t = take.fetch_add(1)) < front.size();) subtree(front[t]);
+        };
+        std::vector<std::thread> th;
+        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        for (unsigned t = 1; t < hw && t < front.size(); t++) {
+            try { th.emplace_back(work); } catch (const std::system_error&) { break; }
+        }
+        work();
+        for (auto& x : th) x.join();
+    }
+    for (size_t t = top.size(); t-- > 0;) row(top[t]);
 
     // top-down: the slots of each wide node; slots that chose "leaf" become leaves
     w.wide_off.assign(N, UINT32_MAX);

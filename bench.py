@@ -587,6 +587,7 @@ def main():
         dropin = None
         if world == 1 and not a.no_dropin and S == 1:
             dropin = dropin_rate(scene, cams, W, H, mode)
+            dropin["fused_shade"] = dropin_rate(scene, cams, W, H, mode, want=("rgb",))
         if world == 1 and not a.no_cpu:
             # the timed step's frames (buffer set 0, the last step at N = 1)
             # checked against the reference frames the baseline renders
@@ -645,28 +646,31 @@ def main():
         dist.destroy_process_group()
 
 
-def dropin_rate(scene, cams, W, H, mode):
+def dropin_rate(scene, cams, W, H, mode, want=("hit_id", "pos")):
     """The drop-in path INTEGRATION.md §2 binds (rt_render_frame: one pose per
     call into host buffers, blocking, as runTest's calculateScreen call,
-    src/main.cpp:253-255): hit ids, distances and PPM bytes for every pose of
-    the orbit, D2H copies included.  Reported beside the headline, never as it."""
+    src/main.cpp:253-255) for every pose of the orbit, D2H copies included.
+    want: the outputs copied back — ("hit_id", "pos") is what
+    gpu_calculate_screen requests (28 B per pixel: runTest rebuilds ray_hits
+    from them and shades on the host); ("rgb",) is the fused-shadeScreen
+    variant of §2 (the PPM bytes and the hit count, 3 B per pixel).
+    Reported beside the headline, never as it."""
     # one set of host arrays reused frame after frame, as runTest reuses its
     # global ray_hits (src/main.cpp:39)
     g = None
     for p, d in cams[:2]:
-        g = scene.calculate_screen(p, d, W, H, mode=mode, want=("hit_id", "dist", "rgb"), out=g)
+        g = scene.calculate_screen(p, d, W, H, mode=mode, want=want, out=g)
     t0 = time.perf_counter()
     dev_s = 0.0
     for p, d in cams:
-        g = scene.calculate_screen(p, d, W, H, mode=mode, out=g)
+        g = scene.calculate_screen(p, d, W, H, mode=mode, want=want, out=g)
         dev_s += g["seconds"]
     wall = time.perf_counter() - t0
     n = len(cams) * W * H
     return {"value": round(n / wall / 1e6, 2), "unit": "Mrays/s", "entry_point": "rt_render_frame",
-            "frames": len(cams), "ms_per_frame": round(wall / len(cams) * 1e3, 3),
+            "outputs": list(want), "frames": len(cams), "ms_per_frame": round(wall / len(cams) * 1e3, 3),
             "device_ms_per_frame": round(dev_s / len(cams) * 1e3, 3),
-            "note": "one pose per call into one reused set of pageable host arrays (hit_id + dist + rgb D2H), "
-                    "blocking"}
+            "note": "one pose per call into one reused set of pageable host arrays, blocking"}
 
 
 if __name__ == "__main__":

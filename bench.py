@@ -41,6 +41,7 @@ CHAIN_BYTES = 52       # fp64 box (48 B) + parent (4 B) per re-verified ancestor
 OUT_BYTES = 15         # u32 hit-id + f64 distance + 3 B rgb written per ray
 CAND_BYTES = 8         # one candidate entry {triangle, t bound} handed to the resolve kernel
 SAMPLE_BYTES = 37      # spp > 1, fused: u32 hit-id + f64 distance + the sample's f64 colour + status byte
+PACKED_SAMPLE_BYTES = 12  # spp 4 / 16, fused and packed (one wave holds a pixel's samples): hit-id + distance
 
 
 def host_cores():
@@ -494,7 +495,8 @@ def main():
         # (spp > 1: per sample its outputs, colour and status for k_average)
         trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES + cs["tri_tests"] * MT64_BYTES +
                        cs["hits"] * WIN_BYTES + cs["chain_nodes"] * CHAIN_BYTES +
-                       cs["rays"] * (OUT_BYTES if S == 1 else SAMPLE_BYTES))
+                       cs["rays"] * (OUT_BYTES if S == 1 else
+                                     PACKED_SAMPLE_BYTES + 3.0 / S if packed_spp(S) else SAMPLE_BYTES))
     elif cs["wave_tiles"]:
         # packet traversal kernel, split resolve: the walk plus the candidate
         # lists it writes
@@ -644,6 +646,14 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def packed_spp(spp):
+    """The library's fp.pack rule (rt_api.cpp frame_params): with the fused
+    resolve, spp 4 and 16 put all samples of a pixel in one wave (its colours
+    summed across lanes, no k_average)."""
+    return (spp > 1 and 64 % spp == 0 and os.environ.get("RT_SPP_PACK", "1")[:1] != "0"
+            and os.environ.get("RT_RESOLVE", "")[:1] != "s")
 
 
 def dropin_rate(scene, cams, W, H, mode, want=("hit_id", "pos")):

@@ -319,7 +319,8 @@ __device__ __forceinline__ uint32_t resolve_list(const RtDevScene& sc, const RtF
 
 // Outcome of one tile for the caller's per-frame hit count (FUSED).
 struct TileOut {
-    bool hit;  // the lane's pixel is resolved here and hit
+    bool hit;       // the lane's pixel is resolved here and hit
+    uint32_t hits;  // fp.pack: on a pixel's first-sample lane, its samples hit
 };
 
 template <int W, int SP, int K, bool COUNT, bool FUSED>
@@ -521,7 +522,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         atomicAdd(&fp.counters[12], (unsigned long long)w_tris);
         atomicAdd(&fp.counters[15], (unsigned long long)w_empty);
     }
-    TileOut res{false};
+    TileOut res{false, 0u};
     if (!valid) return res;
     const RtLaunchAux aux = kload(&A->aux);
     const bool dropped = drop < __builtin_huge_valf() && drop <= tcull;  // a dropped candidate could still win
@@ -561,6 +562,39 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                 shade_color(cam, out, sh, c);
                 store_rgb(fp, ob, c);
                 res.hit = hit_s;
+            }
+        } else if (fp.pack) {
+            // the pixel's spp samples are lanes base .. base + spp - 1 of this
+            // wave (sample k in lane base + k): each lane stores its sample's
+            // outputs, the colours are summed in sample order across the lanes
+            // (k_average's order), and the first lane stores the pixel or, if
+            // a sample is unresolved, sends the pixel to k_fixup whole
+            const int base = lane & ~(spp - 1);
+            const uint64_t gm = (spp == 64 ? ~0ull : ((1ull << spp) - 1ull)) << base;
+            const uint64_t bad = __ballot(redo != 0) & gm;
+            const uint64_t hm = __ballot(hit_s) & gm;
+            const size_t fpix = (size_t)fp.W * (size_t)fp.nrows;
+            const size_t po = (size_t)ob - (size_t)f * fpix;
+            double c[3] = {0.0, 0.0, 0.0};
+            if (!redo) {
+                store_sample(fp, out_index(fp, pose, po) * (size_t)spp + (size_t)(f - pose * spp), out, sh);
+                shade_color(cam, out, sh, c);
+            }
+            double acc[3] = {0.0, 0.0, 0.0};
+            for (int k = 0; k < spp; k++) {
+                acc[0] = acc[0] + __shfl(c[0], base + k);
+                acc[1] = acc[1] + __shfl(c[1], base + k);
+                acc[2] = acc[2] + __shfl(c[2], base + k);
+            }
+            if (lane == base) {
+                const size_t pix = out_index(fp, pose, po);
+                if (bad) {
+                    const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
+                    aux.redo[slot] = (uint32_t)pix;
+                } else {
+                    store_rgb(fp, pix, acc);
+                    res.hits = (uint32_t)__builtin_popcountll(hm);
+                }
             }
         } else {
             // one sample of a pixel: its outputs at sample index pix * spp + k
@@ -824,9 +858,14 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     for (;;) {
         A = launder(A);
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
-        const int tiles_x = (W_ + 7) >> 3;
-        const int tiles_f = tiles_x * ((nrows + 7) >> 3);  // tiles per frame
-        const int tiles = tiles_f * kword(&A->fp.nframes);
+        // fp.pack: a tile is ts x ts pixels of one pose with all spp samples
+        // (ts = 8 / n), else 8 x 8 pixels of one sample frame
+        const bool pack = FUSED && kword(&A->fp.pack);
+        const int spp = kword(&A->fp.spp);
+        const int ts = pack ? 8 / kword(&A->fp.spp_n) : 8;
+        const int tiles_x = (W_ + ts - 1) / ts;
+        const int tiles_f = tiles_x * ((nrows + ts - 1) / ts);  // tiles per frame (pose when packed)
+        const int tiles = tiles_f * (pack ? kword(&A->fp.nframes) / spp : kword(&A->fp.nframes));
         claim = tiles >= 64 * (int)(gridDim.x * kPacketWaves) ? 2 : 1;
         int t = 0;
         bool claimed = false;
@@ -853,20 +892,33 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             pend_n = 1;
         }
         if (tile >= tiles) break;
-        const int f = tile / tiles_f;  // frame of the batch
-        const int ft = tile - f * tiles_f;
-        const int i = (ft % tiles_x) * 8 + (lane & 7);
-        const int r = (ft / tiles_x) * 8 + (lane >> 3);
+        const int fr = tile / tiles_f;  // frame of the batch (pose when packed)
+        const int ft = tile - fr * tiles_f;
+        int f = fr, i, r;
+        if (pack) {  // lane = pixel * spp + sample
+            const int pl = lane / spp;
+            f = fr * spp + (lane & (spp - 1));
+            i = (ft % tiles_x) * ts + pl % ts;
+            r = (ft / tiles_x) * ts + pl / ts;
+        } else {
+            i = (ft % tiles_x) * 8 + (lane & 7);
+            r = (ft / tiles_x) * 8 + (lane >> 3);
+        }
         const TileOut o =
             trace_packet<W, SP, K, COUNT, FUSED>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);
         if constexpr (FUSED) {
-            const uint32_t h = (uint32_t)__builtin_popcountll(__ballot(o.hit));
-            if (f != hf) {
+            uint32_t h = (uint32_t)__builtin_popcountll(__ballot(o.hit));
+            if (pack) {  // samples hit per pixel (<= 64) summed over the wave
+                h = 0;
+#pragma unroll
+                for (int b = 0; b < 7; b++) h += (uint32_t)__builtin_popcountll(__ballot((o.hits >> b) & 1u)) << b;
+            }
+            if (fr != hf) {
                 if (hacc != 0 && lane == 0)
                     atomicAdd(kload(&A->aux.tile_ctr) + RT_HIT_BASE + (hf * RT_HIT_SLOTS + hslot) * RT_QUEUE_STRIDE,
                               hacc);
                 hacc = 0;
-                hf = f;
+                hf = fr;
             }
             hacc += h;
         }

@@ -785,7 +785,13 @@ bool split_resolve(int spp) {
 }
 // the packet pipeline needs the candidate buffers: the split resolve's lists,
 // or spp > 1 with the fused resolve (each sample's colour and status)
-bool needs_cand(int spp) { return spp > 1 || split_resolve(spp); }
+// (spp 4 and 16 with the fused resolve: a wave sums a pixel's samples across
+// its lanes, nothing goes through HBM — the host's fp.pack rule)
+bool packs_samples(int spp) {
+    const char* e = getenv("RT_SPP_PACK");
+    return spp > 1 && 64 % spp == 0 && !(e && e[0] == '0');
+}
+bool needs_cand(int spp) { return (spp > 1 && !packs_samples(spp)) || split_resolve(spp); }
 
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
@@ -804,7 +810,7 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
                 hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
-            if (fp.spp > 1) {
+            if (fp.spp > 1 && !fp.pack) {
                 const uint64_t bpf = ((uint64_t)fp.W * (uint64_t)fp.nrows + 255) / 256;
                 hipLaunchKernelGGL(k_average, dim3((unsigned)(bpf * (uint64_t)(fp.nframes / fp.spp))), blk, 0, s, fp,
                                    aux);

@@ -440,6 +440,10 @@ RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row
     // sample q of each pose sits at ((q % g) + 0.5) / g, ((q / g) + 0.5) / g
     // (computed in-kernel by frame_cam with these same expressions)
     fp.spp_n = spp_grid(spp);
+    // the fused packet walk takes a pixel's samples in one wave when they
+    // divide it (spp 4, 16, 64; RT_SPP_PACK=0 keeps one sample frame per tile)
+    const char* pk = std::getenv("RT_SPP_PACK");
+    fp.pack = spp > 1 && 64 % spp == 0 && !(pk && pk[0] == '0');
     for (int p = 0; p < n; p++) {
         RtPose k{};
         k.pad = frame_pad(s, &c[p]);

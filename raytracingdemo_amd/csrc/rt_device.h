@@ -205,6 +205,7 @@ struct RtFrameParams {
     int32_t spp;                  // samples per pixel (n x n stratified), >= 1
     int32_t band;                 // 1: rows (row0, row_stride in rows); RT_SHARD_BAND: banded shard (in bands)
     int32_t spp_n;                // n of the n x n sample pattern (spp = n * n)
+    int32_t pack;                 // 1: a packet wave takes all spp samples of (8/n)^2 pixels (64 % spp == 0)
     RT_G uint32_t* hit_id;
     RT_G double* dist;
     RT_G double* hit_pos;

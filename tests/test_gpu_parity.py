@@ -367,13 +367,17 @@ def _spp_render(s, cams, W, H, spp, row0=0, stride=1, nrows=None, mode="exact"):
 
 
 @pytest.mark.parametrize("mode", ["exact", "fp64", "split"])
-@pytest.mark.parametrize("spp", [4, 9])
+@pytest.mark.parametrize("spp", [4, 9, 16])
 def test_stratified_spp_matches_oracle(oracle, spp, mode, monkeypatch):
-    """spp = n*n stratified samples per pixel (config c4's 2x2 and a 3x3): every
-    sample's hit id, distance and position, the averaged colour and the per-pose
-    hit count against the oracle; 5 poses span launch boundaries.  "exact" is
-    the fused resolve (each sample resolved in the walk kernel, k_average
-    forming the pixels), "split" the candidate lists handed to k_resolve."""
+    """spp = n*n stratified samples per pixel (config c4's 2x2, a 3x3 and a
+    4x4): every sample's hit id, distance and position, the averaged colour and
+    the per-pose hit count against the oracle; 5 poses span launch boundaries.
+    "exact" is the fused resolve (spp 4 and 16: a wave takes all samples of
+    4x4 / 2x2 pixels and sums them across its lanes; spp 9: one sample frame
+    per tile, k_average forming the pixels), "split" the candidate lists
+    handed to k_resolve."""
+    if spp == 16 and mode != "exact":
+        pytest.skip("16 spp: the fused, packed path only")
     if mode == "split":
         monkeypatch.setenv("RT_RESOLVE", "split")
         mode = "exact"
@@ -394,6 +398,24 @@ def test_stratified_spp_matches_oracle(oracle, spp, mode, monkeypatch):
         assert np.array_equal(g["pos"][f][m], o["pos"][m]), f
         assert np.array_equal(g["rgb"][f], o["rgb"]), f
         assert g["hits"][f] == o["hits"], f
+
+
+@pytest.mark.parametrize("spp", [4, 16])
+def test_packed_samples_equal_sample_frames(spp, monkeypatch):
+    """A wave holding every sample of (8/n)^2 pixels (fp.pack, packet_kernel.h)
+    renders what one-sample-frame-per-tile tiles and k_average render, bit for
+    bit, on odd frame sizes (partial tiles) and a strided row shard."""
+    tris = golden_scene("suzanne.obj")
+    s = scene("suzanne.obj", "bsah", 8)
+    path = rt.CameraPath(rt.scene_center(tris), 36)
+    cams = [path.circular_path(f) for f in (3, 17, 30)]
+    for W, H, row0, stride in [(37, 23, 0, 1), (64, 48, 1, 3)]:
+        monkeypatch.setenv("RT_SPP_PACK", "0")
+        a = _spp_render(s, cams, W, H, spp, row0=row0, stride=stride)
+        monkeypatch.delenv("RT_SPP_PACK")
+        b = _spp_render(s, cams, W, H, spp, row0=row0, stride=stride)
+        for k in ("id", "dist", "pos", "rgb", "hits"):
+            assert np.array_equal(a[k], b[k]), (spp, W, H, k)
 
 
 def test_spp_row_shards_and_sponza_band(oracle):

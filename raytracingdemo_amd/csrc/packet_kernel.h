@@ -323,7 +323,7 @@ struct TileOut {
     uint32_t hits;  // fp.pack: on a pixel's first-sample lane, its samples hit
 };
 
-template <int W, int SP, int K, bool COUNT, bool FUSED>
+template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK>
 __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, bool valid,
                                                 uint32_t* __restrict__ wstack, uint2* __restrict__ cand) {
     const int lane = threadIdx.x & 63;
@@ -563,7 +563,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                 store_rgb(fp, ob, c);
                 res.hit = hit_s;
             }
-        } else if (fp.pack) {
+        } else if constexpr (PACK) {
             // the pixel's spp samples are lanes base .. base + spp - 1 of this
             // wave (sample k in lane base + k): each lane stores its sample's
             // outputs, the colours are summed in sample order across the lanes
@@ -825,7 +825,7 @@ constexpr int kPacketWaves = RT_PACKET_WAVES;
 #define RT_PACKET_ATTR
 #endif
 
-template <int W, int SP, int K, bool COUNT, bool FUSED>
+template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK = false>
 __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_packet(PacketArgs args) {
     __shared__ uint32_t stacks[kPacketWaves][SP];
     __shared__ uint2 cands[kPacketWaves][K * 64];
@@ -860,7 +860,7 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
         // fp.pack: a tile is ts x ts pixels of one pose with all spp samples
         // (ts = 8 / n), else 8 x 8 pixels of one sample frame
-        const bool pack = FUSED && kword(&A->fp.pack);
+        constexpr bool pack = FUSED && PACK;  // (launched only when fp.pack)
         const int spp = kword(&A->fp.spp);
         const int ts = pack ? 8 / kword(&A->fp.spp_n) : 8;
         const int tiles_x = (W_ + ts - 1) / ts;
@@ -895,7 +895,7 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
         const int fr = tile / tiles_f;  // frame of the batch (pose when packed)
         const int ft = tile - fr * tiles_f;
         int f = fr, i, r;
-        if (pack) {  // lane = pixel * spp + sample
+        if constexpr (pack) {  // lane = pixel * spp + sample
             const int pl = lane / spp;
             f = fr * spp + (lane & (spp - 1));
             i = (ft % tiles_x) * ts + pl % ts;
@@ -905,10 +905,10 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             r = (ft / tiles_x) * 8 + (lane >> 3);
         }
         const TileOut o =
-            trace_packet<W, SP, K, COUNT, FUSED>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);
+            trace_packet<W, SP, K, COUNT, FUSED, PACK>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);
         if constexpr (FUSED) {
             uint32_t h = (uint32_t)__builtin_popcountll(__ballot(o.hit));
-            if (pack) {  // samples hit per pixel (<= 64) summed over the wave
+            if constexpr (pack) {  // samples hit per pixel (<= 64) summed over the wave
                 h = 0;
 #pragma unroll
                 for (int b = 0; b < 7; b++) h += (uint32_t)__builtin_popcountll(__ballot((o.hits >> b) & 1u)) << b;

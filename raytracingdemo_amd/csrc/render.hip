@@ -785,13 +785,10 @@ bool split_resolve(int spp) {
 }
 // the packet pipeline needs the candidate buffers: the split resolve's lists,
 // or spp > 1 with the fused resolve (each sample's colour and status)
-// (spp 4 and 16 with the fused resolve: a wave sums a pixel's samples across
-// its lanes, nothing goes through HBM — the host's fp.pack rule)
-bool packs_samples(int spp) {
-    const char* e = getenv("RT_SPP_PACK");
-    return spp > 1 && 64 % spp == 0 && !(e && e[0] == '0');
-}
-bool needs_cand(int spp) { return (spp > 1 && !packs_samples(spp)) || split_resolve(spp); }
+// (pack: spp 4 and 16 on an 8-wide walk tree with the fused resolve — a wave
+// sums a pixel's samples across its lanes, nothing goes through HBM; the
+// host's fp.pack, rt_api.cpp pack_samples)
+bool needs_cand(int spp, bool pack) { return (spp > 1 && !pack) || split_resolve(spp); }
 
 template <int W>
 hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
@@ -803,14 +800,29 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     if (use_packet(sc.stack_bound)) {
         const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
         if (!split_resolve(fp.spp)) {
-            if (count)
+            // packed samples (fp.pack, 8-wide walk trees) in their own
+            // instantiation: its epilogue's registers stay out of spp = 1's
+            bool packed = false;
+            if constexpr (W == 8) {
+                if (fp.pack) {
+                    packed = true;
+                    if (count)
+                        hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, true, true>), pgrid,
+                                           pblk, 0, s, PacketArgs{sc, fp, aux});
+                    else
+                        hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true, true>), pgrid,
+                                           pblk, 0, s, PacketArgs{sc, fp, aux});
+                }
+            }
+            if (packed) {
+            } else if (count)
                 hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, true>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             else
                 hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true>), pgrid, pblk, 0, s,
                                    PacketArgs{sc, fp, aux});
             if (ev) (void)hipEventRecord(ev[1], s);
-            if (fp.spp > 1 && !fp.pack) {
+            if (fp.spp > 1 && !packed) {
                 const uint64_t bpf = ((uint64_t)fp.W * (uint64_t)fp.nrows + 255) / 256;
                 hipLaunchKernelGGL(k_average, dim3((unsigned)(bpf * (uint64_t)(fp.nframes / fp.spp))), blk, 0, s, fp,
                                    aux);
@@ -903,7 +915,7 @@ int exact_lds_stack() {
     return a < RT_PW_STACK ? a : RT_PW_STACK;
 }
 int packet_candidates() { return RT_CAND_LDS; }  // HBM list entries per pixel (spp > 1, wavefront paths)
-bool packet_split(int spp) { return needs_cand(spp); }
+bool packet_split(int spp, bool pack) { return needs_cand(spp, pack); }
 uint32_t params_bytes() { return (uint32_t)sizeof(RtFrameParams); }
 
 // Host entry: validates the launch geometry against what the kernels assume
@@ -943,7 +955,7 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     if (use_packet(sc.stack_bound) &&
         (!aux.redo || aux.redo_cap < bpix / (uint64_t)fp.spp || !aux.pool || aux.pgrid <= 0))
         return hipErrorInvalidValue;
-    if (use_packet(sc.stack_bound) && needs_cand(fp.spp) &&
+    if (use_packet(sc.stack_bound) && needs_cand(fp.spp, fp.pack && sc.width == 8) &&
         (!aux.cand || !aux.cand_cnt || !aux.cand_drop || !aux.cand_ovf || aux.cand_cap < bpix))
         return hipErrorInvalidValue;
     const bool packet = use_packet(sc.stack_bound);

@@ -31,7 +31,7 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
                            uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
-bool packet_split(int spp);
+bool packet_split(int spp, bool pack);
 uint32_t params_bytes();
 int exact_lds_stack();
 hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_off, int G, int F, int H, int W,
@@ -431,6 +431,14 @@ float frame_pad(const rt_scene* s, const rt_camera* c) {
 // and per sample frame its stratified sub-pixel offset: sample s of an
 // n x n pattern sits at ((s % n) + 0.5) / n, ((s / n) + 0.5) / n (spp = 1:
 // the reference's pixel centre 0.5, camera.hpp:35-37).
+// The fused packet walk takes a pixel's samples in one wave when they divide
+// it (spp 4, 16) and the walk tree is 8 wide; RT_SPP_PACK=0 keeps one sample
+// frame per tile (packet_kernel.h).
+bool pack_samples(const rt_scene* s, int spp) {
+    const char* pk = std::getenv("RT_SPP_PACK");
+    return spp > 1 && 64 % spp == 0 && s->flat.width == 8 && !(pk && pk[0] == '0');
+}
+
 RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row0, int row_stride, int nrows,
                            int spp = 1, int band = 1) {
     RtFrameParams fp{};
@@ -440,10 +448,7 @@ RtFrameParams frame_params(const rt_scene* s, const rt_camera* c, int n, int row
     // sample q of each pose sits at ((q % g) + 0.5) / g, ((q / g) + 0.5) / g
     // (computed in-kernel by frame_cam with these same expressions)
     fp.spp_n = spp_grid(spp);
-    // the fused packet walk takes a pixel's samples in one wave when they
-    // divide it (spp 4, 16, 64; RT_SPP_PACK=0 keeps one sample frame per tile)
-    const char* pk = std::getenv("RT_SPP_PACK");
-    fp.pack = spp > 1 && 64 % spp == 0 && !(pk && pk[0] == '0');
+    fp.pack = pack_samples(s, spp);
     for (int p = 0; p < n; p++) {
         RtPose k{};
         k.pad = frame_pad(s, &c[p]);
@@ -549,7 +554,7 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
     int per = std::max(1, batch_frames() / spp);
     while (per > 1 && fpix * (uint64_t)(per * spp) >= (1ull << 31)) per--;
     if (fpix * (uint64_t)spp >= (1ull << 31)) throw rt::Error{RT_ERR_INVALID_ARGUMENT, "image too large for spp"};
-    const bool split = mode == RT_MODE_EXACT && rt::packet_split(spp);
+    const bool split = mode == RT_MODE_EXACT && rt::packet_split(spp, pack_samples(s, spp));
     if (split) {
         // candidate lists in HBM (73 B per sample pixel): at most half of
         // the device memory that is free (or already ours), fewer poses
@@ -1096,7 +1101,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
             e1 = s->grp.ev1;
         } else {
             ensure_redo(r, npx);
-            if (mode == RT_MODE_EXACT && rt::packet_split(1)) ensure_cand(r, npx);
+            if (mode == RT_MODE_EXACT && rt::packet_split(1, false)) ensure_cand(r, npx);
             order_on(r, r.stream);
             HIP_TRY(hipEventRecord(r.ev0, r.stream));
             launch(s, r, fp, mode, false, r.stream, nullptr);

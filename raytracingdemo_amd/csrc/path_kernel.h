@@ -145,7 +145,11 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
 // COUNT (the counting pass, RT_FLAG_COUNT, W = 8 only): per-lane node steps,
 // triangle pre-filter and fp64 tests summed into the fetch counters for the
 // roofline's algorithmic bytes (bench.py --paths).
-template <int W, int S, bool COUNT = false>
+// PACK (fp.pack, 64 % spp == 0): a wave takes all spp samples of 64 / spp
+// pixels, one sample path per lane (lane = pixel * spp + sample; the pixels a
+// tw x th block), and the pixel's radiance is summed across its lanes in
+// sample order — the same additions as the per-lane sample loop.
+template <int W, int S, bool COUNT = false, bool PACK = false>
 __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
                                                int bounces) {
     __shared__ uint2 lds[S][256];
@@ -154,8 +158,16 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
 #endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int tiles_x = (fp.W + 7) >> 3;
-    const int tiles = tiles_x * ((fp.nrows + 7) >> 3);
+    const int spp = fp.spp;
+    int tw = 8, th = 8;  // pixels per tile
+    if constexpr (PACK) {
+        const int P = 64 / spp;
+        tw = 1;
+        while (tw * tw < P) tw <<= 1;
+        th = P / tw;
+    }
+    const int tiles_x = (fp.W + tw - 1) / tw;
+    const int tiles = tiles_x * ((fp.nrows + th - 1) / th);
     LaneStack<S> st;
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
@@ -164,15 +176,24 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         if (lane == 0) tile = (int)atomicAdd(aux.tile_ctr, 1u);
         tile = __shfl(tile, 0);
         if (tile >= tiles) break;
-        const int i = (tile % tiles_x) * 8 + (lane & 7);
-        const int r = (tile / tiles_x) * 8 + (lane >> 3);
+        int i, r, s0 = 0, s1 = spp;  // the lane's pixel and samples [s0, s1)
+        if constexpr (PACK) {
+            const int pl = lane / spp;
+            s0 = lane & (spp - 1);
+            s1 = s0 + 1;
+            i = (tile % tiles_x) * tw + pl % tw;
+            r = (tile / tiles_x) * th + pl / tw;
+        } else {
+            i = (tile % tiles_x) * 8 + (lane & 7);
+            r = (tile / tiles_x) * 8 + (lane >> 3);
+        }
         uint32_t hits = 0, segs = 0;  // segs: ray segments traced (RT_FLAG_COUNT)
         LaneCounts tot;               // COUNT: the lane's fetch counts over its paths
         if (i < fp.W && r < fp.nrows) {
             const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
             const size_t pix = (size_t)r * fp.W + i;
             double acc[3] = {0.0, 0.0, 0.0};
-            for (int s = 0; s < fp.spp; s++) {
+            for (int s = s0; s < s1; s++) {
                 const uint32_t seed = path_seed(frame, (uint32_t)j * (uint32_t)fp.W + (uint32_t)i, (uint32_t)s);
                 // primary ray through (i + u0, j + u1): gen_ray with the sample's offsets
                 RtFrameCam c1 = cam;
@@ -232,7 +253,19 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                 acc[1] = acc[1] + L[1];
                 acc[2] = acc[2] + L[2];
             }
-            store_rgb(fp, pix, acc);
+            if constexpr (PACK) {
+                // the pixel's samples are lanes base .. base + spp - 1
+                const int base = lane & ~(spp - 1);
+                double sum[3] = {0.0, 0.0, 0.0};
+                for (int k = 0; k < spp; k++) {
+                    sum[0] = sum[0] + __shfl(acc[0], base + k);
+                    sum[1] = sum[1] + __shfl(acc[1], base + k);
+                    sum[2] = sum[2] + __shfl(acc[2], base + k);
+                }
+                if (lane == base) store_rgb(fp, pix, sum);
+            } else {
+                store_rgb(fp, pix, acc);
+            }
         }
         wave_add<13>(fp.hit_count, hits);
         if (fp.counters) wave_add<20>(fp.counters, segs);

@@ -1038,8 +1038,13 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
         case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         case 8:
-            if (fp.counters)  // the counting pass: fetch counts too
+            // (fp.pack: a wave holds every sample of 64 / spp pixels)
+            if (fp.counters && fp.pack)  // the counting pass: fetch counts too
+                hipLaunchKernelGGL((k_paths<8, kPathStack, true, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+            else if (fp.counters)
                 hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+            else if (fp.pack)
+                hipLaunchKernelGGL((k_paths<8, kPathStack, false, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
             else
                 hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
             break;

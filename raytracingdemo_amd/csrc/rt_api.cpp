@@ -1016,6 +1016,12 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
         hipStream_t st = (hipStream_t)stream;
         RtFrameParams fp = frame_params(s, cam, 1, row0, row_stride, nrows);
         fp.spp = spp;  // samples per pixel of the paths (one frame: offsets come from the hash)
+        {
+            // a wave takes every sample of 64 / spp pixels, one path per lane
+            // (8-wide walk trees; RT_PATHS_PACK=0: one pixel per lane)
+            const char* e = std::getenv("RT_PATHS_PACK");
+            fp.pack = spp > 1 && 64 % spp == 0 && s->flat.width == 8 && !(e && e[0] == '0');
+        }
         fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;  // [0] += ray segments traced
         fp.hit_id = out->hit_id;
         fp.dist = out->dist;

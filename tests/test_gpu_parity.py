@@ -471,11 +471,12 @@ def _paths_render(s, pos, d, W, H, frame, spp, bounces, row0=0, stride=1):
 
 
 @pytest.mark.parametrize("model,spp,bounces", [("stanford-bunny.obj", 4, 4), ("suzanne.obj", 3, 2),
-                                               ("teapot.obj", 1, 0)])
+                                               ("teapot.obj", 1, 0), ("stanford-bunny.obj", 16, 2)])
 def test_paths_match_oracle(oracle, model, spp, bounces):
     """Diffuse paths (secondary rays, config c5's model at small size): every
     pixel colour, every sample's primary hit and the hit count equal the oracle;
-    bounces = 0 with one sample is a jittered primary render."""
+    bounces = 0 with one sample is a jittered primary render.  spp 4 and 16
+    run packed (a wave holds every sample of 16 / 4 pixels, path_kernel.h)."""
     tris = golden_scene(model)
     s = scene(model, "bsah", 8)
     b = oracle.bvh(tris, "bsah", 8)
@@ -492,6 +493,24 @@ def test_paths_match_oracle(oracle, model, spp, bounces):
         assert np.array_equal(g["rgb"], o["rgb"]), (frame, np.flatnonzero((g["rgb"] != o["rgb"]).any(1))[:10])
         assert g["hits"] == o["hits"], frame
         assert g["rgb"].max() > 0
+
+
+@pytest.mark.parametrize("spp", [2, 8, 16, 32])
+def test_paths_packed_equal_per_lane_samples(spp, monkeypatch):
+    """k_paths with every sample of 64 / spp pixels in one wave (one path per
+    lane, the radiance summed across lanes) equals one pixel per lane with
+    its samples in a loop, bit for bit: odd sizes, a strided shard."""
+    tris = golden_scene("suzanne.obj")
+    s = scene("suzanne.obj", "bsah", 8)
+    pos, d = rt.CameraPath(rt.scene_center(tris), 36).circular_path(11)
+    for W, H, row0, stride in [(37, 23, 0, 1), (50, 31, 2, 3)]:
+        monkeypatch.setenv("RT_PATHS_PACK", "0")
+        a = _paths_render(s, pos, d, W, H, 11, spp, 3, row0, stride)
+        monkeypatch.delenv("RT_PATHS_PACK")
+        b = _paths_render(s, pos, d, W, H, 11, spp, 3, row0, stride)
+        for k in ("id", "dist", "rgb", "hits"):
+            assert np.array_equal(a[k], b[k]), (spp, W, H, k)
+        assert b["rgb"].max() > 0
 
 
 def test_paths_sponza_proxy_shard(oracle):

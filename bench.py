@@ -304,19 +304,33 @@ def paths_cpu_baseline(tris, a, path, W, H, S, B):
     cores over whole rows of the same pose until ~cpu_seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
-    threads = int(os.environ.get("RT_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    host = host_cores()
+    threads = int(os.environ.get("RT_CPU_THREADS", host["usable"]))
     b = pyoracle.Oracle().bvh(tris, a.algo, a.k)
     pos, d = path.circular_path(0)
-    rows, spent, j = 0, 0.0, 0
-    while spent < a.cpu_seconds and rows < H:
-        n = max(1, threads // 4)
-        t0 = time.perf_counter()
-        b.render_paths(pos, d, W, H, 0, S, B, row0=j, nrows=min(n, H - j), threads=threads)
-        spent += time.perf_counter() - t0
-        rows += min(n, H - j)
-        j = (j + 97 * n) % (H - n)
-    return {"value": round(rows * W * S * (1 + B) / spent / 1e6, 4), "unit": "Mrays/s", "cores": threads,
-            "kind": "port", "sample": f"{rows} rows of {W} px x {S} spp x (1 + {B}) segments, pose 0 ({spent:.1f} s)"}
+
+    def leg(nthreads, budget_s):
+        rows, spent, j = 0, 0.0, 0
+        n = max(1, nthreads // 4)  # whole rows per call, spread over the image
+        while spent < budget_s and rows < H:
+            t0 = time.perf_counter()
+            b.render_paths(pos, d, W, H, 0, S, B, row0=j, nrows=min(n, H - j), threads=nthreads)
+            spent += time.perf_counter() - t0
+            rows += min(n, H - j)
+            j = (j + 97 * n) % (H - n)
+        return rows, spent
+
+    rows, spent = leg(threads, a.cpu_seconds)
+    rows1, spent1 = leg(1, a.cpu_seconds / 3)
+    rate = lambda r, s: round(r * W * S * (1 + B) / s / 1e6, 4)
+    return {"value": rate(rows, spent), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{rows} rows of {W} px x {S} spp x (1 + {B}) segments, pose 0 ({spent:.1f} s)",
+            "all_cores": {"value": rate(rows, spent), "cores": threads},
+            "one_core": {"value": rate(rows1, spent1), "cores": 1,
+                         "sample": f"{rows1} rows of {W} px, pose 0 ({spent1:.1f} s)"},
+            "host": host,
+            "note": "nominal rays (W x H x spp x (1 + bounces)) per second, as the GPU line; the reference has "
+                    "no path tracer, so the oracle's restatement of this build's model is timed"}
 
 
 def main():
@@ -486,17 +500,26 @@ def main():
     survey_bytes_per_ray = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
                             cs["rays"] * OUT_BYTES) / max(cs["rays"], 1)
     fused = cs["wave_tiles"] and os.environ.get("RT_RESOLVE", "")[:1] != "s"
+    walk_bytes = cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES
+    conventions = None
     if fused:
-        # packet traversal kernel with the fused resolve (the dominant kernel):
-        # a node or triangle record is fetched once per wave for its 64 rays;
-        # per ray the Moller-Trumbore part of each exact test, the winner's
-        # shading fields, the ancestor boxes re-verified and the outputs
-        # (rays are generated in-kernel: no camera reads)
-        # (spp > 1: per sample its outputs, colour and status for k_average)
-        trace_bytes = (cs["wave_nodes"] * nb + cs["wave_tris"] * TRI32_BYTES + cs["tri_tests"] * MT64_BYTES +
-                       cs["hits"] * WIN_BYTES + cs["chain_nodes"] * CHAIN_BYTES +
-                       cs["rays"] * (OUT_BYTES if S == 1 else
-                                     PACKED_SAMPLE_BYTES + 3.0 / S if packed_spp(S) else SAMPLE_BYTES))
+        # packet traversal kernel with the fused resolve (the dominant kernel),
+        # every record counted once per wave: a node or fp32 triangle record
+        # fetched once for the wave's 64 rays, and the fp64 records the lanes
+        # resolve counted once per wave-distinct triangle (the Moller-Trumbore
+        # part per candidate, the shading part per winner: neighbouring rays
+        # test and hit the same triangles); per lane the ancestor boxes
+        # re-verified and the outputs (rays are generated in-kernel: no camera
+        # reads; spp > 1: per sample its outputs, colour and status)
+        out_bytes = cs["rays"] * (OUT_BYTES if S == 1 else
+                                  PACKED_SAMPLE_BYTES + 3.0 / S if packed_spp(S) else SAMPLE_BYTES)
+        resolve_lane = cs["tri_tests"] * MT64_BYTES + cs["hits"] * WIN_BYTES + cs["chain_nodes"] * CHAIN_BYTES
+        resolve_wave = (cs["wave_tri_tests"] * MT64_BYTES + cs["wave_winners"] * WIN_BYTES +
+                        cs["chain_nodes"] * CHAIN_BYTES)
+        trace_bytes = walk_bytes + resolve_wave + out_bytes
+        conventions = {"per_wave": trace_bytes / F, "walk_only": walk_bytes / F,
+                       "walk_and_outputs": (walk_bytes + out_bytes) / F,
+                       "per_lane_resolve": (walk_bytes + resolve_lane + out_bytes) / F}
     elif cs["wave_tiles"]:
         # packet traversal kernel, split resolve: the walk plus the candidate
         # lists it writes
@@ -556,6 +579,9 @@ def main():
     frames_per_launch = frames_timed / launches_timed if ks["timed_launches"] else 1.0
     alg_bytes_per_launch = alg_bytes_per_frame * frames_per_launch
     achieved = alg_bytes_per_launch / avg_kernel_s / 1e9
+    # the same kernel time against the other byte conventions (GB/s)
+    rates = ({k: v * frames_per_launch / avg_kernel_s / 1e9 for k, v in conventions.items()}
+             if conventions else {})
 
     if rank == 0:
         key = (f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}|fpl{frames_per_launch:g}" + (f"|spp{S}" if S > 1 else "")
@@ -614,7 +640,16 @@ def main():
                        **({"gather_verified": verified} if world > 1 else {}),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "valu": valu,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         **({"convention": "every record once per wave (walk nodes and fp32 triangles per node "
+                                           "step; fp64 records per wave-distinct triangle tested / won); ancestor "
+                                           "boxes and outputs per ray",
+                             "frac_walk": round(rates["walk_only"] / HBM_PEAK_GBS, 4),
+                             "frac_walk_and_outputs": round(rates["walk_and_outputs"] / HBM_PEAK_GBS, 4),
+                             "frac_per_lane_resolve": round(rates["per_lane_resolve"] / HBM_PEAK_GBS, 4),
+                             **({"frac_dram": round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4)}
+                                if traffic else {})} if rates else {}),
+                         "valu": valu,
                          "kernel": ("k_trace_packet (walk + fused exact resolve)" if fused else
                                     "k_trace_packet (walk)" if cs["wave_tiles"] else "k_trace_exact"),
                          "kernel_ms_avg": round(avg_kernel_s * 1e3, 4),
@@ -627,6 +662,8 @@ def main():
                          "per_ray": {"node_fetches": round(cs["node_fetches"] / max(cs["rays"], 1), 3),
                                      "tri_prefilter": round(cs["tri_prefilter"] / max(cs["rays"], 1), 3),
                                      "tri_tests_fp64": round(cs["tri_tests"] / max(cs["rays"], 1), 3),
+                                     "wave_tri_tests_per_tile": round(cs["wave_tri_tests"] / max(cs["wave_tiles"], 1), 2),
+                                     "wave_winners_per_tile": round(cs["wave_winners"] / max(cs["wave_tiles"], 1), 2),
                                      "chain_checks": round(cs["chain_checks"] / max(cs["rays"], 1), 4),
                                      "chain_nodes": round(cs["chain_nodes"] / max(cs["rays"], 1), 4),
                                      "wave_nodes_per_tile": round(cs["wave_nodes"] / max(cs["wave_tiles"], 1), 2),

@@ -134,7 +134,11 @@ typedef struct {
                                dropped (certified bound, else fix-up)      */
     uint64_t empty_node_steps; /* packet kernel: node steps where no lane entered
                                   any child                                */
-    uint64_t reserved[9];
+    uint64_t wave_tri_tests; /* packet kernel, fused resolve: fp64 triangle records
+                                tested, counted once per wave (distinct over its
+                                lanes; tri_tests counts them per lane)     */
+    uint64_t wave_winners;   /*   winners' shading records, once per wave  */
+    uint64_t reserved[7];
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */
@@ -195,9 +199,10 @@ int rt_scene_create_on_device(const double *tri_v, uint64_t n_tris, int algo, in
 int rt_scene_build_times(const rt_scene *s, rt_build_times_t *out);
 
 /* Replicate the flattened scene on each listed HIP device (ordinal).  With
- * more than one device the library also creates an RCCL communicator over
- * them (ncclCommInitAll, one rank per device in this process; rank g = the
- * g-th uploaded device), used by rt_render_frame / rt_render_batch_multi. */
+ * more than one device, the first rt_render_frame / rt_render_batch_multi
+ * creates an RCCL communicator over them (ncclCommInitAll, one rank per device
+ * in this process; rank g = the g-th uploaded device); uploading itself never
+ * needs RCCL. */
 int rt_scene_upload(rt_scene *s, const int *devices, int n_devices);
 
 /* One whole frame, blocking; replaces calculateScreen + shadeScreen
@@ -231,9 +236,10 @@ int rt_shard_height(int height, int nshards, int shard);
  * With G > 1 devices the frames are sharded as rt_render_shard_device's, each device
  * renders its rows of every pose, and one RCCL gather per call brings the
  * shards to the first device, which de-interleaves them; hit_count[f] adds
- * all shards.  Results are identical to a one-device render.  (Test hook:
+ * all shards.  Results are identical to a one-device render.  (Test hooks:
  * RT_VIRTUAL_SHARDS=N shards a one-device scene into N row shards on that
- * device, gathered with device copies.) */
+ * device, gathered with device copies; RT_GROUP_RCCL=1 sends a one-device
+ * scene through the RCCL gather with a one-rank communicator.) */
 int rt_render_batch_multi(rt_scene *s, const rt_camera *cams, int nframes, int spp, int mode, const rt_device_out *out,
                           void *stream, uint32_t flags);
 

@@ -76,7 +76,8 @@ class rt_frame_stats_t(C.Structure):
                 ("tri_prefilter", C.c_uint64), ("wave_nodes", C.c_uint64), ("wave_leaves", C.c_uint64),
                 ("wave_tiles", C.c_uint64), ("wave_tris", C.c_uint64), ("redo_rays", C.c_uint64), ("redo_chain", C.c_uint64),
                 ("spilled_rays", C.c_uint64), ("dropped_rays", C.c_uint64), ("empty_node_steps", C.c_uint64),
-                ("reserved", C.c_uint64 * 9), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
+                ("wave_tri_tests", C.c_uint64), ("wave_winners", C.c_uint64),
+                ("reserved", C.c_uint64 * 7), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
 
 
 class rt_build_times_t(C.Structure):

@@ -10,6 +10,7 @@
 // yields the same permutation as sorting the reference's Primitive* vector.
 // Compiled with -ffp-contract=off (the reference's x86-64 -O0 build had no FMA).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -43,13 +44,30 @@ inline double area(const Box& b) {
     return 2.0 * (ex * ey + ey * ez + ez * ex);
 }
 
-// Runs f on a new thread kept in `th`, or here when no thread can be made
-// (the result is the same either way).
+// Threads alive in the builders at once, over every spawn site (subtrees
+// and the sorts inside them nest): past the budget work runs inline.
+std::atomic<int> g_live_threads{0};
+int thread_budget() {
+    static const int b = (int)std::max(2u, std::min(32u, std::thread::hardware_concurrency()));
+    return b;
+}
+
+// Runs f on a new thread kept in `th`, or here when the thread budget is
+// spent or no thread can be made (the result is the same either way).
 template <class F>
 void spawn(std::vector<std::thread>& th, F&& f) {
+    if (g_live_threads.fetch_add(1) >= thread_budget()) {
+        g_live_threads.fetch_sub(1);
+        f();
+        return;
+    }
     try {
-        th.emplace_back(f);
+        th.emplace_back([f]() mutable {
+            f();
+            g_live_threads.fetch_sub(1);
+        });
     } catch (const std::system_error&) {
+        g_live_threads.fetch_sub(1);
         f();
     }
 }
@@ -877,6 +895,27 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
     } else {
         f.root_ref = F.ref_of(0, 0);
         if (f.n_wide == 0) F.alloc_node();  // root is a leaf: keep a valid node array
+    }
+    // Each child record's pad word carries the CHILD node's ordering meta
+    // (sort axis | valid slots << 2; slot 0's pad held the node's own meta
+    // until here), so the packet kernel knows a node's valid slots before it
+    // loads the node and loads and tests only those (packet_kernel.h); leaf
+    // and empty slots get 0.  The root's meta is root_meta.  The packet
+    // kernel carries a node's meta in bits 24-30 of its ref: node ids stay
+    // below 2^24.
+    if (f.n_wide >= (1u << 24)) throw Error{RT_ERR_INVALID_ARGUMENT, "scene too large (wide nodes)"};
+    {
+        const uint64_t nb = rt_node_bytes(W);
+        std::vector<uint32_t> meta(f.n_wide);
+        for (uint64_t x = 0; x < f.n_wide; x++) meta[x] = reinterpret_cast<const uint32_t*>(f.wide.data() + x * nb)[7];
+        for (uint64_t x = 0; x < f.n_wide; x++) {
+            uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + x * nb);
+            for (int c = 0; c < W; c++) {
+                const uint32_t r = p[8 * c + RT_CHILD_REF];
+                p[8 * c + 7] = (r != RT_INVALID_REF && !(r & RT_LEAF_BIT)) ? meta[r] : 0u;
+            }
+        }
+        f.root_meta = (f.root_ref != RT_INVALID_REF && !(f.root_ref & RT_LEAF_BIT)) ? meta[f.root_ref] : 0u;
     }
     // ordered traversal pushes at most W-1 siblings per wide level
     f.stack_bound = F.wide_depth * (uint32_t)(W - 1) + 1;

@@ -111,6 +111,28 @@ __device__ __forceinline__ void pin_s(const float4& a, const float4& b, const fl
                  "s"(c.y), "s"(c.z), "s"(c.w));
 }
 
+// RT_PROFILE=1 (a measurement build, never shipped): the timed kernel adds
+// shader-clock cycles per phase of each tile to the counters (18: ray set-up,
+// 19: node steps, 20: leaf steps, 21: resolve and stores, 22: tiles, 23:
+// whole tiles; tools/phase_profile.py reads them with rt_diag_raw).  The
+// s_memtime reads cost some overlap; the proportions are what it is for.
+#ifndef RT_PROFILE
+#define RT_PROFILE 0
+#endif
+constexpr bool kProfile = RT_PROFILE != 0;
+__device__ __forceinline__ uint64_t prof_clock() {
+    if constexpr (kProfile) return (uint64_t)__builtin_amdgcn_s_memtime();
+    return 0;
+}
+
+#ifndef RT_PIN_REC
+#define RT_PIN_REC 1
+#endif
+__device__ __forceinline__ void pin_rec(const ChildRec& r) {
+    if constexpr (RT_PIN_REC)
+        asm volatile("" ::"s"(r.lx), "s"(r.hx), "s"(r.ly), "s"(r.hy), "s"(r.lz), "s"(r.hz), "s"(r.ref), "s"(r.pad));
+}
+
 // Lane-private candidate list: entry c of lane l at cand[c * 64 + l]
 // ({triangle, bits of t lower bound}; consecutive lanes -> consecutive 8-B
 // words, conflict-free ds_read/write_b64).
@@ -206,6 +228,35 @@ __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32&
         }
         hm[c] = __ballot(t0 <= t1);
     }
+}
+
+// Which of a node's nv valid children (a prefix of the W slots) any lane's
+// ray enters, as a bit mask.  The wide nodes of the walk tree hold 4.1 valid
+// children on average: for W = 8 the slots are tested in groups (RT_SLOT_GROUP
+// slots each) and a group past nv is skipped with a uniform branch.  The
+// records stay loaded unconditionally (no value flows out of a branch but
+// the mask), so the skipped VALU costs no register copies.
+#ifndef RT_SLOT_GROUP
+#define RT_SLOT_GROUP 8
+#endif
+template <int W, int OCT>
+__device__ __forceinline__ uint32_t node_mask(const float (&bx)[W][6], const Ray32& q, const f2 nox, const f2 noy,
+                                              const f2 noz, float tcull, uint32_t nv) {
+    constexpr int G = (W == 8 && RT_SLOT_GROUP < 8) ? RT_SLOT_GROUP : W;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int g0 = 0; g0 < W; g0 += G) {
+        if (g0 > 0 && nv <= (uint32_t)g0) break;  // (nv >= 1: group 0 is always tested)
+        float b[G][6];
+#pragma unroll
+        for (int c = 0; c < G; c++)
+#pragma unroll
+            for (int a = 0; a < 6; a++) b[c][a] = bx[g0 + c][a];
+        uint64_t hm[G];
+        child_hits<G, OCT>(b, q, nox, noy, noz, tcull, hm);
+        mask |= any_mask<G>(hm) << g0;
+    }
+    return mask & ((1u << nv) - 1u);
 }
 
 // Per-lane counters of the counting pass (RT_FLAG_COUNT).
@@ -317,6 +368,34 @@ __device__ __forceinline__ uint32_t resolve_list(const RtDevScene& sc, const RtF
     return 0;
 }
 
+// Counting pass only: distinct values over the wave's active lanes, lane l
+// contributing get(0) .. get(n - 1) (n <= 32).  The fused resolve fetches the
+// fp64 record of every candidate a lane tests; neighbouring rays test the
+// same triangles, so a record read by several lanes of the wave is one fetch
+// — the per-wave convention the walk's node and triangle records are counted
+// in (bench.py roofline).
+template <class GetFn>
+__device__ uint32_t wave_distinct(uint32_t n, GetFn&& get) {
+    uint32_t done = 0, count = 0;
+    for (;;) {
+        uint32_t mine = 0;
+        bool have = false;
+        for (uint32_t c = 0; c < n; c++)
+            if (!((done >> c) & 1u)) {
+                mine = get(c);
+                have = true;
+                break;
+            }
+        const uint64_t act = __ballot(have);
+        if (act == 0) break;
+        const uint32_t u = (uint32_t)__shfl((int)mine, (int)__builtin_ctzll(act));
+        count++;
+        for (uint32_t c = 0; c < n; c++)
+            if (!((done >> c) & 1u) && get(c) == u) done |= 1u << c;
+    }
+    return count;
+}
+
 // Outcome of one tile for the caller's per-frame hit count (FUSED).
 struct TileOut {
     bool hit;       // the lane's pixel is resolved here and hit
@@ -327,6 +406,9 @@ template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK>
 __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, bool valid,
                                                 uint32_t* __restrict__ wstack, uint2* __restrict__ cand) {
     const int lane = threadIdx.x & 63;
+    const uint64_t p0 = prof_clock();
+    uint64_t p_node = 0, p_leaf = 0, p_prev = 0;  // RT_PROFILE only
+    bool prev_node = false;
     if (!valid) { i = 0; r = 0; }
     Ray32 q;
     float tsl;  // distance slack (see trace_exact), fp32 rounded up
@@ -335,8 +417,10 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     {
         const RtFrameParams fp = kload(&A->fp);
         const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f / fp.spp]), fp, f);  // this tile's frame
-        const Ray64 ray = gen_ray(fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r));
-        q = make_ray32(ray, cam.pad);
+        // kFastInv: the fp32 reciprocals straight from the fp32 direction
+        // (v_rcp_f32 + a Newton step: no fp64 divisions in the set-up)
+        const Ray64 ray = gen_ray<!kFastInv>(fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r));
+        q = make_ray32<kFastInv>(ray, cam.pad);
         tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
         pd = cam.pad;
         // the lane's pixel in the batch (< 2^31, host-checked)
@@ -361,7 +445,10 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     int nsp = 0;                         // candidates in the lane's overflow chunk
     uint32_t chunk = kNoChunk;           // the lane's overflow pool chunk
     float drop = __builtin_huge_valf();  // smallest t lower bound of a dropped candidate
+    // node refs carry the node's meta (sort axis | valid slots << 2, from the
+    // parent's record; bvh_build.cpp flatten) in bits 24-30
     uint32_t cur = kword(&A->sc.root_ref);
+    if (!(cur & RT_LEAF_BIT)) cur |= kword(&A->sc.root_meta) << 24;
     {
         float b[6];
         for (int a = 0; a < 6; a++) b[a] = kword(&A->sc.root_box[a]);
@@ -377,37 +464,50 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     // The walk, specialised on the tile's octant (one dispatch per tile, not
     // per node step: 9 copies of the loop).  Every popped ref is a real node
     // or leaf, so only the root can be invalid: tested once, not per step.
+    const uint64_t p1 = prof_clock();
+    p_prev = p1;
     auto walk = [&]<int OCT>() __attribute__((always_inline)) {
         if (cur == RT_INVALID_REF) return;
         for (;;) {
+            if constexpr (kProfile) {  // the previous step's cycles to its bucket
+                const uint64_t now = prof_clock();
+                (prev_node ? p_node : p_leaf) += now - p_prev;
+                p_prev = now;
+                prev_node = !(cur & RT_LEAF_BIT);
+            }
             if (!(cur & RT_LEAF_BIT)) {
                 if (COUNT) {
                     w_nodes++;
                     n_nodes += valid;
                 }
                 float bx[W][6];  // child boxes {lx, hx, ly, hy, lz, hz}
-                uint32_t rs[W];  // the children's refs (scalars)
-                uint32_t meta;   // slot 0's pad: sort axis | valid slots << 2 (bvh_build.cpp set_meta)
+                uint32_t rs[W];  // the children's refs (scalars), their nodes' meta in bits 24-30
+                const uint32_t meta = cur >> 24;  // sort axis | valid slots << 2
+                const uint32_t nv = meta >> 2;    // valid slots (a prefix)
+                uint32_t mask;   // bit c: some lane's ray enters child c
                 {
-                    // all W records are loaded before any branch so their
-                    // loads are in flight together
-                    const cchild_p nb = (cchild_p)(nodes + (size_t)cur * (32 * W));
+                    // all W records are loaded before any test so their loads
+                    // are in flight together
+                    const cchild_p nb = (cchild_p)(nodes + (size_t)(cur & 0x00FFFFFFu) * (32 * W));
                     ChildRec ch[W];
 #pragma unroll
                     for (int c = 0; c < W; c++) ch[c] = load_child(nb + c);
+                    // every record is materialised here: the compiler would
+                    // otherwise sink the loads of skipped slot groups into
+                    // their branches (a second round trip per node step)
+#pragma unroll
+                    for (int c = 0; c < W; c++) pin_rec(ch[c]);
 #pragma unroll
                     for (int c = 0; c < W; c++) {
                         bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;
                         bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
                     }
-                    // the ref words come with the boxes (same scalar loads)
+                    // the ref words come with the boxes (same scalar loads);
+                    // an inner child's ref gets its node's meta (leaf pads are 0)
 #pragma unroll
-                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref;
-                    meta = ch[0].pad;
+                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref | (ch[c].pad << 24);
+                    mask = node_mask<W, OCT>(bx, q, nox, noy, noz, tcull, nv);
                 }
-                uint64_t hm[W];  // per child: lanes whose ray enters it
-                child_hits<W, OCT>(bx, q, nox, noy, noz, tcull, hm);
-                const uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);
                 if (COUNT) w_empty += mask == 0;
                 if (mask != 0) {
                     // children are sorted along `axis`: walk them front to back
@@ -513,6 +613,11 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         case 7: walk.template operator()<7>(); break;
         default: walk.template operator()<-1>(); break;
     }
+    uint64_t p2 = 0;
+    if constexpr (kProfile) {
+        p2 = prof_clock();
+        (prev_node ? p_node : p_leaf) += p2 - p_prev;
+    }
     A = launder(A);
     const RtFrameParams fp = kload(&A->fp);
     if (COUNT && fp.counters && lane == 0) {
@@ -523,7 +628,23 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         atomicAdd(&fp.counters[15], (unsigned long long)w_empty);
     }
     TileOut res{false, 0u};
-    if (!valid) return res;
+    auto prof_out = [&]() __attribute__((always_inline)) {
+        if constexpr (kProfile) {
+            const uint64_t p3 = prof_clock();
+            if (fp.counters && lane == (int)__builtin_ctzll(__ballot(true))) {
+                atomicAdd(&fp.counters[18], (unsigned long long)(p1 - p0));
+                atomicAdd(&fp.counters[19], (unsigned long long)p_node);
+                atomicAdd(&fp.counters[20], (unsigned long long)p_leaf);
+                atomicAdd(&fp.counters[21], (unsigned long long)(p3 - p2));
+                atomicAdd(&fp.counters[22], 1ull);
+                atomicAdd(&fp.counters[23], (unsigned long long)(p3 - p0));
+            }
+        }
+    };
+    if (!valid) {
+        if (__ballot(true) == ~0ull) prof_out();  // (a wholly invalid tile)
+        return res;
+    }
     const RtLaunchAux aux = kload(&A->aux);
     const bool dropped = drop < __builtin_huge_valf() && drop <= tcull;  // a dropped candidate could still win
     if (chunk != kNoChunk && chunk != kPoolDry && nsp < RT_POOL_CHUNK)  // terminate the chunk
@@ -555,7 +676,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
             if (redo) {
                 // k_fixup redoes the pixel with the exact per-lane path
                 const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-                aux.redo[slot] = ob | (redo == 2u ? kRedoPass1 : 0u);
+                if (slot < aux.redo_cap) aux.redo[slot] = ob | (redo == 2u ? kRedoPass1 : 0u);
             } else {
                 store_sample(fp, ob, out, sh);
                 double c[3];
@@ -590,7 +711,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                 const size_t pix = out_index(fp, pose, po);
                 if (bad) {
                     const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-                    aux.redo[slot] = (uint32_t)pix;
+                    if (slot < aux.redo_cap) aux.redo[slot] = (uint32_t)pix;
                 } else {
                     store_rgb(fp, pix, acc);
                     res.hits = (uint32_t)__builtin_popcountll(hm);
@@ -616,6 +737,20 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
             }
         }
         if (COUNT && fp.counters) {
+            // wave-distinct fp64 records: the candidates' Moller-Trumbore parts
+            // and the winners' shading parts (one wave-level fetch each)
+            static_assert(K + RT_POOL_CHUNK <= 32, "one bit per list entry");
+            uint32_t nch = 0;
+            if (ch)
+                while (nch < (uint32_t)RT_POOL_CHUNK && ch[nch].x != ~0u) nch++;
+            const uint32_t u_tests = wave_distinct(nl + nch, [&](uint32_t c) {
+                return c < nl ? cand[c * 64 + lane].x : ch[c - nl].x;
+            });
+            const uint32_t u_win = wave_distinct(out.tri >= 0 ? 1u : 0u, [&](uint32_t) { return (uint32_t)out.tri; });
+            if (lane == (int)__builtin_ctzll(__ballot(true))) {
+                atomicAdd(&fp.counters[16], (unsigned long long)u_tests);
+                atomicAdd(&fp.counters[17], (unsigned long long)u_win);
+            }
             atomicAdd(&fp.counters[0], 1ull);
             atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
             atomicAdd(&fp.counters[2], (unsigned long long)rc.tris);
@@ -628,6 +763,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
             if (spilled) atomicAdd(&fp.counters[13], 1ull);
             if (dropped) atomicAdd(&fp.counters[14], 1ull);
         }
+        prof_out();
     } else {
         // hand the lane's surviving candidates to k_resolve: count per
         // pixel, entry c of batch pixel o at cand[c * npix + o] (coalesced
@@ -719,7 +855,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
         if (redo_any) {
             // k_fixup redoes every sample of the pixel with the exact per-lane path
             const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-            aux.redo[slot] = (uint32_t)pix;
+            if (slot < aux.redo_cap) aux.redo[slot] = (uint32_t)pix;
             hits = 0;
         } else {
             store_rgb(fp, pix, acc);
@@ -781,7 +917,7 @@ __global__ void __launch_bounds__(256) k_average(RtFrameParams fp, RtLaunchAux a
         const size_t pix = out_index(fp, p, po);
         if (redo) {
             const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-            aux.redo[slot] = (uint32_t)pix;
+            if (slot < aux.redo_cap) aux.redo[slot] = (uint32_t)pix;
             hits = 0;
         } else {
             store_rgb(fp, pix, acc);
@@ -894,15 +1030,16 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
         if (tile >= tiles) break;
         const int fr = tile / tiles_f;  // frame of the batch (pose when packed)
         const int ft = tile - fr * tiles_f;
+        const int ty = ft / tiles_x, tx = ft - ty * tiles_x;
         int f = fr, i, r;
         if constexpr (pack) {  // lane = pixel * spp + sample
             const int pl = lane / spp;
             f = fr * spp + (lane & (spp - 1));
-            i = (ft % tiles_x) * ts + pl % ts;
-            r = (ft / tiles_x) * ts + pl / ts;
+            i = tx * ts + pl % ts;
+            r = ty * ts + pl / ts;
         } else {
-            i = (ft % tiles_x) * 8 + (lane & 7);
-            r = (ft / tiles_x) * 8 + (lane >> 3);
+            i = tx * 8 + (lane & 7);
+            r = ty * 8 + (lane >> 3);
         }
         const TileOut o =
             trace_packet<W, SP, K, COUNT, FUSED, PACK>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);
@@ -924,6 +1061,410 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
         }
     }
     if (FUSED && hacc != 0 && lane == 0)
+        atomicAdd(kload(&launder(A)->aux.tile_ctr) + RT_HIT_BASE + (hf * RT_HIT_SLOTS + hslot) * RT_QUEUE_STRIDE,
+                  hacc);
+}
+
+// v_mbcnt_lo_u32_b32: bits of m set below this lane (lanes 0-31; m = ~0: the
+// lane id).  volatile: recomputed at each use rather than held across a loop.
+__device__ __forceinline__ uint32_t mbcnt_lo(uint32_t m) {
+    uint32_t v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, %1, 0" : "=v"(v) : "s"(m));
+    return v;
+}
+
+// --------------------------------------------------------------------------
+// R rays per lane (spp = 1, fused resolve): a wave walks an (8 R) x 8 pixel
+// tile, lane l holding the R horizontally adjacent pixels (8 R tx + R (l & 7)
+// + k, 8 ty + (l >> 3)), k < R.  Node steps per tile grow far slower than the
+// tile (the tree's depth sets most of them: 8x8 tiles 12.36 per tile, 4x4
+// pixels of packed samples 11.47), while a node step's scalar work — the
+// child-record loads and their round trip, the any-lane mask, the near-child
+// pick, the pushes and pops — is paid once per wave however many rays test
+// the children.  With R = 2 each step serves 128 rays.
+//
+// Each ray keeps K LDS candidates (entry c of ray k of lane l at
+// cand[(c R + k) 64 + l]: R K entries per lane, the same LDS as the
+// one-ray kernel's K R); past them the K nearest lower bounds are kept and
+// the smallest dropped bound certifies the winner (else the pixel is redone
+// by k_fixup) — no overflow pool.  The resolve runs ray by ray.
+// Returns the lane's hits (bit k: ray k resolved here and hit).
+template <int W, int SP, int K, int R, bool COUNT>
+__device__ __forceinline__ uint32_t trace_packet_r(args_p A, int f, int i0, int r, const bool (&valid)[R],
+                                                   uint32_t* __restrict__ wstack, uint2* __restrict__ cand) {
+    const int lane = threadIdx.x & 63;
+    Ray32 q[R];
+    float tsl, pd;
+    uint32_t ob0;  // the lane's first pixel in the batch (ray k: ob0 + k)
+    {
+        const RtFrameParams fp = kload(&A->fp);
+        const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f]), fp, f);
+        const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, valid[0] ? r : 0);
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            const Ray64 ray = gen_ray(fp, cam, valid[k] ? i0 + k : 0, j);
+            q[k] = make_ray32(ray, cam.pad);
+        }
+        tsl = round_up_f(0x1p-40 * ((double)q[0].co + 1.0));
+        pd = cam.pad;
+        ob0 = (uint32_t)out_index(fp, f, (size_t)(valid[0] ? r : 0) * fp.W + (valid[0] ? i0 : 0));
+    }
+    // the tile's octant: lane 0's first ray's direction signs, if every ray
+    // that takes part shares them (else 8, the general slab test)
+    uint32_t lsg[R];
+    bool mixed = false;
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        lsg[k] = (q[k].ix < 0.f ? 1u : 0u) | (q[k].iy < 0.f ? 2u : 0u) | (q[k].iz < 0.f ? 4u : 0u);
+    }
+    const uint32_t dsg = uni(lsg[0]);
+#pragma unroll
+    for (int k = 0; k < R; k++) mixed |= valid[k] && lsg[k] != dsg;
+    const int oct = __ballot(mixed) == 0 ? (int)dsg : 8;
+    const RT_G uint8_t* const nodes = kload(&A->sc.nodes);
+    const RT_G float* const tri32 = kload(&A->sc.tri32);
+    f2 nox[R], noy[R], noz[R];
+    float tcull[R], drop[R];
+    int nc[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        nox[k] = f2{-(q[k].ox + pd) * q[k].ix, -(q[k].ox - pd) * q[k].ix};
+        noy[k] = f2{-(q[k].oy + pd) * q[k].iy, -(q[k].oy - pd) * q[k].iy};
+        noz[k] = f2{-(q[k].oz + pd) * q[k].iz, -(q[k].oz - pd) * q[k].iz};
+        tcull[k] = valid[k] ? __builtin_huge_valf() : -1.f;
+        drop[k] = __builtin_huge_valf();
+        nc[k] = 0;
+    }
+    uint32_t n_nodes = 0, n_pre = 0, w_nodes = 0, w_leaves = 0, w_tris = 0, w_empty = 0;  // COUNT only
+    uint32_t cur = kword(&A->sc.root_ref);
+    if (!(cur & RT_LEAF_BIT)) cur |= kword(&A->sc.root_meta) << 24;
+    {
+        float b[1][6];
+        for (int a = 0; a < 6; a++) b[0][a] = kword(&A->sc.root_box[a]);
+        uint64_t any = 0;
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+            uint64_t h[1];
+            child_hits<1, -1>(b, q[k], nox[k], noy[k], noz[k], tcull[k], h);
+            any |= h[0];
+        }
+        if (any == 0) cur = RT_INVALID_REF;
+    }
+    int sp = 0;
+    // candidate list of ray k: entry c at cand[(c * R + k) * 64 + lane]
+    auto entry = [&](int c, int k) -> uint2& { return cand[(c * R + k) * 64 + lane]; };
+    auto walk = [&]<int OCT>() __attribute__((always_inline)) {
+        if (cur == RT_INVALID_REF) return;
+        for (;;) {
+            if (!(cur & RT_LEAF_BIT)) {
+                if (COUNT) w_nodes++;
+                float bx[W][6];
+                uint32_t rs[W];
+                const uint32_t meta = cur >> 24;
+                const uint32_t nv = meta >> 2;
+                uint64_t hm[W];
+                {
+                    const cchild_p nb = (cchild_p)(nodes + (size_t)(cur & 0x00FFFFFFu) * (32 * W));
+                    ChildRec ch[W];
+#pragma unroll
+                    for (int c = 0; c < W; c++) ch[c] = load_child(nb + c);
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;
+                        bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
+                    }
+#pragma unroll
+                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref | (ch[c].pad << 24);
+                    // child c is needed if any ray of any lane enters it
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        bool in = false;
+#pragma unroll
+                        for (int k = 0; k < R; k++) {
+                            const float (&bc)[6] = bx[c];
+                            const float tlx = __builtin_fmaf(bc[0], q[k].ix, nox[k].x),
+                                        thx = __builtin_fmaf(bc[1], q[k].ix, nox[k].y);
+                            const float tly = __builtin_fmaf(bc[2], q[k].iy, noy[k].x),
+                                        thy = __builtin_fmaf(bc[3], q[k].iy, noy[k].y);
+                            const float tlz = __builtin_fmaf(bc[4], q[k].iz, noz[k].x),
+                                        thz = __builtin_fmaf(bc[5], q[k].iz, noz[k].y);
+                            float t0, t1;
+                            if constexpr (OCT < 0) {
+                                t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
+                                t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fminf(fmaxf(tlz, thz), tcull[k]));
+                            } else {
+                                const float nx = (OCT & 1) ? thx : tlx, fx = (OCT & 1) ? tlx : thx;
+                                const float ny = (OCT & 2) ? thy : tly, fy = (OCT & 2) ? tly : thy;
+                                const float nz = (OCT & 4) ? thz : tlz, fz = (OCT & 4) ? tlz : thz;
+                                t0 = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+                                t1 = fminf(fminf(fx, fy), fminf(fz, tcull[k]));
+                            }
+                            in |= t0 <= t1;
+                        }
+                        hm[c] = __ballot(in);
+                    }
+                }
+                const uint32_t mask = any_mask<W>(hm) & ((1u << nv) - 1u);
+                if (COUNT) w_empty += mask == 0;
+                if (mask != 0) {
+                    const bool rev = (dsg >> (meta & 3u)) & 1u;
+                    const int near_c = rev ? 31 - __builtin_clz(mask) : __builtin_ctz(mask);
+                    const uint32_t pm = mask & ~(1u << near_c);
+                    if (pm != 0) {
+                        const uint32_t refv = lanes_of<W>(rs);
+                        // the slot from the lane's own position in pm, with the
+                        // lane id made here (v_mbcnt) instead of kept live across
+                        // the walk: no register, no spill reload on the push path
+                        const uint32_t lid = mbcnt_lo(~0u);  // lane id (lanes < 32)
+                        const uint32_t below = mbcnt_lo(pm);  // pm's bits below the lane
+                        const uint32_t mine = (pm >> (lid & 31u)) & 1u;
+                        const uint32_t above = (uint32_t)__builtin_popcount(pm) - below - mine;
+                        const int slot = (int)(rev ? below : above);
+                        if (mine & (lid < (uint32_t)W)) wstack[sp + slot] = refv;
+                        sp += __builtin_popcount(pm);
+                    }
+                    uint32_t nr = rs[0];
+#pragma unroll
+                    for (int c = 1; c < W; c++) nr = near_c == c ? rs[c] : nr;
+                    cur = nr;
+                    continue;
+                }
+            } else {
+                const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+                const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+                if (COUNT) {
+                    w_leaves++;
+                    w_tris += cnt;
+                }
+                const uint32_t end = first + cnt;
+                for (uint32_t k0 = first; k0 < end; k0 += kLeafChunk) {
+                    const cfloat_p Rp = (cfloat_p)(tri32 + 12 * (size_t)k0);
+                    float4 TA[kLeafChunk], TB[kLeafChunk], TC[kLeafChunk];
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        TA[t] = load_f4(Rp + 12 * t);
+                        TB[t] = load_f4(Rp + 12 * t + 4);
+                        TC[t] = load_f4(Rp + 12 * t + 8);
+                    }
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) pin_s(TA[t], TB[t], TC[t]);
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        const uint32_t tri = k0 + t;
+                        if (tri >= end) break;
+                        int cls[R];
+                        float tl[R], tu[R];
+                        bool anyc = false;
+#pragma unroll
+                        for (int k = 0; k < R; k++) {
+                            if (COUNT) n_pre += valid[k];
+                            cls[k] = valid[k] ? tri_classify(TA[t], TB[t], TC[t], q[k].ox, q[k].oy, q[k].oz, q[k].dx,
+                                                             q[k].dy, q[k].dz, q[k].co, tcull[k], tl[k], tu[k])
+                                              : 0;
+                            anyc |= cls[k] != 0;
+                        }
+                        if (__ballot(anyc) == 0) continue;
+#pragma unroll
+                        for (int k = 0; k < R; k++) {
+                            if (cls[k] == 0) continue;
+                            if (cls[k] == 2) tcull[k] = fminf(tcull[k], (tu[k] + tsl) * (1.f + 0x1p-20f));
+                            if (nc[k] == K) {  // full: compact against the culling distance
+                                int m = 0;
+                                for (int c = 0; c < K; c++) {
+                                    const uint2 e = entry(c, k);
+                                    if (__uint_as_float(e.y) <= tcull[k]) entry(m++, k) = e;
+                                }
+                                nc[k] = m;
+                            }
+                            if (nc[k] < K) {
+                                entry(nc[k], k) = make_uint2(tri, __float_as_uint(tl[k]));
+                                nc[k]++;
+                            } else {
+                                // keep the K smallest lower bounds; the smallest
+                                // dropped bound certifies the winner
+                                int far_c = 0;
+                                float far_t = __uint_as_float(entry(0, k).y);
+                                for (int c = 1; c < K; c++) {
+                                    const float tt = __uint_as_float(entry(c, k).y);
+                                    if (tt > far_t) { far_t = tt; far_c = c; }
+                                }
+                                if (tl[k] >= far_t) {
+                                    drop[k] = fminf(drop[k], tl[k]);
+                                } else {
+                                    entry(far_c, k) = make_uint2(tri, __float_as_uint(tl[k]));
+                                    drop[k] = fminf(drop[k], far_t);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            if (sp == 0) break;
+            sp--;
+            cur = uni(wstack[sp]);
+        }
+    };
+    switch (oct) {
+        case 0: walk.template operator()<0>(); break;
+        case 1: walk.template operator()<1>(); break;
+        case 2: walk.template operator()<2>(); break;
+        case 3: walk.template operator()<3>(); break;
+        case 4: walk.template operator()<4>(); break;
+        case 5: walk.template operator()<5>(); break;
+        case 6: walk.template operator()<6>(); break;
+        case 7: walk.template operator()<7>(); break;
+        default: walk.template operator()<-1>(); break;
+    }
+    A = launder(A);
+    const RtFrameParams fp = kload(&A->fp);
+    if (COUNT && fp.counters && lane == 0) {
+        atomicAdd(&fp.counters[7], (unsigned long long)w_nodes);
+        atomicAdd(&fp.counters[8], (unsigned long long)w_leaves);
+        atomicAdd(&fp.counters[9], 1ull);
+        atomicAdd(&fp.counters[12], (unsigned long long)w_tris);
+        atomicAdd(&fp.counters[15], (unsigned long long)w_empty);
+    }
+    if (COUNT) {
+#pragma unroll
+        for (int k = 0; k < R; k++) n_nodes += valid[k] ? w_nodes : 0u;
+    }
+    uint32_t hits = 0;
+    const RtLaunchAux aux = kload(&A->aux);
+    const RtDevScene sc = kload(&A->sc);
+    const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f]), fp, f);
+    uint32_t u_tests = 0, u_win = 0;
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        // ray k's list compacted against its final culling distance
+        uint32_t nl = 0;
+        for (int c = 0; c < nc[k]; c++) {
+            const uint2 e = entry(c, k);
+            if (__uint_as_float(e.y) <= tcull[k]) entry(nl++, k) = e;
+        }
+        if (!valid[k]) nl = 0;
+        const bool dropped = valid[k] && drop[k] < __builtin_huge_valf() && drop[k] <= tcull[k];
+        Best out;
+        Shade sh;
+        ResolveCounts rc;
+        uint32_t redo = 0;
+        if (valid[k]) {
+            redo = resolve_list<COUNT>(
+                sc, fp, cam, i0 + k, rt_image_row(fp.row0, fp.row_stride, fp.band, r), nl,
+                nl ? entry(0, k) : make_uint2(0u, 0u), [&](uint32_t c) { return entry(c, k); }, nullptr, dropped,
+                drop[k], out, sh, rc);
+            const uint32_t ob = ob0 + (uint32_t)k;
+            if (redo) {
+                const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
+                if (slot < aux.redo_cap) aux.redo[slot] = ob | (redo == 2u ? kRedoPass1 : 0u);
+            } else {
+                store_sample(fp, ob, out, sh);
+                double c[3];
+                shade_color(cam, out, sh, c);
+                store_rgb(fp, ob, c);
+                if (out.tri >= 0) hits |= 1u << k;
+            }
+        } else {
+            out.tri = -1;
+        }
+        if (COUNT && fp.counters) {
+            u_tests += wave_distinct(nl, [&](uint32_t c) { return entry(c, k).x; });
+            u_win += wave_distinct(valid[k] && out.tri >= 0 ? 1u : 0u, [&](uint32_t) { return (uint32_t)out.tri; });
+            if (valid[k]) {
+                atomicAdd(&fp.counters[0], 1ull);
+                atomicAdd(&fp.counters[2], (unsigned long long)rc.tris);
+                atomicAdd(&fp.counters[3], (unsigned long long)rc.chain);
+                if (!redo && out.tri >= 0) atomicAdd(&fp.counters[4], 1ull);
+                atomicAdd(&fp.counters[5], (unsigned long long)rc.chain_nodes);
+                if (redo == 1) atomicAdd(&fp.counters[10], 1ull);
+                if (redo == 2) atomicAdd(&fp.counters[11], 1ull);
+                if (dropped) atomicAdd(&fp.counters[14], 1ull);
+            }
+        }
+    }
+    if (COUNT && fp.counters) {
+        atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
+        atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
+        if (lane == 0) {
+            atomicAdd(&fp.counters[16], (unsigned long long)u_tests);
+            atomicAdd(&fp.counters[17], (unsigned long long)u_win);
+        }
+    }
+    return hits;
+}
+
+// Persistent waves over (8 R) x 8 tiles, spp = 1 with the fused resolve
+// (k_trace_packet's queues, claims and hit-count partials).
+template <int W, int SP, int K, int R, bool COUNT>
+__global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_packet_r(PacketArgs args) {
+    __shared__ uint32_t stacks[kPacketWaves][SP];
+    __shared__ uint2 cands[kPacketWaves][K * R * 64];
+    __shared__ PacketArgs s_args;
+    {
+        const __attribute__((address_space(4))) uint32_t* src =
+            (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&s_args);
+        for (unsigned w = threadIdx.x; w < sizeof(PacketArgs) / 4; w += blockDim.x) dst[w] = src[w];
+        __syncthreads();
+    }
+    args_p A = (args_p)&s_args;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const uint32_t xq = blockIdx.x % RT_QUEUES;
+    bool first = true;
+    int pend = -1, pend_n = 0;
+    int claim = 1;
+    uint32_t hacc = 0;
+    int hf = -1;
+    const uint32_t hslot = (blockIdx.x * kPacketWaves + (uint32_t)wv) % RT_HIT_SLOTS;
+    for (;;) {
+        A = launder(A);
+        const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
+        const int tiles_x = (W_ + 8 * R - 1) / (8 * R);
+        const int tiles_f = tiles_x * ((nrows + 7) / 8);
+        const int tiles = tiles_f * kword(&A->fp.nframes);
+        claim = tiles >= 64 * (int)(gridDim.x * kPacketWaves) ? 2 : 1;
+        int t = 0;
+        bool claimed = false;
+        if (pend >= 0) {
+            t = pend;
+            pend = (++pend_n < claim) ? pend + RT_QUEUES : -1;
+        } else if (first) {
+            first = false;
+            t = (int)(xq + RT_QUEUES * ((blockIdx.x / RT_QUEUES) * kPacketWaves + wv));
+        } else {
+            claimed = true;
+            if (lane == 0) {
+                const uint32_t nwq = kPacketWaves * ((gridDim.x + RT_QUEUES - 1 - xq) / RT_QUEUES);
+                t = (int)(xq + RT_QUEUES * (nwq + (uint32_t)claim * atomicAdd(kload(&A->aux.tile_ctr) +
+                                                                                  xq * RT_QUEUE_STRIDE, 1u)));
+            }
+        }
+        const int tile = __builtin_amdgcn_readlane(t, 0);
+        if (claimed && claim > 1) {
+            pend = tile + RT_QUEUES;
+            pend_n = 1;
+        }
+        if (tile >= tiles) break;
+        const int fr = tile / tiles_f;
+        const int ft = tile - fr * tiles_f;
+        const int ty = ft / tiles_x, tx = ft - ty * tiles_x;
+        const int i0 = tx * 8 * R + (lane & 7) * R, r = ty * 8 + (lane >> 3);
+        bool valid[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) valid[k] = i0 + k < W_ && r < nrows;
+        const uint32_t hits = trace_packet_r<W, SP, K, R, COUNT>(A, fr, i0, r, valid, stacks[wv], cands[wv]);
+        uint32_t h = 0;
+#pragma unroll
+        for (int k = 0; k < R; k++) h += (uint32_t)__builtin_popcountll(__ballot((hits >> k) & 1u));
+        if (fr != hf) {
+            if (hacc != 0 && lane == 0)
+                atomicAdd(kload(&A->aux.tile_ctr) + RT_HIT_BASE + (hf * RT_HIT_SLOTS + hslot) * RT_QUEUE_STRIDE, hacc);
+            hacc = 0;
+            hf = fr;
+        }
+        hacc += h;
+    }
+    if (hacc != 0 && lane == 0)
         atomicAdd(kload(&launder(A)->aux.tile_ctr) + RT_HIT_BASE + (hf * RT_HIT_SLOTS + hslot) * RT_QUEUE_STRIDE,
                   hacc);
 }

@@ -57,6 +57,27 @@ struct Ray32 {
     float onx, ony, onz, ofx, ofy, ofz;  // near / far plane offsets
 };
 
+// fp32 reciprocal of a direction component without an fp64 division:
+// v_rcp_f32 of the rounded component and one Newton step, within 3 * 2^-24
+// relative of 1/d (the rounded fp64 quotient: 2^-24).  The slab pad covers
+// it with room to spare: a relative reciprocal error e moves a slab plane by
+// at most e (|o|max + |coord|max) in world units, and pad = 2^-19 of that
+// (the fp32 roundings of o, the reciprocal and the fma then
+// use 6 / 32 of the pad instead of 4 / 32).  Zero and tiny components get
+// the same large finite value as the fp64 path (no 0 * inf NaNs).
+#ifndef RT_FAST_INV
+#define RT_FAST_INV 0
+#endif
+constexpr bool kFastInv = RT_FAST_INV != 0;
+[[maybe_unused]] __device__ __forceinline__ float inv32_fast(double v) {
+    const float f = (float)v;
+    float r = __builtin_amdgcn_rcpf(f);
+    r = __builtin_fmaf(r, __builtin_fmaf(-f, r, 1.f), r);
+    if (!(__builtin_fabsf(r) <= 1e18f)) r = v < 0 ? -1e18f : 1e18f;
+    return r;
+}
+
+template <bool FAST = false>
 __device__ __forceinline__ Ray32 make_ray32(const Ray64& ray, float pad) {
     Ray32 q;
     q.ox = (float)ray.ox;
@@ -74,9 +95,15 @@ __device__ __forceinline__ Ray32 make_ray32(const Ray64& ray, float pad) {
         if (!(__builtin_fabsf(f) <= 1e18f)) f = v < 0 ? -1e18f : 1e18f;
         return f;
     };
-    q.ix = inv32(ray.ix);
-    q.iy = inv32(ray.iy);
-    q.iz = inv32(ray.iz);
+    if constexpr (FAST) {
+        q.ix = inv32_fast(ray.dx);
+        q.iy = inv32_fast(ray.dy);
+        q.iz = inv32_fast(ray.dz);
+    } else {
+        q.ix = inv32(ray.ix);
+        q.iy = inv32(ray.iy);
+        q.iz = inv32(ray.iz);
+    }
     // Slab planes widened by `pad` (world units): near planes use
     // o + pad*sgn(inv), far planes o - pad*sgn(inv); pad bounds every fp32
     // rounding of o, inv and the fma (DESIGN.md "exactness").
@@ -544,8 +571,28 @@ __device__ __forceinline__ void wave_add(RT_G unsigned long long* p, uint32_t v)
     if (p && sum != 0 && (int)(threadIdx.x & 63) == __builtin_ctzll(act)) atomicAdd(p, (unsigned long long)sum);
 }
 
+// Adds each active lane's v (< 2^BITS) to base[key] with one atomic per
+// distinct key of the wave: the lanes of a fix-up wave take redo-list entries
+// of different poses of the launch, whose hit counts are separate counters.
+template <int BITS = 6>
+__device__ __forceinline__ void wave_add_keyed(RT_G unsigned long long* base, int key, uint32_t v) {
+    uint64_t todo = __ballot(1);
+    const int lane = (int)(threadIdx.x & 63);
+    while (todo) {
+        const int leader = (int)__builtin_ctzll(todo);
+        const int k = __shfl(key, leader);
+        const bool mine = key == k;
+        uint32_t sum = 0;
+#pragma unroll
+        for (int b = 0; b < BITS; b++) sum += (uint32_t)__builtin_popcountll(__ballot(mine && ((v >> b) & 1u))) << b;
+        if (base && sum != 0 && lane == leader) atomicAdd(base + k, (unsigned long long)sum);
+        todo &= ~__ballot(mine);
+    }
+}
+
 // All spp samples of pixel (i, r) of pose p with the per-lane exact kernel:
-// per-sample outputs, the averaged colour and the pose's hit count.
+// per-sample outputs, the averaged colour and the pose's hit count (the
+// lanes of a wave may hold pixels of different poses).
 template <int W, int S, bool COUNT>
 __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameParams& fp, int p, int i, int r,
                                             LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
@@ -565,7 +612,7 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
         hits += b.tri >= 0;
     }
     store_rgb(fp, po, acc);
-    wave_add(fp.hit_count ? fp.hit_count + p : nullptr, hits);
+    wave_add_keyed(fp.hit_count, p, hits);
 }
 
 #include "packet_kernel.h"
@@ -575,8 +622,12 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
 // Finishes the pixels the packet pipeline handed over (redo list, count in
 // tile_ctr[RT_REDO_COUNT]) with the per-lane exact kernel: from pass 0 after a
 // candidate overflow, straight into the inline-verifying pass 1 when the
-// winner's ancestor chain failed.  Grid-stride; every thread reaches the exit
-// test.  It also leaves the launch's work-queue block zeroed for the next
+// winner's ancestor chain failed.  The list holds redo_cap entries (a fixed
+// pool, not one per pixel); a count past it means entries were not stored, and
+// the launch is retried whole here: every pose pixel of the launch goes through
+// the exact per-lane path (from pass 0, which ends in pass 1 when needed) and
+// the walk kernel's hit-count partials are discarded, since every pixel is
+// counted again.  Grid-stride; every thread reaches the exit test.  It also leaves the launch's work-queue block zeroed for the next
 // launch: block 0 folds the per-frame hit-count partials into the caller's
 // counters and clears them, the tile queues and the pool counter (nothing
 // else reads them now); the last block to have read the redo count clears it.
@@ -597,6 +648,7 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
     if (blockIdx.x == 0) {
         if (tid < RT_MAX_BATCH) frame_sum[tid] = 0;
         __syncthreads();
+        const bool retry = n_sh > aux.redo_cap;  // (n_sh is set: tid 0 wrote it before the barrier)
         const int poses = fp.nframes / fp.spp;
         for (int k = tid; k < poses * RT_HIT_SLOTS; k += 256) {
             RT_G uint32_t* const slot = aux.tile_ctr + RT_HIT_BASE + k * RT_QUEUE_STRIDE;
@@ -609,17 +661,19 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
         if (tid < RT_QUEUES) aux.tile_ctr[tid * RT_QUEUE_STRIDE] = 0;
         if (tid == 0) aux.tile_ctr[RT_POOL_COUNT] = 0;
         __syncthreads();
-        if (fp.hit_count && tid < poses && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
+        if (!retry && fp.hit_count && tid < poses && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
     }
     __syncthreads();
-    const uint32_t n = n_sh;
+    const uint32_t npix = (uint32_t)fp.W * (uint32_t)fp.nrows;
+    const bool retry = n_sh > aux.redo_cap;
+    // the redo list, or (retry) every pose pixel of the launch
+    const uint32_t n = retry ? npix * (uint32_t)(fp.nframes / fp.spp) : n_sh;
     if (n == 0) return;
     LaneStack<S> st;
     st.attach(lds, aux, tid);
-    const uint32_t npix = (uint32_t)fp.W * (uint32_t)fp.nrows;
     // (grid-stride over the redo list; every thread reaches the exit test)
     for (uint32_t e = blockIdx.x * 256u + (uint32_t)tid; e < n; e += gridDim.x * 256u) {
-        const uint32_t v = aux.redo[e];
+        const uint32_t v = retry ? e : aux.redo[e];
         const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: pose * npix + pixel
         const int p = (int)(ob / npix);
         const uint32_t o = ob - (uint32_t)p * npix;
@@ -746,6 +800,26 @@ constexpr int kCandidates = RT_CAND_LDS;  // packet kernel: LDS candidate list e
 static_assert(RT_PW_K <= RT_CAND_LDS, "wavefront walk lists share the candidate buffers");
 constexpr int kFixupGrid = 256;    // k_fixup blocks (the redo list is short)
 
+// Rays per lane of the spp = 1 packet kernel: 1 (8x8 tiles, k_trace_packet)
+// or 2 (16x8 tiles, k_trace_packet_r).  RT_PACKET_RAYS, read per call.
+int packet_rays() {
+    const char* e = getenv("RT_PACKET_RAYS");
+    return e && e[0] == '2' ? 2 : 1;
+}
+template <int W>
+int packet_blocks_per_cu_w();
+// Resident workgroups per CU of k_trace_packet_r (its own register count).
+int packet_r_blocks_per_cu() {
+    static const int n = [] {
+        int m = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &m, k_trace_packet_r<8, kPacketStack, kCandidates / 2, 2, false>, 64 * kPacketWaves, 0) != hipSuccess)
+            m = 1;
+        return m < 1 ? 1 : m;
+    }();
+    return n;
+}
+
 // Kernel choice: the packet kernel unless its stack cannot hold the tree's
 // bound or RT_KERNEL=lane asks for the per-lane kernel.
 bool use_packet(uint32_t stack_bound) {
@@ -812,6 +886,19 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
                     else
                         hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true, true>), pgrid,
                                            pblk, 0, s, PacketArgs{sc, fp, aux});
+                }
+            }
+            if constexpr (W == 8) {
+                // spp = 1: R rays per lane (RT_PACKET_RAYS, read per call)
+                if (!packed && fp.spp == 1 && packet_rays() == 2) {
+                    packed = true;  // (launched here)
+                    const dim3 g2((unsigned)(aux.pgrid / packet_blocks_per_cu_w<8>() * packet_r_blocks_per_cu()));
+                    if (count)
+                        hipLaunchKernelGGL((k_trace_packet_r<8, kPacketStack, kCandidates / 2, 2, true>), g2, pblk, 0,
+                                           s, PacketArgs{sc, fp, aux});
+                    else
+                        hipLaunchKernelGGL((k_trace_packet_r<8, kPacketStack, kCandidates / 2, 2, false>), g2, pblk,
+                                           0, s, PacketArgs{sc, fp, aux});
                 }
             }
             if (packed) {
@@ -949,11 +1036,10 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     }
     if (aux.spill_cap + kLdsStack < sc.stack_bound || !aux.tile_ctr || !aux.spill || aux.grid <= 0)
         return hipErrorInvalidValue;
-    // the redo list must hold every pixel of the shard; the split resolve
-    // needs candidate lists for every pixel of the batch
+    // the redo list is a fixed pool (k_fixup retries the launch whole past
+    // it); the split resolve needs candidate lists for every pixel of the batch
     const uint64_t bpix = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.nframes;  // pixels of the batch
-    if (use_packet(sc.stack_bound) &&
-        (!aux.redo || aux.redo_cap < bpix / (uint64_t)fp.spp || !aux.pool || aux.pgrid <= 0))
+    if (use_packet(sc.stack_bound) && (!aux.redo || aux.redo_cap < 1 || !aux.pool || aux.pgrid <= 0))
         return hipErrorInvalidValue;
     if (use_packet(sc.stack_bound) && needs_cand(fp.spp, fp.pack && sc.width == 8) &&
         (!aux.cand || !aux.cand_cnt || !aux.cand_drop || !aux.cand_ovf || aux.cand_cap < bpix))

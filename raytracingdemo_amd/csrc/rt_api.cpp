@@ -14,6 +14,7 @@
 #include <memory>
 #include <exception>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <string>
 #include <array>
@@ -74,7 +75,7 @@ size_t align_up(size_t x) {
 }
 
 // d_counters: RT_FLAG_COUNT counters (rt_frame_stats)
-constexpr size_t kCounterWords = 16;
+constexpr size_t kCounterWords = 24;  // 18-23: RT_PROFILE builds (packet_kernel.h)
 // Candidate overflow pool: chunks of RT_POOL_CHUNK entries, one per lane whose
 // LDS list overflows in a launch (a dry pool falls back to the certified
 // dropped bound, so the size trades memory against fix-up work only).
@@ -299,6 +300,7 @@ void upload_one(rt_scene* s, int device) {
     d.ref2walk = reinterpret_cast<const uint32_t*>(at(12));
     d.qnodes = qn.empty() ? nullptr : at(13);
     d.root_ref = f.root_ref;
+    d.root_meta = f.root_meta;
     std::memcpy(d.root_box, f.root_box, sizeof d.root_box);
     d.n_tris = (uint32_t)s->soup.n;
     d.node_bytes = rt_node_bytes(f.width);
@@ -342,8 +344,21 @@ void quiesce(Replica& r) {
     HIP_TRY(hipEventSynchronize(r.ev_out));
 }
 
-// Redo list for `pixels` pose pixels of a launch (grown, never shrunk).
+// Redo list: a fixed pool of entries, not one per pose pixel (on the sponza
+// proxy ~0 pixels are redone; a launch whose redo count passes the pool is
+// retried whole by k_fixup).  RT_REDO_CAP (read per call; a test hook) lowers
+// the entries a launch may use.
+constexpr uint64_t kRedoEntries = 1u << 20;  // 4 MiB
+uint64_t redo_limit() {
+    const char* e = std::getenv("RT_REDO_CAP");
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? std::min<uint64_t>((uint64_t)v, kRedoEntries) : kRedoEntries;
+}
+
+// Redo list for a launch of `pixels` pose pixels (grown, never shrunk; at
+// most kRedoEntries).
 void ensure_redo(Replica& r, uint64_t pixels) {
+    pixels = std::min<uint64_t>(std::max<uint64_t>(pixels, 1), kRedoEntries);
     if (r.redo_cap >= pixels) return;
     quiesce(r);
     if (r.d_redo) HIP_TRY(hipFree(r.d_redo));
@@ -501,7 +516,7 @@ RtLaunchAux aux_of(Replica& r) {
     a.grid = r.grid;
     a.pgrid = r.pgrid;
     a.redo = r.d_redo;
-    a.redo_cap = r.redo_cap;
+    a.redo_cap = std::min<uint64_t>(r.redo_cap, redo_limit());
     a.pool = r.d_pool;
     a.pool_chunks = r.pool_chunks;
     a.cand = static_cast<uint64_t*>(r.d_cand);
@@ -577,7 +592,11 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
         fp.hit_pos = out->pos ? out->pos + 3 * soff : nullptr;
         fp.rgb = out->rgb ? out->rgb + 3 * off : nullptr;
         fp.hit_count = out->hit_count ? out->hit_count + f0 : nullptr;
+#if defined(RT_PROFILE) && RT_PROFILE
+        fp.counters = r->d_counters;  // (a phase-profiling build: the timed kernel writes counters 18-23)
+#else
         fp.counters = (flags & RT_FLAG_COUNT) ? r->d_counters : nullptr;
+#endif
         const hipEvent_t* tev = nullptr;
         if (flags & RT_FLAG_TIMING) {
             if (r->tev_used == r->tev.size()) {
@@ -591,14 +610,47 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
     }
 }
 
+// RT_GROUP_RCCL=1 (test hook, read per call): a one-device scene takes the
+// multi-device path with its real transport — a one-rank RCCL communicator
+// over that device, ncclGroupStart / ncclGather / ncclGroupEnd into the root
+// buffer, then the de-interleave — so the RCCL branch runs on a one-GPU box.
+bool rccl_self(const rt_scene* s) {
+    if (s->reps.size() != 1) return false;
+    const char* e = std::getenv("RT_GROUP_RCCL");
+    return e && e[0] == '1';
+}
+
 // Shards of a multi-device frame: RT_VIRTUAL_SHARDS=N (test hook, read per
 // call) splits a one-device scene into N shards on that device, gathered by
 // device copies instead of RCCL.
 int group_shards(const rt_scene* s) {
     if (s->reps.size() > 1) return (int)s->reps.size();
+    if (rccl_self(s)) return 1;
     const char* e = std::getenv("RT_VIRTUAL_SHARDS");
     const int v = e ? std::atoi(e) : 1;
     return v >= 1 && v <= 64 ? v : 1;
+}
+
+// The multi-device path (render_group) is taken for more than one shard, or
+// for the one-rank RCCL hook.
+bool use_group(const rt_scene* s) { return group_shards(s) > 1 || rccl_self(s); }
+
+// The RCCL communicator over the uploaded devices (rank g = the g-th
+// replica), created on the first group render that needs it: uploading to
+// several devices does not need RCCL, and per-device entry points never
+// touch it.  Built into a local vector and kept only on success, so a failed
+// init leaves no null handles behind and the next call retries.
+void ensure_comms(rt_scene* s) {
+    Group& gp = s->grp;
+    if (gp.comms.size() == s->reps.size()) return;
+    for (auto& r : s->reps) quiesce(*r);
+    for (ncclComm_t c : gp.comms) rccl().destroy(c);
+    gp.comms.clear();
+    std::vector<int> devs;
+    for (auto& r : s->reps) devs.push_back(r->device);
+    std::vector<ncclComm_t> comms(devs.size(), nullptr);
+    NCCL_TRY(rccl().init_all(comms.data(), (int)devs.size(), devs.data()));
+    gp.comms = std::move(comms);
 }
 
 // Block layout of one shard (256-B aligned sections): per-sample hit ids,
@@ -634,9 +686,10 @@ void render_group(rt_scene* s, const rt_camera* cams, int nframes, int spp, int 
     Group& gp = s->grp;
     const int G = group_shards(s);
     const int W = cams[0].width, H = cams[0].height, R = rt_shard_pad(H, G);
-    const bool virt = s->reps.size() == 1;
+    const bool virt = s->reps.size() == 1 && !rccl_self(s);
     Replica& r0 = *s->reps.front();
     const ShardLayout L = shard_layout(out, nframes, R, W, spp);
+    if (!virt) ensure_comms(s);
     // buffers (grown, never shrunk; earlier groups finished first)
     if (gp.block < L.bytes || (int)gp.stage.size() != G) {
         for (auto& r : s->reps) quiesce(*r);
@@ -745,6 +798,8 @@ int rt_load_obj(const char* path, double scale, double** tris, uint64_t* n_tris)
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -763,6 +818,8 @@ int rt_load_obj_cached(const char* path, double scale, const char* cache_dir, do
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -815,22 +872,30 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
                 // reference tree builds on host threads while this thread
                 // drives the device build of the walk tree (mostly waiting)
                 std::exception_ptr tree_err;
-                std::thread ref([&] {
+                auto ref_tree = [&] {
                     try {
                         s->tree = rt::build_tree(s->soup, algo, k, collapse);
                     } catch (...) { tree_err = std::current_exception(); }
                     t2 = clk::now();
-                });
+                };
+                // spawn-or-run-inline: a host that cannot start a thread
+                // builds the reference tree on this one first
+                std::thread ref;
+                try {
+                    ref = std::thread(ref_tree);
+                } catch (const std::system_error&) {
+                    ref_tree();
+                }
                 try {
                     wt = rt::build_walk_tree_device(s->soup, walk_device, rt::walk_max_leaf(), rt::walk_node_cost());
                     rt::plan_wide_collapse(wt, 8);
                 } catch (...) {
-                    ref.join();
+                    if (ref.joinable()) ref.join();
                     throw;
                 }
                 s->times.walk_device = walk_device;
                 t3 = clk::now();
-                ref.join();
+                if (ref.joinable()) ref.join();
                 if (tree_err) std::rethrow_exception(tree_err);
             } else {
                 // host walk build: one after the other (both want the host's
@@ -856,6 +921,8 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
         return fail(e.status, e.msg);
     } catch (const std::bad_alloc&) {
         return fail(RT_ERR_RUNTIME, "out of memory");
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -887,18 +954,13 @@ int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {
             for (auto& r : s->reps) have |= r->device == devices[q];
             if (!have) upload_one(s, devices[q]);
         }
-        // more than one device: a fresh communicator over all of them (rank g =
-        // the g-th uploaded device, the shard order of rt_render_batch_multi)
-        if (s->reps.size() > 1 && s->grp.comms.size() != s->reps.size()) {
-            free_group(s);
-            std::vector<int> devs;
-            for (auto& r : s->reps) devs.push_back(r->device);
-            s->grp.comms.resize(devs.size());
-            NCCL_TRY(rccl().init_all(s->grp.comms.data(), (int)devs.size(), devs.data()));
-        }
+        // (the RCCL communicator over several devices is created by the first
+        // multi-device render, ensure_comms)
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -929,6 +991,8 @@ int rt_render_batch_spp_device(rt_scene* s, int device, const rt_camera* cams, i
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -951,13 +1015,15 @@ int rt_render_batch_multi(rt_scene* s, const rt_camera* cams, int nframes, int s
         if (s->reps.empty()) return fail(RT_ERR_NO_DEVICE, "scene not uploaded");
         Replica& r0 = *s->reps.front();
         DevGuard g(r0.device);
-        if (group_shards(s) == 1)
+        if (!use_group(s))
             render_batch_locked(s, r0, cams, nframes, spp, mode, 0, 1, cams[0].height, out, (hipStream_t)stream, flags);
         else
             render_group(s, cams, nframes, spp, mode, out, (hipStream_t)stream, flags);
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -986,6 +1052,8 @@ int rt_render_shard_device(rt_scene* s, int device, const rt_camera* cams, int n
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -1054,6 +1122,8 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -1098,7 +1168,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         fp.rgb = d.rgb;
         fp.hit_count = d.hit_count;
         hipEvent_t e0 = r.ev0, e1 = r.ev1;
-        if (group_shards(s) > 1) {
+        if (use_group(s)) {
             // every uploaded device renders its interleaved rows; the frame
             // is gathered and de-interleaved on the first device (the device
             // time is the group's, first device's stream: renders to gather)
@@ -1127,6 +1197,8 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -1155,6 +1227,8 @@ int rt_diag_raw(rt_scene* s, int device, uint64_t* out, size_t n) {
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -1184,6 +1258,8 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->spilled_rays = c[13];
         out->dropped_rays = c[14];
         out->empty_node_steps = c[15];
+        out->wave_tri_tests = c[16];
+        out->wave_winners = c[17];
         out->timed_launches = r.tev_used;
         out->trace_ms = 0.0;
         for (size_t k = 0; k < r.tev_used; k++) {
@@ -1196,6 +1272,8 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_RUNTIME, e.what());
     }
 }
 
@@ -1233,6 +1311,7 @@ int rt_scene_stats(const rt_scene* s, rt_scene_stats_t* o) {
     vec(f.wide); vec(f.tri32); vec(f.tri64); vec(f.tri_id); vec(f.tri_rank); vec(f.tri_leaf); vec(f.rbox);
     vec(f.rparent); vec(f.rkid_off); vec(f.rkid); vec(f.rrange); vec(f.ref2walk);
     mix(&f.root_ref, sizeof f.root_ref);
+    mix(&f.root_meta, sizeof f.root_meta);
     mix(f.root_box, sizeof f.root_box);
     mix(&f.stack_bound, sizeof f.stack_bound);
     o->layout_digest = h;

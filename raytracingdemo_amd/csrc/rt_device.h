@@ -2,7 +2,8 @@
 //
 // HBM layout of one scene replica (see DESIGN.md §Data layout):
 //   wide nodes   W child records of 32 B: fp32 lo.x hi.x lo.y hi.y lo.z hi.z,
-//                u32 ref, pad — one s_load_dwordx8 per child in the packet
+//                u32 ref, u32 meta of the child node (its children's sort
+//                axis | valid slots << 2; 0 for leaves) — one s_load_dwordx8 per child in the packet
 //                kernel, two dwordx4 in the per-lane kernel; node_bytes(W) =
 //                32*W (W=8: 256 B, four 64-B lines).  Bounds are the
 //                reference's fp64 boxes rounded outward to fp32 (a
@@ -152,7 +153,8 @@ struct RtDevScene {
     uint32_t stack_bound;
     double coord_max;             // max |coordinate| of the scene (slab margins of arbitrary rays)
     uint32_t n_wide;              // wide nodes
-    uint32_t reserved;
+    uint32_t root_meta;           // the root's sort axis | valid slots << 2 (each child record's pad
+                                  // word holds its child node's; bvh_build.cpp flatten)
 };
 
 // Per-launch resources of the persistent exact kernel.
@@ -162,7 +164,7 @@ struct RtLaunchAux {
     uint32_t spill_cap;
     int32_t grid;         // persistent blocks (CUs x resident blocks per CU)
     RT_G uint32_t* redo;       // packet kernel -> k_fixup: pixel index | start-pass bit
-    uint64_t redo_cap;    // entries (>= pixels of the launch)
+    uint64_t redo_cap;    // entries (a fixed pool: past it k_fixup retries the whole launch)
     RT_G uint64_t* pool;       // candidate overflow pool: pool_chunks x RT_POOL_CHUNK entries
     uint32_t pool_chunks;
     int32_t pgrid;             // workgroups of the packet kernel (64 * kPacketWaves threads each)

@@ -96,6 +96,7 @@ std::vector<uint8_t> quantize_wide8(const uint8_t* wide, uint64_t n_nodes);
 struct Flat {
     int width = 8;                        // W
     uint32_t root_ref = 0;
+    uint32_t root_meta = 0;               // the root's sort axis | valid slots << 2 (child records carry their node's)
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     double pad = 0, coord_max = 0;        // max |coordinate| (sizes the per-frame margin)
     std::vector<uint8_t> wide;            // wide nodes, node_bytes(W) each

@@ -249,11 +249,24 @@ struct Split {
     uint32_t leaf;    // 1: the task becomes a leaf
 };
 
+// Per task of a level: 1 if it becomes an inner node, its children of more
+// than kSmall triangles (next level's tasks) and of at most kSmall (k_small's
+// subtrees); an exclusive scan over the tasks numbers them.  Three full u32
+// fields: a level of up to n / (kSmall + 1) tasks cannot overflow them.
+struct Cnt3 {
+    uint32_t inner, big, small;
+};
+struct Cnt3Sum {
+    __host__ __device__ Cnt3 operator()(const Cnt3& a, const Cnt3& b) const {
+        return Cnt3{a.inner + b.inner, a.big + b.big, a.small + b.small};
+    }
+};
+
 // walk_tree.cpp:117-167 for one task (all big tasks have > kSmall >= LMAX
 // triangles, so the leaf rule never applies here, but it is kept for symmetry)
 __global__ void k_split(uint32_t T, const uint32_t* task_node, const uint32_t* task_b, const uint32_t* task_e,
                         const uint64_t* box, const uint64_t* cbox, const uint32_t* bin_cnt, const uint64_t* bin_box,
-                        int lmax, double node_cost, DNode* nodes, Split* split, unsigned long long* pack) {
+                        int lmax, double node_cost, DNode* nodes, Split* split, Cnt3* pack) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     double mn[3], mx[3];
@@ -319,7 +332,7 @@ __global__ void k_split(uint32_t T, const uint32_t* task_node, const uint32_t* t
         nd.first = task_b[t];
         nd.count = cnt;
         split[t] = s;
-        pack[t] = 0;
+        pack[t] = Cnt3{0u, 0u, 0u};
         return;
     }
     if (best_axis >= 0) {
@@ -330,8 +343,8 @@ __global__ void k_split(uint32_t T, const uint32_t* task_node, const uint32_t* t
     if (s.axis < 0) s.nleft = cnt / 2;
     split[t] = s;
     const uint32_t nl = s.nleft, nr = cnt - s.nleft;
-    const uint64_t big = (nl > kSmall) + (nr > kSmall), small = 2 - big;
-    pack[t] = 1ull | (big << 21) | (small << 42);  // inner | big children | small children
+    const uint32_t big = (nl > kSmall) + (nr > kSmall), small = 2 - big;
+    pack[t] = Cnt3{1u, big, small};  // inner, big children, small children
 }
 
 struct Small {
@@ -339,7 +352,7 @@ struct Small {
 };
 
 __global__ void k_children(uint32_t T, const uint32_t* task_node, const uint32_t* task_b, const uint32_t* task_e,
-                           const Split* split, const unsigned long long* off, uint32_t node_base, uint32_t small_base,
+                           const Split* split, const Cnt3* off, uint32_t node_base, uint32_t small_base,
                            DNode* nodes, uint32_t* nx_node, uint32_t* nx_b, uint32_t* nx_e, Small* small,
                            int32_t* child_task) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -347,9 +360,8 @@ __global__ void k_children(uint32_t T, const uint32_t* task_node, const uint32_t
     const Split s = split[t];
     child_task[2 * t] = child_task[2 * t + 1] = -1;
     if (s.leaf) return;
-    const uint64_t o = off[t];
-    const uint32_t q = (uint32_t)(o & 0x1FFFFF), qb = (uint32_t)((o >> 21) & 0x1FFFFF),
-                   qs = (uint32_t)((o >> 42) & 0x1FFFFF);
+    const Cnt3 o = off[t];
+    const uint32_t q = o.inner, qb = o.big, qs = o.small;
     const uint32_t b = task_b[t], e = task_e[t];
     const uint32_t cb[2] = {b, b + s.nleft}, ce[2] = {b + s.nleft, e};
     DNode& nd = nodes[task_node[t]];
@@ -610,8 +622,8 @@ WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node
     uint32_t* bin_cnt = P.get<uint32_t>((size_t)tcap * 3 * kBins);
     uint64_t* bin_box = P.get<uint64_t>((size_t)tcap * 3 * kBins * 6);
     Split* split = P.get<Split>(tcap);
-    unsigned long long* pack = P.get<unsigned long long>(tcap + 1);
-    unsigned long long* off = P.get<unsigned long long>(tcap + 1);
+    Cnt3* pack = P.get<Cnt3>(tcap + 1);
+    Cnt3* off = P.get<Cnt3>(tcap + 1);
     int32_t* child_task = P.get<int32_t>(2 * (size_t)tcap);
     Small* small = P.get<Small>(n);
     DNode* nodes = P.get<DNode>(2 * (size_t)n);
@@ -619,7 +631,7 @@ WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node
     // hipcub scan workspaces (the larger of the two scans)
     size_t ws_a = 0, ws_b = 0;
     HT(hipcub::DeviceScan::ExclusiveSum(nullptr, ws_a, flag, scan, n + 1, st));
-    HT(hipcub::DeviceScan::ExclusiveSum(nullptr, ws_b, pack, off, tcap + 1, st));
+    HT(hipcub::DeviceScan::ExclusiveScan(nullptr, ws_b, pack, off, Cnt3Sum{}, Cnt3{0u, 0u, 0u}, tcap + 1, st));
     void* ws = P.get<uint8_t>(std::max(ws_a, ws_b));
     const size_t ws_bytes = std::max(ws_a, ws_b);
 
@@ -646,10 +658,10 @@ WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node
         hipLaunchKernelGGL(k_bin, dim3(egrid), blk, 0, st, tr, n, idx, seg, cbox, bin_cnt, bin_box);
         hipLaunchKernelGGL(k_split, dim3(tg), blk, 0, st, T, tnode[cur], tb[cur], te[cur], box, cbox, bin_cnt,
                            bin_box, lmax, node_cost, nodes, split, pack);
-        HT(hipMemsetAsync(pack + T, 0, sizeof(unsigned long long), st));
+        HT(hipMemsetAsync(pack + T, 0, sizeof(Cnt3), st));
         size_t wsb = ws_bytes;
-        HT(hipcub::DeviceScan::ExclusiveSum(ws, wsb, pack, off, T + 1, st));
-        unsigned long long tot = 0;
+        HT(hipcub::DeviceScan::ExclusiveScan(ws, wsb, pack, off, Cnt3Sum{}, Cnt3{0u, 0u, 0u}, T + 1, st));
+        Cnt3 tot{0u, 0u, 0u};
         HT(hipMemcpyAsync(&tot, off + T, sizeof tot, hipMemcpyDeviceToHost, st));
         hipLaunchKernelGGL(k_children, dim3(tg), blk, 0, st, T, tnode[cur], tb[cur], te[cur], split, off, node_base,
                            nsmall, nodes, tnode[cur ^ 1], tb[cur ^ 1], te[cur ^ 1], small, child_task);
@@ -663,8 +675,7 @@ WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node
         HT(hipStreamSynchronize(st));  // tot: this level's inner / big / small children
         std::swap(idx, idx2);
         std::swap(seg, seg2);
-        const uint32_t inner = (uint32_t)(tot & 0x1FFFFF), big = (uint32_t)((tot >> 21) & 0x1FFFFF),
-                       sm = (uint32_t)((tot >> 42) & 0x1FFFFF);
+        const uint32_t inner = tot.inner, big = tot.big, sm = tot.small;
         node_base += 2 * inner;
         nsmall += sm;
         T = big;

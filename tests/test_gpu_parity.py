@@ -621,6 +621,51 @@ def test_sharded_frames_through_the_abi_equal_one_device(monkeypatch, shards):
     assert torch.equal(g4c, c4)
 
 
+@pytest.mark.parametrize("spp", [1, 4])
+def test_rccl_group_branch_equals_one_device(monkeypatch, spp):
+    """The RCCL branch of render_group (rt_api.cpp): RT_GROUP_RCCL=1 sends a
+    one-device scene through the multi-device path with its real transport — a
+    one-rank communicator from ncclCommInitAll over {0}, created lazily on the
+    first group render; ncclGroupStart / ncclGather / ncclGroupEnd of the
+    staging block into the root buffer; k_deinterleave / k_sum_counts — through
+    rt_render_batch_multi and rt_render_frame.  Outputs equal the one-device
+    render bit for bit (the multi-GPU drop-in path, INTEGRATION.md §2,
+    replacing src/main.cpp:253-255)."""
+    torch = pytest.importorskip("torch")
+    tris = golden_scene("stanford-bunny.obj")
+    s = scene("stanford-bunny.obj", "bsah", 8)
+    path = rt.CameraPath(rt.scene_center(tris), 36)
+    cams = [path.circular_path(f) for f in (1, 8, 27)]
+    W, H, F = 211, 97, 3
+    st = torch.cuda.current_stream().cuda_stream
+    want = (("id", torch.int32, spp), ("dist", torch.float64, spp), ("pos", torch.float64, 3 * spp),
+            ("rgb", torch.uint8, 3))
+    ref = {k: torch.empty(F * H * W * per, dtype=dt, device="cuda:0") for k, dt, per in want}
+    ref_cnt = torch.zeros(F, dtype=torch.int64, device="cuda:0")
+    s.render_batch_device(0, cams, W, H, 0, 1, H, hit_id=ref["id"].data_ptr(), dist=ref["dist"].data_ptr(),
+                          hit_pos=ref["pos"].data_ptr(), rgb=ref["rgb"].data_ptr(), hit_count=ref_cnt.data_ptr(),
+                          stream=st, spp=spp)
+    monkeypatch.setenv("RT_GROUP_RCCL", "1")
+    for it in range(2):  # the second call reuses the communicator and the staging blocks
+        got = {k: torch.full_like(v, 7) for k, v in ref.items()}
+        cnt = torch.zeros(F, dtype=torch.int64, device="cuda:0")
+        s.render_batch_multi(cams, W, H, hit_id=got["id"].data_ptr(), dist=got["dist"].data_ptr(),
+                             hit_pos=got["pos"].data_ptr(), rgb=got["rgb"].data_ptr(), hit_count=cnt.data_ptr(),
+                             stream=st, spp=spp)
+        torch.cuda.synchronize()
+        for k in ref:
+            assert torch.equal(got[k], ref[k]), (spp, it, k)
+        assert torch.equal(cnt, ref_cnt), (spp, it)
+    if spp == 1:
+        # the blocking host-buffer frame call (rt_render_frame) over the group
+        p, d = cams[1]
+        g = s.calculate_screen(p, d, W, H, want=("hit_id", "dist", "rgb"))
+        assert np.array_equal(g["hit_id"], ref["id"].cpu().numpy().view(np.uint32).reshape(F, -1)[1])
+        assert np.array_equal(g["dist"], ref["dist"].cpu().numpy().reshape(F, -1)[1])
+        assert np.array_equal(g["rgb"].reshape(-1), ref["rgb"].cpu().numpy().reshape(F, -1)[1])
+        assert g["hits"] == int(ref_cnt[1])
+
+
 def test_band_shards_reassemble_to_full_frame():
     """rt_render_shard_device (bands of 8 rows interleaved over the shards, the
     multi-GPU partition bench.py uses) reassembles through shards.py into the

@@ -30,6 +30,18 @@ for s in $STEPS; do
         split) RT_RESOLVE=split run bench_split 300 python bench.py --no-cpu --steps 10 ;;
         shard8) run bench_shard8 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of 8 ;;
         shards) for n in 2 4 8; do run bench_shard$n 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of $n || exit 1; done ;;
+        rccl)  run rccl 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rccl -o rccl \
+                   -- python tools/rccl_group_probe.py ;;
+        c5)    run c5 900 python -u -m pytest tests/test_gpu_headline.py -x -v --timeout 600 --timeout-method thread \
+                   -p no:cacheprovider -k "c5 or c3_shape" ;;
+        rcclt) run rcclt 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
+                   -p no:cacheprovider -k "rccl_group" ;;
+        fetchcal) run fetchcal 300 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/fcal \
+                   -o fcal -- ./tools/fetch_probe && \
+               run fetchcalw 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/fcal \
+                   -o wcal -- ./tools/fetch_probe && \
+               python tools/fetch_calib.py gpurun_out/fcal/fcal_counter_collection.csv gpurun_out/fetch_calib.json \
+                   gpurun_out/fcal/wcal_counter_collection.csv ;;
         rehearse) RT_BENCH_REHEARSE=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                       --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu ;;
         spp4)  run bench_spp4 300 python bench.py --no-cpu --steps 5 --spp 4 ;;
@@ -40,8 +52,11 @@ for s in $STEPS; do
                    -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin --key-out gpurun_out/pmc_key.txt && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
                    -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin && \
+               RT_RESOLVE=split run pmcs 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv \
+                   -d gpurun_out/pmc -o walkonly -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin && \
                python tools/pmc_traffic.py gpurun_out/pmc/fetch_counter_collection.csv \
-                   gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json ;;
+                   gpurun_out/pmc/write_counter_collection.csv gpurun_out/pmc_key.txt gpurun_out/pmc_traffic.json \
+                   k_trace_packet gpurun_out/pmc/walkonly_counter_collection.csv ;;
         pmcpaths) run pmcp 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmcp -o fetch \
                    -- python bench.py --paths --steps 1 --warmup 0 --no-cpu --key-out gpurun_out/pmcp_key.txt && \
                run pmcpw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcp -o write \

@@ -6,11 +6,19 @@ and the WRITE_SIZE pass written by `tools/gpu_session.sh pmc`, averages the
 non-counting traversal-kernel dispatches and writes the JSON that bench.py
 reads for `roofline.traffic`.
 
-Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports
-half of the bytes of wide coalesced reads (128-B requests tallied at 64 B), so
-read bytes = 2 x FETCH_SIZE; WRITE_SIZE is taken as is.
+Correction: on gfx950 FETCH_SIZE reports half of the bytes of wide
+coalesced reads (MI355X_MICROARCH.md, HBM section: 128-B requests tallied at
+64 B).  tools/fetch_probe calibrates the other read types
+(profiles/r03_fetch_calib.json): vector gathers (8 B per lane; the first 72 B
+of 128-B records per lane) read 2 x FETCH_SIZE like the wide reads, but
+uniform (scalar) loads are exact — 64-B requests, FETCH_SIZE x 1.  The packet
+kernel reads its walk records (nodes, fp32 triangles) with scalar loads and
+its fp64 resolve records with vector gathers, so with WALK_CSV (the same
+launch with RT_RESOLVE=split, whose walk kernel reads by scalar loads only):
+read bytes = F_walk + 2 (F_fused - F_walk); without it, 2 x FETCH_SIZE (an
+upper bound for a kernel with scalar reads).  WRITE_SIZE is taken as is.
 
-Usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV KEY_FILE OUT_JSON [KERNEL]
+Usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV KEY_FILE OUT_JSON [KERNEL [WALK_CSV]]
 (KERNEL: k_trace_packet, the default, or k_paths for config c5)
 """
 import collections
@@ -55,7 +63,16 @@ def main():
     if rdreq > 0:
         ratio = fetch / (rdreq * 64.0)
         unit = 1.0 if abs(ratio - 1.0) < 0.25 else 1024.0
-    read_b = 2.0 * fetch * unit
+    walk = None
+    if len(sys.argv) > 6:
+        wk = per_dispatch(sys.argv[6], kern)
+        if wk:
+            walk = sum(d["FETCH_SIZE"] for d in wk.values()) / len(wk)
+    if walk is not None:
+        # scalar walk reads at FETCH_SIZE x 1, the rest (vector) at x 2
+        read_b = (walk + 2.0 * max(0.0, fetch - walk)) * unit
+    else:
+        read_b = 2.0 * fetch * unit
     write_b = write * unit
     res = {
         "workload_key": key,
@@ -66,8 +83,13 @@ def main():
         "read_bytes_per_launch": read_b,
         "write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
-        "method": "rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum / --pmc WRITE_SIZE, separate passes; "
-                  "read = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE",
+        **({"walk_only_fetch_size_avg": walk, "read_bytes_upper_bound": 2.0 * fetch * unit,
+            "read_bytes_lower_bound": fetch * unit} if walk is not None else {}),
+        "method": ("rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum / --pmc WRITE_SIZE, separate passes; " +
+                   ("read = walk-only FETCH_SIZE x 1 (scalar loads, calibrated exact) + the fused kernel's "
+                    "remaining FETCH_SIZE x 2 (vector gathers, calibrated x 2; profiles/r03_fetch_calib.json)"
+                    if walk is not None else "read = 2 x FETCH_SIZE (gfx950 correction)") +
+                   ", write = WRITE_SIZE"),
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -125,6 +125,20 @@ __device__ __forceinline__ uint64_t prof_clock() {
     return 0;
 }
 
+// Keep the tile set-up's fp64 ray direction (6 VGPRs) through the walk for
+// the resolve instead of generating it again there (a square root and a
+// division per ray).
+#ifndef RT_KEEP_DIR
+#define RT_KEEP_DIR 1
+#endif
+constexpr bool kKeepDir = RT_KEEP_DIR != 0;
+
+// Load entry 0's shading fields with its Moller-Trumbore part (resolve_list).
+#ifndef RT_SPEC_WIN
+#define RT_SPEC_WIN 0
+#endif
+constexpr bool kSpecWin = RT_SPEC_WIN != 0;
+
 #ifndef RT_PIN_REC
 #define RT_PIN_REC 1
 #endif
@@ -280,7 +294,7 @@ template <bool COUNT, class GetFn>
 __device__ __forceinline__ uint32_t resolve_list(const RtDevScene& sc, const RtFrameParams& fp, const RtFrameCam& cam,
                                                  int i, int j, uint32_t nlist, const uint2 e0, GetFn&& get,
                                                  const RT_G uint2* chunk, bool dropped, float drop, Best& out,
-                                                 Shade& sh, ResolveCounts& rc) {
+                                                 Shade& sh, ResolveCounts& rc, const Ray64* pre = nullptr) {
     out.dist = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
     out.rank = 0xFFFFFFFFu;
     out.tri = -1;
@@ -291,13 +305,31 @@ __device__ __forceinline__ uint32_t resolve_list(const RtDevScene& sc, const RtF
     // as soon as its index is known; the fp64 ray is built while it is in
     // flight.  The winner's shading fields are loaded once, after the list.
     double R0[9];
+    // kSpecWin: entry 0's shading fields too (normal, {id, leaf}, leaf box:
+    // the rest of its record), requested with its MT part — entry 0 is the
+    // winner of most pixels, whose resolve then makes one memory round trip
+    // instead of two
+    double N0[3] = {0.0, 0.0, 0.0};
+    uint2 IL0 = make_uint2(0u, 0u);
+    float4 B0a = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 B0b = make_float2(0.f, 0.f);
     if (nlist > 0) {
         const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)e0.x;
 #pragma unroll
         for (int k = 0; k < 9; k++) R0[k] = T[k];
+        if constexpr (kSpecWin) {
+            N0[0] = T[RT_T64_NORMAL];
+            N0[1] = T[RT_T64_NORMAL + 1];
+            N0[2] = T[RT_T64_NORMAL + 2];
+            IL0 = *reinterpret_cast<const RT_G uint2*>(T + RT_T64_IDLEAF);
+            B0a = *reinterpret_cast<const RT_G float4*>(T + RT_T64_BOX);
+            B0b = *reinterpret_cast<const RT_G float2*>(T + RT_T64_BOX + 2);
+        }
         __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the ray's fp64 set-up
     }
-    const Ray64 ray = gen_ray<false>(fp, cam, i, j);
+    // the pixel's fp64 ray: the walk's own (pre, kept from the tile set-up)
+    // or generated again (the same expressions, so the same bits)
+    const Ray64 ray = pre ? *pre : gen_ray<false>(fp, cam, i, j);
     double best_t = 0.0;
     // exact test of candidate e (MT part T: global or a register copy), kept
     // if it is the (distance, visit rank) minimum
@@ -348,18 +380,25 @@ __device__ __forceinline__ uint32_t resolve_list(const RtDevScene& sc, const RtF
     if (out.tri < 0) return 0;
     // the winner's shading fields: unit normal, {loader id, real leaf}, leaf
     // box (6 floats rounded inward) — the rest of its record
-    const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)out.tri;
-    sh.nx = T[RT_T64_NORMAL];
-    sh.ny = T[RT_T64_NORMAL + 1];
-    sh.nz = T[RT_T64_NORMAL + 2];
-    const uint2 il = *reinterpret_cast<const RT_G uint2*>(T + RT_T64_IDLEAF);
-    sh.id = il.x;
+    uint2 il;
     float lb[6];
-    {
+    if (kSpecWin && nlist > 0 && out.tri == (int32_t)e0.x) {  // entry 0 won: its fields are here
+        sh.nx = N0[0];
+        sh.ny = N0[1];
+        sh.nz = N0[2];
+        il = IL0;
+        lb[0] = B0a.x; lb[1] = B0a.y; lb[2] = B0a.z; lb[3] = B0a.w; lb[4] = B0b.x; lb[5] = B0b.y;
+    } else {
+        const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)out.tri;
+        sh.nx = T[RT_T64_NORMAL];
+        sh.ny = T[RT_T64_NORMAL + 1];
+        sh.nz = T[RT_T64_NORMAL + 2];
+        il = *reinterpret_cast<const RT_G uint2*>(T + RT_T64_IDLEAF);
         const float4 b0 = *reinterpret_cast<const RT_G float4*>(T + RT_T64_BOX);
         const float2 b1 = *reinterpret_cast<const RT_G float2*>(T + RT_T64_BOX + 2);
         lb[0] = b0.x; lb[1] = b0.y; lb[2] = b0.z; lb[3] = b0.w; lb[4] = b1.x; lb[5] = b1.y;
     }
+    sh.id = il.x;
     (void)hit_dist(ray, best_t, out.px, out.py, out.pz);
     // the reference must see the winner: re-verify its ancestor chain
     if (COUNT) rc.chain++;
@@ -414,12 +453,16 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     float tsl;  // distance slack (see trace_exact), fp32 rounded up
     float pd;
     uint32_t ob;
+    double kd[3];  // kKeepDir: the fp64 direction, kept for the resolve
     {
         const RtFrameParams fp = kload(&A->fp);
         const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f / fp.spp]), fp, f);  // this tile's frame
         // kFastInv: the fp32 reciprocals straight from the fp32 direction
         // (v_rcp_f32 + a Newton step: no fp64 divisions in the set-up)
         const Ray64 ray = gen_ray<!kFastInv>(fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r));
+        kd[0] = ray.dx;
+        kd[1] = ray.dy;
+        kd[2] = ray.dz;
         q = make_ray32<kFastInv>(ray, cam.pad);
         tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
         pd = cam.pad;
@@ -668,9 +711,20 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         ResolveCounts rc;
         const RT_G uint2* ch = spilled ? reinterpret_cast<const RT_G uint2*>(aux.pool) + (size_t)chunk * RT_POOL_CHUNK
                                        : nullptr;
+        Ray64 pre;
+        if constexpr (kKeepDir) {
+            pre.ox = cam.pos[0];
+            pre.oy = cam.pos[1];
+            pre.oz = cam.pos[2];
+            pre.dx = kd[0];
+            pre.dy = kd[1];
+            pre.dz = kd[2];
+            pre.ix = pre.iy = pre.iz = 0.0;
+        }
         const uint32_t redo = resolve_list<COUNT>(
             sc, fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r), nl, nl ? cand[lane] : make_uint2(0u, 0u),
-            [&](uint32_t c) { return cand[c * 64 + lane]; }, ch, dropped, drop, out, sh, rc);
+            [&](uint32_t c) { return cand[c * 64 + lane]; }, ch, dropped, drop, out, sh, rc,
+            kKeepDir ? &pre : nullptr);
         const bool hit_s = !redo && out.tri >= 0;
         if (spp == 1) {
             if (redo) {

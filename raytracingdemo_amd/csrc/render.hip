@@ -66,10 +66,10 @@ struct Ray32 {
 // use 6 / 32 of the pad instead of 4 / 32).  Zero and tiny components get
 // the same large finite value as the fp64 path (no 0 * inf NaNs).
 #ifndef RT_FAST_INV
-#define RT_FAST_INV 0
+#define RT_FAST_INV 1
 #endif
 constexpr bool kFastInv = RT_FAST_INV != 0;
-[[maybe_unused]] __device__ __forceinline__ float inv32_fast(double v) {
+__device__ __forceinline__ float inv32_fast(double v) {
     const float f = (float)v;
     float r = __builtin_amdgcn_rcpf(f);
     r = __builtin_fmaf(r, __builtin_fmaf(-f, r, 1.f), r);

@@ -232,8 +232,10 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
     # quantize_wide8), 48-B fp32 triangle records through the pre-filter,
     # 72-B fp64 Moller-Trumbore records, 52 B per ancestor-chain check and the
     # winner's 56-B record; 3 B of colour per pixel
-    alg_pose = (cs["node_fetches"] * 96 + cs["tri_prefilter"] * 48 + cs["tri_tests"] * 72
-                + cs["chain_checks"] * 52 + cs["rays"] * 56) / F + my_rows * W * 3
+    # (primary segments walked by the wave, path_kernel.h wave_walk: 256-B
+    # nodes and 48-B triangle records once per wave)
+    alg_pose = (cs["node_fetches"] * 96 + cs["wave_nodes"] * 256 + cs["wave_tris"] * 48 + cs["tri_prefilter"] * 48
+                + cs["tri_tests"] * 72 + cs["chain_checks"] * 52 + cs["rays"] * 56) / F + my_rows * W * 3
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -290,8 +292,10 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
                          "per_segment": {k: round(cs[c] / max(cs["rays"], 1), 3) for k, c in
                                          (("node_fetches", "node_fetches"), ("tri_prefilter", "tri_prefilter"),
                                           ("tri_tests_fp64", "tri_tests"), ("chain_checks", "chain_checks"))},
-                         "bytes": "node steps x 96 (quantised) + pre-filter x 48 + fp64 tests x 72 + chain checks "
-                                  "x 52 + segments x 56 + 3 per pixel"},
+                         "bytes": "per-lane node steps x 96 (quantised) + wave node steps x 256 and wave triangle "
+                                  "records x 48 (primary segments walked by the wave) + pre-filter x 48 + fp64 tests "
+                                  "x 72 + chain checks x 52 + segments x 56 + 3 per pixel",
+                         "wave_nodes_per_pose": round(cs["wave_nodes"] / F), "wave_tris_per_pose": round(cs["wave_tris"] / F)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

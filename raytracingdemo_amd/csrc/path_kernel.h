@@ -119,6 +119,166 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
     return round_up_f(__builtin_ldexp(om + sc.coord_max + 1e-30, -19));
 }
 
+// The primary segment of a packed wave (PACK: every sample of 2x2 pixels at
+// 16 spp, one per lane) through the wave-cooperative walk of the packet
+// kernel (packet_kernel.h: the 64 rays share one camera origin and a 2x2
+// pixel footprint, so a node's W child records come once per wave through
+// scalar loads, every lane slab-tests them and `ballot` picks the children
+// any ray enters) instead of 64 per-lane walks of the quantised nodes.  The
+// outputs are lane_walk's: per lane the survivors of the fp32 triangle
+// filter in cand[0 .. nc)[tid] ({triangle, t lower bound}), the culling
+// distance, and `over` when more than K survive (the lane then takes the
+// exact per-lane path).  wstack: this wave's u32 stack (>= stack bound
+// entries).  COUNT: the wave's node steps and triangle records (counters 7
+// and 12, as the packet kernel's), the lane's pre-filter tests in lc.pre.
+template <int W, int K, bool COUNT>
+__device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFrameParams& fp, const Ray32& q, float pd,
+                                          float tsl, bool valid, uint32_t* __restrict__ wstack,
+                                          uint2 (*cand)[256], int tid, LaneCounts& lc, float& tcull_out, int& nc_out,
+                                          bool& over_out) {
+    const int lane = tid & 63;
+    const uint32_t lsg = (q.ix < 0.f ? 1u : 0u) | (q.iy < 0.f ? 2u : 0u) | (q.iz < 0.f ? 4u : 0u);
+    const uint32_t dsg = uni(lsg);
+    const int oct = __ballot(valid && lsg != dsg) == 0 ? (int)dsg : 8;
+    const f2 nox{-(q.ox + pd) * q.ix, -(q.ox - pd) * q.ix};
+    const f2 noy{-(q.oy + pd) * q.iy, -(q.oy - pd) * q.iy};
+    const f2 noz{-(q.oz + pd) * q.iz, -(q.oz - pd) * q.iz};
+    float tcull = valid ? __builtin_huge_valf() : -1.f;
+    int nc = 0;
+    bool over = false;
+    uint32_t w_nodes = 0, w_tris = 0;
+    uint32_t cur = sc.root_ref;
+    if (!(cur & RT_LEAF_BIT)) cur |= sc.root_meta << 24;
+    {
+        float b[1][6];
+        for (int a = 0; a < 6; a++) b[0][a] = sc.root_box[a];
+        uint64_t h[1];
+        child_hits<1, -1>(b, q, nox, noy, noz, tcull, h);
+        if (h[0] == 0) cur = RT_INVALID_REF;
+    }
+    int sp = 0;
+    const RT_G uint8_t* const nodes = sc.nodes;
+    const RT_G float* const tri32 = sc.tri32;
+    auto walk = [&]<int OCT>() __attribute__((always_inline)) {
+        if (cur == RT_INVALID_REF) return;
+        for (;;) {
+            if (!(cur & RT_LEAF_BIT)) {
+                if (COUNT) w_nodes++;
+                float bx[W][6];
+                uint32_t rs[W];
+                const uint32_t meta = cur >> 24;
+                uint64_t hm[W];
+                {
+                    const cchild_p nb = (cchild_p)(nodes + (size_t)(cur & 0x00FFFFFFu) * (32 * W));
+                    ChildRec ch[W];
+#pragma unroll
+                    for (int c = 0; c < W; c++) ch[c] = load_child(nb + c);
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;
+                        bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
+                    }
+#pragma unroll
+                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref | (ch[c].pad << 24);
+                    child_hits<W, OCT>(bx, q, nox, noy, noz, tcull, hm);
+                }
+                const uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);
+                if (mask != 0) {
+                    const bool rev = (dsg >> (meta & 3u)) & 1u;
+                    const int near_c = rev ? 31 - __builtin_clz(mask) : __builtin_ctz(mask);
+                    const uint32_t pm = mask & ~(1u << near_c);
+                    if (pm != 0) {
+                        const uint32_t refv = lanes_of<W>(rs);
+                        const uint32_t lid = mbcnt_lo(~0u);
+                        const uint32_t below = mbcnt_lo(pm);
+                        const uint32_t mine = (pm >> (lid & 31u)) & 1u;
+                        const uint32_t above = (uint32_t)__builtin_popcount(pm) - below - mine;
+                        const int slot = (int)(rev ? below : above);
+                        if (mine & (lid < (uint32_t)W)) wstack[sp + slot] = refv;
+                        sp += __builtin_popcount(pm);
+                    }
+                    uint32_t nr = rs[0];
+#pragma unroll
+                    for (int c = 1; c < W; c++) nr = near_c == c ? rs[c] : nr;
+                    cur = nr;
+                    continue;
+                }
+            } else {
+                const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+                const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+                if (COUNT) w_tris += cnt;
+                const uint32_t end = first + cnt;
+                for (uint32_t k0 = first; k0 < end; k0 += kLeafChunk) {
+                    const cfloat_p R = (cfloat_p)(tri32 + 12 * (size_t)k0);
+                    float4 TA[kLeafChunk], TB[kLeafChunk], TC[kLeafChunk];
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        TA[t] = load_f4(R + 12 * t);
+                        TB[t] = load_f4(R + 12 * t + 4);
+                        TC[t] = load_f4(R + 12 * t + 8);
+                    }
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) pin_s(TA[t], TB[t], TC[t]);
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        const uint32_t k = k0 + t;
+                        if (k >= end) break;
+                        if (COUNT) lc.pre += valid;
+                        float tl, tu;
+                        const int cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz,
+                                                             q.co, tcull, tl, tu)
+                                              : 0;
+                        if (__ballot(cls != 0) == 0) continue;
+                        if (cls == 0) continue;
+                        if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
+                        if (nc == K) {
+                            int m = 0;
+                            for (int c = 0; c < K; c++) {
+                                const uint2 e = cand[c][tid];
+                                if (__uint_as_float(e.y) <= tcull) cand[m++][tid] = e;
+                            }
+                            nc = m;
+                        }
+                        if (nc < K) {
+                            cand[nc][tid] = make_uint2(k, __float_as_uint(tl));
+                            nc++;
+                        } else {
+                            over = true;
+                        }
+                    }
+                }
+            }
+            if (sp == 0) break;
+            sp--;
+            cur = uni(wstack[sp]);
+        }
+    };
+    switch (oct) {
+        case 0: walk.template operator()<0>(); break;
+        case 1: walk.template operator()<1>(); break;
+        case 2: walk.template operator()<2>(); break;
+        case 3: walk.template operator()<3>(); break;
+        case 4: walk.template operator()<4>(); break;
+        case 5: walk.template operator()<5>(); break;
+        case 6: walk.template operator()<6>(); break;
+        case 7: walk.template operator()<7>(); break;
+        default: walk.template operator()<-1>(); break;
+    }
+    if (COUNT && fp.counters && lane == 0) {
+        atomicAdd(&fp.counters[7], (unsigned long long)w_nodes);
+        atomicAdd(&fp.counters[12], (unsigned long long)w_tris);
+    }
+    tcull_out = tcull;
+    nc_out = nc;
+    over_out = over;
+}
+
+// Primary segments through wave_walk (PRIM, PACK on 8-wide trees whose stack
+// bound fits 128 entries): RT_PATHS_PRIMARY=0 walks them per lane.
+#ifndef RT_PATHS_PRIM
+#define RT_PATHS_PRIM 1
+#endif
+
 // Persistent waves over 8x8 pixel tiles of one pose; every lane traces all
 // spp paths of its pixel (segments in order), so the pixel's sum is formed in
 // sample order.  frame: the hash's frame number.
@@ -149,9 +309,10 @@ __device__ __forceinline__ float ray_pad(const RtDevScene& sc, const Ray64& r) {
 // pixels, one sample path per lane (lane = pixel * spp + sample; the pixels a
 // tw x th block), and the pixel's radiance is summed across its lanes in
 // sample order — the same additions as the per-lane sample loop.
-template <int W, int S, bool COUNT = false, bool PACK = false>
+template <int W, int S, bool COUNT = false, bool PACK = false, bool PRIM = false>
 __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
                                                int bounces) {
+    static_assert(!PRIM || (PACK && W == 8 && RT_PATHS_DEFER), "wave-walked primaries: packed 8-wide deferred paths");
     __shared__ uint2 lds[S][256];
 #if RT_PATHS_DEFER
     __shared__ uint2 pcand[RT_PATHS_K][256];
@@ -189,6 +350,26 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         }
         uint32_t hits = 0, segs = 0;  // segs: ray segments traced (RT_FLAG_COUNT)
         LaneCounts tot;               // COUNT: the lane's fetch counts over its paths
+        // PRIM: the primary segment of every lane of the wave (one sample per
+        // lane) walked together, before the lanes go their own ways
+        float p_tcull = 0.f;
+        int p_nc = 0;
+        bool p_over = false;
+        if constexpr (PRIM) {
+            const bool valid = i < fp.W && r < fp.nrows;
+            const int iv = valid ? i : 0, jv = rt_image_row(fp.row0, fp.row_stride, fp.band, valid ? r : 0);
+            const uint32_t seed = path_seed(frame, (uint32_t)jv * (uint32_t)fp.W + (uint32_t)iv, (uint32_t)s0);
+            RtFrameCam c1 = cam;
+            c1.ox = path_u(seed, 0);
+            c1.oy = path_u(seed, 1);
+            const Ray64 ray0 = gen_ray<false>(fp, c1, iv, jv);
+            const float pd = ray_pad(sc, ray0);
+            const Ray32 q0 = make_ray32<true>(ray0, pd);
+            const float tsl = round_up_f(0x1p-40 * ((double)q0.co + 1.0));
+            uint32_t* wstack = reinterpret_cast<uint32_t*>(&lds[0][tid & ~63]);  // 128 u32 of this wave's row
+            wave_walk<W, RT_PATHS_K, COUNT>(sc, fp, q0, pd, tsl, valid, wstack, pcand, tid, tot, p_tcull, p_nc,
+                                            p_over);
+        }
         if (i < fp.W && r < fp.nrows) {
             const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
             const size_t pix = (size_t)r * fp.W + i;
@@ -207,8 +388,20 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                 for (int b = 0; b <= bounces; b++) {
                     LaneCounts lc;
 #if RT_PATHS_DEFER
-                    const Win win = trace_deferred<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES>(
-                        sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, pcand, lc);
+                    Win win;
+                    if (PRIM && b == 0) {
+                        // the wave walk's list: trace_deferred's resolve and fall-backs
+                        auto ray_of = [&]() { return with_inv(ray); };
+                        if (p_over) {
+                            win = trace_core<W, S, COUNT>(sc, ray_of, ray_pad(sc, ray), st, 0, lc);
+                        } else if (resolve_cands<COUNT>(sc, ray_of(), [&](int c) { return pcand[c][tid]; }, p_nc,
+                                                        p_tcull, win, lc) != 0) {
+                            win = trace_core<W, S, COUNT>(sc, ray_of, ray_pad(sc, ray), st, 1, lc);
+                        }
+                    } else {
+                        win = trace_deferred<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES>(
+                            sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, pcand, lc);
+                    }
 #else
                     const Win win =
                         trace_core<W, S, COUNT>(sc, [&]() { return with_inv(ray); }, ray_pad(sc, ray), st, 0, lc);

@@ -1108,6 +1108,15 @@ hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_of
     return hipGetLastError();
 }
 
+// Packed primary path segments through the wave walk: 8-wide trees whose
+// stack bound fits a wave's 128-entry stack (RT_PATHS_PRIMARY=0: per lane;
+// read per call).
+bool paths_primary_wave(const RtDevScene& sc) {
+    const char* e = getenv("RT_PATHS_PRIMARY");
+    if (e && e[0] == '0') return false;
+    return RT_PATHS_PRIM && RT_PATHS_DEFER && sc.width == 8 && sc.stack_bound <= (uint32_t)kPacketStack;
+}
+
 // Diffuse path tracing of one pose (path_kernel.h): spp paths per pixel of
 // 1 + bounces segments each, on a zeroed work queue; leaves it dirty.
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
@@ -1125,7 +1134,14 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
         case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         case 8:
             // (fp.pack: a wave holds every sample of 64 / spp pixels)
-            if (fp.counters && fp.pack)  // the counting pass: fetch counts too
+            if (fp.pack && paths_primary_wave(sc)) {  // primary segments by the wave walk (path_kernel.h)
+                if (fp.counters)
+                    hipLaunchKernelGGL((k_paths<8, kPathStack, true, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
+                                       bounces);
+                else
+                    hipLaunchKernelGGL((k_paths<8, kPathStack, false, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
+                                       bounces);
+            } else if (fp.counters && fp.pack)  // the counting pass: fetch counts too
                 hipLaunchKernelGGL((k_paths<8, kPathStack, true, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
             else if (fp.counters)
                 hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);

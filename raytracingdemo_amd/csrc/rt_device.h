@@ -66,11 +66,15 @@
 // one atomic, sized by the host; a dry pool falls back to the certified
 // dropped bound).  With spp > 1 the LDS entries go to HBM for k_resolve
 // ([RT_CAND_LDS][pixels] + count byte + dropped bound + chunk index).
+#ifndef RT_CAND_LDS
 #define RT_CAND_LDS 8
+#endif
 #define RT_POOL_CHUNK 24
 // Quantised W = 8 node for the per-lane walk (walk_tree.cpp quantize_wide8):
 // origin, exponents, SoA 8-bit planes, refs.
+#ifndef RT_QNODE_BYTES
 #define RT_QNODE_BYTES 96
+#endif
 // tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
 #define RT_TRI32_PAD 4
 

@@ -45,6 +45,9 @@ for s in $STEPS; do
         rehearse) RT_BENCH_REHEARSE=1 run rehearse2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                       --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu ;;
         spp4)  run bench_spp4 300 python bench.py --no-cpu --steps 5 --spp 4 ;;
+        ptests) run ptests 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_headline.py -x -v --timeout 600 \
+                   --timeout-method thread -p no:cacheprovider -k "paths or c5 or spp_one" ;;
+        paths0) RT_PATHS_PRIMARY=0 run bench_paths0 300 python bench.py --paths --no-cpu --steps 3 --warmup 1 ;;
         paths) run bench_paths 300 python bench.py --paths --steps 3 --warmup 1 ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
                    -- python bench.py --steps 3 --warmup 1 --no-cpu --no-dropin ;;

@@ -309,20 +309,29 @@ __device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, 
 // instead of 256 B: 6 vector loads per node step instead of 16; the planes
 // are 8-bit offsets from a per-node origin in steps of 2^e, each plane's t
 // one fma from per-node terms — DESIGN.md §11).
+#ifndef RT_PATHS_WW
+#define RT_PATHS_WW 0
+#endif
 template <int W, int S, int K, bool COUNT, bool QN = false>
-__device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, float tsl, LaneStack<S>& st,
-                                          uint2 (*cand)[256], LaneCounts& lc, float& tcull_out, int& nc_out,
-                                          bool& over_out) {
+struct LaneWalk {
     static_assert(!QN || W == 8, "quantised nodes are 8 wide");
-    constexpr int G = W < 4 ? W : 4;  // children tested per load group
-    const int tid = st.tid;
-    const bool sx = q.ix < 0.f, sy = q.iy < 0.f, sz = q.iz < 0.f;
-    float tcull = __builtin_huge_valf();
-    int nc = 0;
-    bool over = false;
-    st.top = 0;
-    uint32_t cur = sc.root_ref;
-    {
+    static constexpr int G = W < 4 ? W : 4;  // children tested per load group
+    Ray32 q;
+    float tsl;
+    float tcull;
+    int nc;
+    bool over;
+    uint32_t cur;  // the node or leaf to visit next; RT_INVALID_REF: the walk is over
+
+    // The root test; the walk starts at the root if the ray enters its box.
+    __device__ __forceinline__ void begin(const RtDevScene& sc, const Ray32& q_, float tsl_, LaneStack<S>& st) {
+        q = q_;
+        tsl = tsl_;
+        tcull = __builtin_huge_valf();
+        nc = 0;
+        over = false;
+        st.top = 0;
+        cur = sc.root_ref;
         const float* b = sc.root_box;
         const float tx0 = __builtin_fmaf(q.ix >= 0.f ? b[0] : b[1], q.ix, -q.onx);
         const float tx1 = __builtin_fmaf(q.ix >= 0.f ? b[1] : b[0], q.ix, -q.ofx);
@@ -334,117 +343,9 @@ __device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, 
         const float tf = fminf(fminf(tx1, ty1), tz1);
         if (!(tn <= tf)) cur = RT_INVALID_REF;
     }
-    while (cur != RT_INVALID_REF) {
-        if (!(cur & RT_LEAF_BIT)) {
-            if (COUNT) lc.nodes++;
-            float tn[W];
-            uint32_t rb[W];
-            uint32_t mask = 0;
-            if constexpr (QN) {
-                const uint4* qb = reinterpret_cast<const uint4*>(sc.qnodes + (size_t)cur * RT_QNODE_BYTES);
-                const uint4 h = qb[0], PX = qb[1], PY = qb[2], PZ = qb[3], R0 = qb[4], R1 = qb[5];
-                // t of plane q: q (2^e ix) + (origin ix - o_near/far ix), exactly
-                // the fp32 walk's plane with o +- pad (make_ray32)
-                const float ox = __uint_as_float(h.x), oy = __uint_as_float(h.y), oz = __uint_as_float(h.z);
-                const float ssx = __uint_as_float((h.w & 0xFFu) << 23) * q.ix;
-                const float ssy = __uint_as_float(((h.w >> 8) & 0xFFu) << 23) * q.iy;
-                const float ssz = __uint_as_float(((h.w >> 16) & 0xFFu) << 23) * q.iz;
-                const float anx = __builtin_fmaf(ox, q.ix, -q.onx), afx = __builtin_fmaf(ox, q.ix, -q.ofx);
-                const float any_ = __builtin_fmaf(oy, q.iy, -q.ony), afy = __builtin_fmaf(oy, q.iy, -q.ofy);
-                const float anz = __builtin_fmaf(oz, q.iz, -q.onz), afz = __builtin_fmaf(oz, q.iz, -q.ofz);
-                // near / far plane bytes: lo for a positive direction, hi for a negative one
-                const uint32_t nx0 = sx ? PX.z : PX.x, nx1 = sx ? PX.w : PX.y, fx0 = sx ? PX.x : PX.z,
-                               fx1 = sx ? PX.y : PX.w;
-                const uint32_t ny0 = sy ? PY.z : PY.x, ny1 = sy ? PY.w : PY.y, fy0 = sy ? PY.x : PY.z,
-                               fy1 = sy ? PY.y : PY.w;
-                const uint32_t nz0 = sz ? PZ.z : PZ.x, nz1 = sz ? PZ.w : PZ.y, fz0 = sz ? PZ.x : PZ.z,
-                               fz1 = sz ? PZ.y : PZ.w;
-                const uint32_t refs[8] = {R0.x, R0.y, R0.z, R0.w, R1.x, R1.y, R1.z, R1.w};
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    const int sh = 8 * (c & 3);
-                    auto byte = [&](uint32_t w0, uint32_t w1) { return (float)(((c < 4 ? w0 : w1) >> sh) & 0xFFu); };
-                    const float a0 = __builtin_fmaf(byte(nx0, nx1), ssx, anx);
-                    const float a1 = __builtin_fmaf(byte(fx0, fx1), ssx, afx);
-                    const float b0 = __builtin_fmaf(byte(ny0, ny1), ssy, any_);
-                    const float b1 = __builtin_fmaf(byte(fy0, fy1), ssy, afy);
-                    const float c0 = __builtin_fmaf(byte(nz0, nz1), ssz, anz);
-                    const float c1 = __builtin_fmaf(byte(fz0, fz1), ssz, afz);
-                    const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
-                    const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
-                    tn[c] = t0;
-                    rb[c] = refs[c];
-                    if (t0 <= t1 && refs[c] != RT_INVALID_REF) mask |= 1u << c;
-                }
-            } else {
-            const float4* nb = reinterpret_cast<const float4*>(sc.nodes + (size_t)cur * sc.node_bytes);
-#pragma unroll
-            for (int g = 0; g < W; g += G) {
-                float4 lo[G], hi[G];  // {lx,hx,ly,hy}, {lz,hz,ref,pad}
-#pragma unroll
-                for (int c = 0; c < G; c++) {
-                    lo[c] = nb[2 * (g + c)];
-                    hi[c] = nb[2 * (g + c) + 1];
-                }
-#pragma unroll
-                for (int c = 0; c < G; c++) {
-                    const float a0 = __builtin_fmaf(sx ? lo[c].y : lo[c].x, q.ix, -q.onx);
-                    const float a1 = __builtin_fmaf(sx ? lo[c].x : lo[c].y, q.ix, -q.ofx);
-                    const float b0 = __builtin_fmaf(sy ? lo[c].w : lo[c].z, q.iy, -q.ony);
-                    const float b1 = __builtin_fmaf(sy ? lo[c].z : lo[c].w, q.iy, -q.ofy);
-                    const float c0 = __builtin_fmaf(sz ? hi[c].y : hi[c].x, q.iz, -q.onz);
-                    const float c1 = __builtin_fmaf(sz ? hi[c].x : hi[c].y, q.iz, -q.ofz);
-                    const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
-                    const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
-                    const uint32_t ref = __float_as_uint(hi[c].z);
-                    tn[g + c] = t0;
-                    rb[g + c] = ref;
-                    if (t0 <= t1 && ref != RT_INVALID_REF) mask |= 1u << (g + c);
-                }
-            }
-            }
-            if (mask) {
-                // push all hit children but the nearest, farthest first
-                while (__builtin_popcount(mask) > 1) {
-                    float far_t = -1.f;
-                    int far_c = 0;
-#pragma unroll
-                    for (int c = 0; c < W; c++)
-                        if (((mask >> c) & 1u) && tn[c] > far_t) { far_t = tn[c]; far_c = c; }
-                    st.push(rb[far_c], far_t);
-                    mask &= ~(1u << far_c);
-                }
-                cur = rb[__builtin_ctz(mask)];
-                continue;
-            }
-        } else {
-            const uint32_t first = cur & RT_LEAF_FIRST_MASK;
-            const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
-            for (uint32_t k = first; k < first + cnt; k++) {
-                const float4* R = reinterpret_cast<const float4*>(sc.tri32 + 12 * (size_t)k);
-                if (COUNT) lc.pre++;
-                float tl, tu;
-                const int cls = tri_classify(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull, tl, tu);
-                if (cls == 0) continue;
-                // dist of a certain hit <= (tu + slack)(1 + 2^-20)
-                if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
-                if (nc == K) {
-                    int m = 0;
-                    for (int c = 0; c < K; c++) {
-                        const uint2 e = cand[c][tid];
-                        if (__uint_as_float(e.y) <= tcull) cand[m++][tid] = e;
-                    }
-                    nc = m;
-                }
-                if (nc < K) {
-                    cand[nc][tid] = make_uint2(k, __float_as_uint(tl));
-                    nc++;
-                } else {
-                    over = true;
-                }
-            }
-        }
-        // pop the next subtree still in front of the culling distance
+
+    // The next subtree still in front of the culling distance, off the stack.
+    __device__ __forceinline__ void pop_next(LaneStack<S>& st) {
         cur = RT_INVALID_REF;
         while (st.top > 0) {
             const uint2 e = st.pop();
@@ -454,9 +355,154 @@ __device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, 
             }
         }
     }
-    tcull_out = tcull;
-    nc_out = nc;
-    over_out = over;
+
+    // An inner node: descend into its nearest hit child (the others pushed),
+    // or pop if no child is hit.
+    __device__ __forceinline__ void visit_node(const RtDevScene& sc, LaneStack<S>& st, LaneCounts& lc) {
+        const bool sx = q.ix < 0.f, sy = q.iy < 0.f, sz = q.iz < 0.f;
+        if (COUNT) lc.nodes++;
+        float tn[W];
+        uint32_t rb[W];
+        uint32_t mask = 0;
+        if constexpr (QN) {
+            const uint4* qb = reinterpret_cast<const uint4*>(sc.qnodes + (size_t)cur * RT_QNODE_BYTES);
+            const uint4 h = qb[0], PX = qb[1], PY = qb[2], PZ = qb[3], R0 = qb[4], R1 = qb[5];
+            // t of plane q: q (2^e ix) + (origin ix - o_near/far ix), exactly
+            // the fp32 walk's plane with o +- pad (make_ray32)
+            const float ox = __uint_as_float(h.x), oy = __uint_as_float(h.y), oz = __uint_as_float(h.z);
+            const float ssx = __uint_as_float((h.w & 0xFFu) << 23) * q.ix;
+            const float ssy = __uint_as_float(((h.w >> 8) & 0xFFu) << 23) * q.iy;
+            const float ssz = __uint_as_float(((h.w >> 16) & 0xFFu) << 23) * q.iz;
+            const float anx = __builtin_fmaf(ox, q.ix, -q.onx), afx = __builtin_fmaf(ox, q.ix, -q.ofx);
+            const float any_ = __builtin_fmaf(oy, q.iy, -q.ony), afy = __builtin_fmaf(oy, q.iy, -q.ofy);
+            const float anz = __builtin_fmaf(oz, q.iz, -q.onz), afz = __builtin_fmaf(oz, q.iz, -q.ofz);
+            // near / far plane bytes: lo for a positive direction, hi for a negative one
+            const uint32_t nx0 = sx ? PX.z : PX.x, nx1 = sx ? PX.w : PX.y, fx0 = sx ? PX.x : PX.z,
+                           fx1 = sx ? PX.y : PX.w;
+            const uint32_t ny0 = sy ? PY.z : PY.x, ny1 = sy ? PY.w : PY.y, fy0 = sy ? PY.x : PY.z,
+                           fy1 = sy ? PY.y : PY.w;
+            const uint32_t nz0 = sz ? PZ.z : PZ.x, nz1 = sz ? PZ.w : PZ.y, fz0 = sz ? PZ.x : PZ.z,
+                           fz1 = sz ? PZ.y : PZ.w;
+            const uint32_t refs[8] = {R0.x, R0.y, R0.z, R0.w, R1.x, R1.y, R1.z, R1.w};
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const int sh = 8 * (c & 3);
+                auto byte = [&](uint32_t w0, uint32_t w1) { return (float)(((c < 4 ? w0 : w1) >> sh) & 0xFFu); };
+                const float a0 = __builtin_fmaf(byte(nx0, nx1), ssx, anx);
+                const float a1 = __builtin_fmaf(byte(fx0, fx1), ssx, afx);
+                const float b0 = __builtin_fmaf(byte(ny0, ny1), ssy, any_);
+                const float b1 = __builtin_fmaf(byte(fy0, fy1), ssy, afy);
+                const float c0 = __builtin_fmaf(byte(nz0, nz1), ssz, anz);
+                const float c1 = __builtin_fmaf(byte(fz0, fz1), ssz, afz);
+                const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
+                const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
+                tn[c] = t0;
+                rb[c] = refs[c];
+                if (t0 <= t1 && refs[c] != RT_INVALID_REF) mask |= 1u << c;
+            }
+        } else {
+        const float4* nb = reinterpret_cast<const float4*>(sc.nodes + (size_t)cur * sc.node_bytes);
+#pragma unroll
+        for (int g = 0; g < W; g += G) {
+            float4 lo[G], hi[G];  // {lx,hx,ly,hy}, {lz,hz,ref,pad}
+#pragma unroll
+            for (int c = 0; c < G; c++) {
+                lo[c] = nb[2 * (g + c)];
+                hi[c] = nb[2 * (g + c) + 1];
+            }
+#pragma unroll
+            for (int c = 0; c < G; c++) {
+                const float a0 = __builtin_fmaf(sx ? lo[c].y : lo[c].x, q.ix, -q.onx);
+                const float a1 = __builtin_fmaf(sx ? lo[c].x : lo[c].y, q.ix, -q.ofx);
+                const float b0 = __builtin_fmaf(sy ? lo[c].w : lo[c].z, q.iy, -q.ony);
+                const float b1 = __builtin_fmaf(sy ? lo[c].z : lo[c].w, q.iy, -q.ofy);
+                const float c0 = __builtin_fmaf(sz ? hi[c].y : hi[c].x, q.iz, -q.onz);
+                const float c1 = __builtin_fmaf(sz ? hi[c].x : hi[c].y, q.iz, -q.ofz);
+                const float t0 = fmaxf(fmaxf(a0, b0), fmaxf(c0, 0.f));
+                const float t1 = fminf(fminf(a1, b1), fminf(c1, tcull));
+                const uint32_t ref = __float_as_uint(hi[c].z);
+                tn[g + c] = t0;
+                rb[g + c] = ref;
+                if (t0 <= t1 && ref != RT_INVALID_REF) mask |= 1u << (g + c);
+            }
+        }
+        }
+        if (mask) {
+            // push all hit children but the nearest, farthest first
+            while (__builtin_popcount(mask) > 1) {
+                float far_t = -1.f;
+                int far_c = 0;
+#pragma unroll
+                for (int c = 0; c < W; c++)
+                    if (((mask >> c) & 1u) && tn[c] > far_t) { far_t = tn[c]; far_c = c; }
+                st.push(rb[far_c], far_t);
+                mask &= ~(1u << far_c);
+            }
+            cur = rb[__builtin_ctz(mask)];
+            return;
+        }
+        pop_next(st);
+    }
+
+    // A leaf: its triangles through tri_classify into the candidate list; pop.
+    __device__ __forceinline__ void visit_leaf(LaneStack<S>& st, const RtDevScene& sc, uint2 (*cand)[256],
+                                               LaneCounts& lc) {
+        const int tid = st.tid;
+        const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+        const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+        for (uint32_t k = first; k < first + cnt; k++) {
+            const float4* R = reinterpret_cast<const float4*>(sc.tri32 + 12 * (size_t)k);
+            if (COUNT) lc.pre++;
+            float tl, tu;
+            const int cls = tri_classify(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull, tl, tu);
+            if (cls == 0) continue;
+            // dist of a certain hit <= (tu + slack)(1 + 2^-20)
+            if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
+            if (nc == K) {
+                int m = 0;
+                for (int c = 0; c < K; c++) {
+                    const uint2 e = cand[c][tid];
+                    if (__uint_as_float(e.y) <= tcull) cand[m++][tid] = e;
+                }
+                nc = m;
+            }
+            if (nc < K) {
+                cand[nc][tid] = make_uint2(k, __float_as_uint(tl));
+                nc++;
+            } else {
+                over = true;
+            }
+        }
+        pop_next(st);
+    }
+
+    // One step of the walk (cur valid).  WW ("while-while"): a lane at an
+    // inner node descends until it reaches a leaf or its walk ends, then
+    // visits that leaf, so the wave's node and leaf visits are not
+    // interleaved lane by lane; else one node or leaf visit.
+    __device__ __forceinline__ void step(const RtDevScene& sc, LaneStack<S>& st, uint2 (*cand)[256], LaneCounts& lc) {
+        if constexpr (RT_PATHS_WW) {
+            while (cur != RT_INVALID_REF && !(cur & RT_LEAF_BIT)) visit_node(sc, st, lc);
+            if (cur != RT_INVALID_REF) visit_leaf(st, sc, cand, lc);
+        } else if (!(cur & RT_LEAF_BIT)) {
+            visit_node(sc, st, lc);
+        } else {
+            visit_leaf(st, sc, cand, lc);
+        }
+    }
+};
+
+// lane_walk: the fp32 walk of ray q to its end (LaneWalk::begin, then steps).
+template <int W, int S, int K, bool COUNT, bool QN = false>
+__device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, float tsl, LaneStack<S>& st,
+                                          uint2 (*cand)[256], LaneCounts& lc, float& tcull_out, int& nc_out,
+                                          bool& over_out) {
+    LaneWalk<W, S, K, COUNT, QN> w;
+    w.begin(sc, q, tsl, st);
+    while (w.cur != RT_INVALID_REF) w.step(sc, st, cand, lc);
+    tcull_out = w.tcull;
+    nc_out = w.nc;
+    over_out = w.over;
 }
 
 // Exact resolve of a candidate list (k_resolve's selection): the (distance,
@@ -1111,6 +1157,14 @@ hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_of
 // Packed primary path segments through the wave walk: 8-wide trees whose
 // stack bound fits a wave's 128-entry stack (RT_PATHS_PRIMARY=0: per lane;
 // read per call).
+// Lanes of a packed path wave walk on their own after the primary segment;
+// the wave resolves the finished walks together once at least this many
+// lanes wait (path_kernel.h, DYN); 0: every segment in lock step.
+int paths_refill() {
+    const char* e = getenv("RT_PATHS_REFILL");
+    return e ? atoi(e) : RT_PATHS_REFILL;
+}
+
 bool paths_primary_wave(const RtDevScene& sc) {
     const char* e = getenv("RT_PATHS_PRIMARY");
     if (e && e[0] == '0') return false;
@@ -1122,6 +1176,7 @@ bool paths_primary_wave(const RtDevScene& sc) {
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
                         int bounces, hipStream_t s, const hipEvent_t* ev) {
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
+    const int refill = paths_refill();
     if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.tile_ctr || !aux.spill || aux.grid <= 0 ||
         aux.spill_cap + kPathStack < sc.stack_bound)
         return hipErrorInvalidValue;
@@ -1130,27 +1185,33 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     const dim3 grid((unsigned)aux.grid), blk(256);
     if (ev) (void)hipEventRecord(ev[0], s);
     switch (sc.width) {
-        case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
-        case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill); break;
+        case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill); break;
         case 8:
             // (fp.pack: a wave holds every sample of 64 / spp pixels)
             if (fp.pack && paths_primary_wave(sc)) {  // primary segments by the wave walk (path_kernel.h)
-                if (fp.counters)
+                if (fp.counters && refill > 0)
+                    hipLaunchKernelGGL((k_paths<8, kPathStack, true, true, true, true>), grid, blk, 0, s, sc, fp, aux,
+                                       frame, bounces, refill);
+                else if (refill > 0)
+                    hipLaunchKernelGGL((k_paths<8, kPathStack, false, true, true, true>), grid, blk, 0, s, sc, fp, aux,
+                                       frame, bounces, refill);
+                else if (fp.counters)
                     hipLaunchKernelGGL((k_paths<8, kPathStack, true, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
-                                       bounces);
+                                       bounces, refill);
                 else
                     hipLaunchKernelGGL((k_paths<8, kPathStack, false, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
-                                       bounces);
+                                       bounces, refill);
             } else if (fp.counters && fp.pack)  // the counting pass: fetch counts too
-                hipLaunchKernelGGL((k_paths<8, kPathStack, true, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                hipLaunchKernelGGL((k_paths<8, kPathStack, true, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
             else if (fp.counters)
-                hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
             else if (fp.pack)
-                hipLaunchKernelGGL((k_paths<8, kPathStack, false, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                hipLaunchKernelGGL((k_paths<8, kPathStack, false, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
             else
-                hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
             break;
-        case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill); break;
         default: return hipErrorInvalidValue;
     }
     if (ev) (void)hipEventRecord(ev[1], s);

@@ -96,6 +96,28 @@ for s in $STEPS; do
                    rc=$?; echo "ab$i exit=$rc"; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/ab$i.log; exit $rc; }
                    python -c "import json; l=[x for x in open('gpurun_out/ab$i.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']; q=r['per_ray']; print('RESULT', '$c', d['value'], r['kernel_ms_avg'], q['wave_nodes_per_tile'], q['wave_leaves_per_tile'], q['wave_tris_per_tile'], q['tri_tests_fp64'])" || true
                done ;;
+        sqlite) # SQ passes 1 and 3 of `sq` for the library RT_LIB names: gpurun_out/sq_${SQ_TAG}
+               t=${SQ_TAG:-x}
+               for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
+                           "SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_TC_DATA_READ_REQ SQC_TC_STALL SQ_INST_LEVEL_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"; do
+                   pn=$((${pn:-0}+1))
+                   run sq_${t}_$pn 600 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sq_$t -o sq$pn \
+                       -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin || exit 1
+               done
+               python tools/pmc_summary.py gpurun_out/sq_$t/sq*_counter_collection.csv > gpurun_out/sq_summary_$t.txt ;;
+        pab)   # paths A/B: PAB_ENVS="A=1;RT_LIB=...;..." (one paths bench per entry)
+               i=0; IFS=';' read -ra cfgs <<< "${PAB_ENVS:-}"
+               for c in "${cfgs[@]}"; do i=$((i+1))
+                   env $c timeout -k 10 300 python bench.py --paths --no-cpu --steps 3 --warmup 1 > gpurun_out/pab$i.log 2>&1
+                   rc=$?; echo "pab$i exit=$rc"; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/pab$i.log; exit $rc; }
+                   python -c "import json; l=[x for x in open('gpurun_out/pab$i.log') if x.startswith('{')][-1]; d=json.loads(l); print('RESULT', '$c', d['value'], d['kernel_ms_avg'])" || true
+               done ;;
+        pdiv)  run pdiv 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
+                   SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pdiv -o paths \
+                   -- python bench.py --paths --steps 1 --warmup 0 --no-cpu && \
+               run hdiv 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
+                   SQ_BUSY_CYCLES --output-format csv -d gpurun_out/hdiv -o head \
+                   -- python bench.py --steps 1 --warmup 0 --no-cpu --no-dropin ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

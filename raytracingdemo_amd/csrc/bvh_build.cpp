@@ -917,38 +917,6 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
         }
         f.root_meta = (f.root_ref != RT_INVALID_REF && !(f.root_ref & RT_LEAF_BIT)) ? meta[f.root_ref] : 0u;
     }
-#if RT_LDS_NODES > 0
-    // Tuning build (packet kernel with the top of the tree staged in LDS):
-    // the first RT_LDS_NODES inner nodes in breadth-first order get ids
-    // 0 .. N-1, the others keep their order after them.
-    if (f.root_ref != RT_INVALID_REF && !(f.root_ref & RT_LEAF_BIT)) {
-        const uint64_t nb = rt_node_bytes(W);
-        std::vector<uint32_t> order{f.root_ref};
-        for (size_t h = 0; h < order.size() && order.size() < (size_t)RT_LDS_NODES; h++) {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(f.wide.data() + order[h] * nb);
-            for (int c = 0; c < W && order.size() < (size_t)RT_LDS_NODES; c++) {
-                const uint32_t r = p[8 * c + RT_CHILD_REF];
-                if (r != RT_INVALID_REF && !(r & RT_LEAF_BIT)) order.push_back(r);
-            }
-        }
-        std::vector<uint32_t> perm(f.n_wide, ~0u);
-        uint32_t next = 0;
-        for (uint32_t x : order) perm[x] = next++;
-        for (uint64_t x = 0; x < f.n_wide; x++)
-            if (perm[x] == ~0u) perm[x] = next++;
-        std::vector<uint8_t> out(f.wide.size());
-        for (uint64_t x = 0; x < f.n_wide; x++) {
-            uint32_t* p = reinterpret_cast<uint32_t*>(out.data() + perm[x] * nb);
-            std::memcpy(p, f.wide.data() + x * nb, nb);
-            for (int c = 0; c < W; c++) {
-                uint32_t& r = p[8 * c + RT_CHILD_REF];
-                if (r != RT_INVALID_REF && !(r & RT_LEAF_BIT)) r = perm[r];
-            }
-        }
-        f.wide.swap(out);
-        f.root_ref = perm[f.root_ref];
-    }
-#endif
     // ordered traversal pushes at most W-1 siblings per wide level
     f.stack_bound = F.wide_depth * (uint32_t)(W - 1) + 1;
     return f;

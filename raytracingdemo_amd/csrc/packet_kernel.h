@@ -139,12 +139,6 @@ constexpr bool kKeepDir = RT_KEEP_DIR != 0;
 #endif
 constexpr bool kSpecWin = RT_SPEC_WIN != 0;
 
-// RT_LDS_NODES (rt_device.h, tuning builds): nodes 0 .. N-1 of an 8-wide
-// tree (the top of the walk tree, breadth-first) are read from an LDS copy
-// made by each workgroup instead of through the scalar cache.
-template <int W>
-constexpr int kLdsNodes = W == 8 ? RT_LDS_NODES : 0;
-typedef const __attribute__((address_space(3))) ChildRec* lchild_p;
 
 #ifndef RT_PIN_REC
 #define RT_PIN_REC 1
@@ -450,8 +444,7 @@ struct TileOut {
 
 template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK>
 __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, bool valid,
-                                                uint32_t* __restrict__ wstack, uint2* __restrict__ cand,
-                                                lchild_p lnodes = nullptr) {
+                                                uint32_t* __restrict__ wstack, uint2* __restrict__ cand) {
     const int lane = threadIdx.x & 63;
     const uint64_t p0 = prof_clock();
     uint64_t p_node = 0, p_leaf = 0, p_prev = 0;  // RT_PROFILE only
@@ -536,33 +529,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                 const uint32_t meta = cur >> 24;  // sort axis | valid slots << 2
                 const uint32_t nv = meta >> 2;    // valid slots (a prefix)
                 uint32_t mask;   // bit c: some lane's ray enters child c
-                const uint32_t nid = cur & 0x00FFFFFFu;
-                if (kLdsNodes<W> > 0 && nid < (uint32_t)kLdsNodes<W>) {
-                    // a node staged in LDS (RT_LDS_NODES): broadcast reads,
-                    // two children per group (16 VGPRs of records at a time)
-                    mask = 0;
-#pragma unroll
-                    for (int c = 0; c < W; c++) rs[c] = RT_INVALID_REF;
-#pragma unroll
-                    for (int g = 0; g < W; g += 2) {
-                        if (g > 0 && nv <= (uint32_t)g) break;
-                        float b[2][6];
-#pragma unroll
-                        for (int c = 0; c < 2; c++) {
-                            const lchild_p lp = lnodes + (nid * W + g + c);
-                            ChildRec rc;
-                            rc.lx = lp->lx; rc.hx = lp->hx; rc.ly = lp->ly; rc.hy = lp->hy;
-                            rc.lz = lp->lz; rc.hz = lp->hz; rc.ref = lp->ref; rc.pad = lp->pad;
-                            b[c][0] = rc.lx; b[c][1] = rc.hx; b[c][2] = rc.ly;
-                            b[c][3] = rc.hy; b[c][4] = rc.lz; b[c][5] = rc.hz;
-                            rs[g + c] = uni(rc.ref | (rc.pad << 24));
-                        }
-                        uint64_t hm[2];
-                        child_hits<2, OCT>(b, q, nox, noy, noz, tcull, hm);
-                        mask |= any_mask<2>(hm) << g;
-                    }
-                    mask &= (1u << nv) - 1u;
-                } else {
+                {
                     // all W records are loaded before any test so their loads
                     // are in flight together
                     const cchild_p nb = (cchild_p)(nodes + (size_t)(cur & 0x00FFFFFFu) * (32 * W));
@@ -1054,7 +1021,6 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     __shared__ uint32_t stacks[kPacketWaves][SP];
     __shared__ uint2 cands[kPacketWaves][K * 64];
     __shared__ PacketArgs s_args;
-    __shared__ ChildRec s_nodes[kLdsNodes<W> > 0 ? kLdsNodes<W> * W : 1];
     {
         const __attribute__((address_space(4))) uint32_t* src =
             (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1063,14 +1029,6 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
         __syncthreads();
     }
     args_p A = (args_p)&s_args;
-    if constexpr (kLdsNodes<W> > 0) {
-        const uint32_t nn = min(kword(&A->sc.n_wide), (uint32_t)kLdsNodes<W>);
-        const uint4* src = reinterpret_cast<const uint4*>(kload(&A->sc.nodes));
-        uint4* dst = reinterpret_cast<uint4*>(s_nodes);
-        for (unsigned w = threadIdx.x; w < nn * W * 2; w += blockDim.x) dst[w] = src[w];
-        __syncthreads();
-    }
-    const lchild_p lnodes = (lchild_p)s_nodes;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     // tile scheduling: one queue per XCD (blocks are dealt to the 8 XCDs
@@ -1139,7 +1097,7 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             r = ty * 8 + (lane >> 3);
         }
         const TileOut o =
-            trace_packet<W, SP, K, COUNT, FUSED, PACK>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv], lnodes);
+            trace_packet<W, SP, K, COUNT, FUSED, PACK>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);
         if constexpr (FUSED) {
             uint32_t h = (uint32_t)__builtin_popcountll(__ballot(o.hit));
             if constexpr (pack) {  // samples hit per pixel (<= 64) summed over the wave

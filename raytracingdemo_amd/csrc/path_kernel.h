@@ -278,9 +278,6 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
 #ifndef RT_PATHS_PRIM
 #define RT_PATHS_PRIM 1
 #endif
-#ifndef RT_PATHS_REFILL
-#define RT_PATHS_REFILL 0
-#endif
 
 // Persistent waves over 8x8 pixel tiles of one pose; every lane traces all
 // spp paths of its pixel (segments in order), so the pixel's sum is formed in
@@ -312,18 +309,10 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
 // pixels, one sample path per lane (lane = pixel * spp + sample; the pixels a
 // tw x th block), and the pixel's radiance is summed across its lanes in
 // sample order — the same additions as the per-lane sample loop.
-// DYN (with PRIM; refill > 0): after the primary segment every lane walks
-// its own path segments, and the wave stops walking to resolve, shade and
-// bounce the lanes whose walks have ended once `refill` of them wait (or no
-// lane walks any more); those lanes then start their next segments' walks
-// while the others carry on where they were.  The lanes of a wave are no
-// longer held in lock step per segment (a segment's walk otherwise lasts as
-// long as its longest ray's); each lane's arithmetic is unchanged.
-template <int W, int S, bool COUNT = false, bool PACK = false, bool PRIM = false, bool DYN = false>
+template <int W, int S, bool COUNT = false, bool PACK = false, bool PRIM = false>
 __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
-                                               int bounces, int refill) {
+                                               int bounces) {
     static_assert(!PRIM || (PACK && W == 8 && RT_PATHS_DEFER), "wave-walked primaries: packed 8-wide deferred paths");
-    static_assert(!DYN || PRIM, "dynamic segments follow the wave-walked primaries");
     __shared__ uint2 lds[S][256];
 #if RT_PATHS_DEFER
     __shared__ uint2 pcand[RT_PATHS_K][256];
@@ -381,106 +370,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
             wave_walk<W, RT_PATHS_K, COUNT>(sc, fp, q0, pd, tsl, valid, wstack, pcand, tid, tot, p_tcull, p_nc,
                                             p_over);
         }
-        if constexpr (DYN) {
-            const bool valid = i < fp.W && r < fp.nrows;
-            const int iv = valid ? i : 0, j = rt_image_row(fp.row0, fp.row_stride, fp.band, valid ? r : 0);
-            const size_t pix = (size_t)r * fp.W + i;
-            const uint32_t seed = path_seed(frame, (uint32_t)j * (uint32_t)fp.W + (uint32_t)iv, (uint32_t)s0);
-            RtFrameCam c1 = cam;
-            c1.ox = path_u(seed, 0);
-            c1.oy = path_u(seed, 1);
-            Ray64 ray = gen_ray<false>(fp, c1, iv, j);
-            double L[3] = {0.0, 0.0, 0.0};
-            double w = 1.0;
-            int b = 0;
-            bool alive = valid;  // the lane's path goes on
-            bool ready = valid;  // its segment b's walk is over (segment 0: the wave walk's list)
-            LaneWalk<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES> lw;
-            lw.tcull = p_tcull;
-            lw.nc = p_nc;
-            lw.over = p_over;
-            lw.cur = RT_INVALID_REF;
-            while (__ballot(alive) != 0) {
-                // walk until `refill` lanes wait for their resolve or none walks
-                for (;;) {
-                    const bool walking = alive && !ready;
-                    if (__ballot(walking) == 0 || (int)__popcll(__ballot(alive && ready)) >= refill) break;
-                    if (walking) {
-                        lw.step(sc, st, pcand, tot);
-                        ready = lw.cur == RT_INVALID_REF;
-                    }
-                }
-                if (alive && ready) {
-                    // trace_deferred's resolve and fall-backs for segment b
-                    LaneCounts lc;
-                    Win win;
-                    auto ray_of = [&]() { return with_inv(ray); };
-                    if (lw.over) {
-                        win = trace_core<W, S, COUNT>(sc, ray_of, ray_pad(sc, ray), st, 0, lc);
-                    } else if (resolve_cands<COUNT>(sc, ray_of(), [&](int c) { return pcand[c][tid]; }, lw.nc,
-                                                    lw.tcull, win, lc) != 0) {
-                        win = trace_core<W, S, COUNT>(sc, ray_of, ray_pad(sc, ray), st, 1, lc);
-                    }
-                    segs++;
-                    if (COUNT) {
-                        tot.nodes += lc.nodes;
-                        tot.pre += lc.pre;
-                        tot.tris += lc.tris;
-                        tot.chain += lc.chain;
-                    }
-                    Best hb;
-                    hb.dist = win.dist;
-                    hb.rank = win.rank;
-                    hb.tri = win.tri;
-                    hb.px = hb.py = hb.pz = 0.0;
-                    if (win.tri >= 0) (void)hit_dist(ray, win.t, hb.px, hb.py, hb.pz);
-                    const Shade sh = shade_of(sc, win.tri);
-                    if (b == 0) {
-                        store_sample(fp, pix * (size_t)fp.spp + s0, hb, sh);
-                        hits += win.tri >= 0;
-                    }
-                    alive = false;
-                    if (win.tri >= 0) {
-                        double c[3];
-                        shade_at(cam, hb.px, hb.py, hb.pz, sh.nx, sh.ny, sh.nz, c);
-                        L[0] = L[0] + w * c[0];
-                        L[1] = L[1] + w * c[1];
-                        L[2] = L[2] + w * c[2];
-                        w = w * 0.5;
-                        if (b < bounces) {
-                            double nx, ny, nz;
-                            bounce_dir(sh.nx, sh.ny, sh.nz, ray.dx, ray.dy, ray.dz,
-                                       path_u(seed, 2u + 2u * (uint32_t)b), path_u(seed, 3u + 2u * (uint32_t)b), nx,
-                                       ny, nz);
-                            ray.ox = hb.px;
-                            ray.oy = hb.py;
-                            ray.oz = hb.pz;
-                            ray.dx = nx;
-                            ray.dy = ny;
-                            ray.dz = nz;
-                            b++;
-                            // the next segment's walk (trace_deferred's set-up)
-                            const Ray32 q = make_ray32(with_inv(ray), ray_pad(sc, ray));
-                            lw.begin(sc, q, round_up_f(0x1p-40 * ((double)q.co + 1.0)), st);
-                            alive = true;
-                            ready = lw.cur == RT_INVALID_REF;
-                        }
-                    }
-                }
-            }
-            if (valid) {
-                const double acc[3] = {0.0 + L[0], 0.0 + L[1], 0.0 + L[2]};
-                // the pixel's samples are lanes base .. base + spp - 1
-                const int base = lane & ~(spp - 1);
-                double sum[3] = {0.0, 0.0, 0.0};
-                for (int k = 0; k < spp; k++) {
-                    sum[0] = sum[0] + __shfl(acc[0], base + k);
-                    sum[1] = sum[1] + __shfl(acc[1], base + k);
-                    sum[2] = sum[2] + __shfl(acc[2], base + k);
-                }
-                if (lane == base) store_rgb(fp, pix, sum);
-            }
-        } else if (i < fp.W && r < fp.nrows) {
+        if (i < fp.W && r < fp.nrows) {
             const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
             const size_t pix = (size_t)r * fp.W + i;
             double acc[3] = {0.0, 0.0, 0.0};

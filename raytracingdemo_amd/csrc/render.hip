@@ -309,9 +309,6 @@ __device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, 
 // instead of 256 B: 6 vector loads per node step instead of 16; the planes
 // are 8-bit offsets from a per-node origin in steps of 2^e, each plane's t
 // one fma from per-node terms — DESIGN.md §11).
-#ifndef RT_PATHS_WW
-#define RT_PATHS_WW 0
-#endif
 template <int W, int S, int K, bool COUNT, bool QN = false>
 struct LaneWalk {
     static_assert(!QN || W == 8, "quantised nodes are 8 wide");
@@ -476,19 +473,12 @@ struct LaneWalk {
         pop_next(st);
     }
 
-    // One step of the walk (cur valid).  WW ("while-while"): a lane at an
-    // inner node descends until it reaches a leaf or its walk ends, then
-    // visits that leaf, so the wave's node and leaf visits are not
-    // interleaved lane by lane; else one node or leaf visit.
+    // One step of the walk (cur valid): one node or leaf visit.
     __device__ __forceinline__ void step(const RtDevScene& sc, LaneStack<S>& st, uint2 (*cand)[256], LaneCounts& lc) {
-        if constexpr (RT_PATHS_WW) {
-            while (cur != RT_INVALID_REF && !(cur & RT_LEAF_BIT)) visit_node(sc, st, lc);
-            if (cur != RT_INVALID_REF) visit_leaf(st, sc, cand, lc);
-        } else if (!(cur & RT_LEAF_BIT)) {
+        if (!(cur & RT_LEAF_BIT))
             visit_node(sc, st, lc);
-        } else {
+        else
             visit_leaf(st, sc, cand, lc);
-        }
     }
 };
 
@@ -1157,14 +1147,6 @@ hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_of
 // Packed primary path segments through the wave walk: 8-wide trees whose
 // stack bound fits a wave's 128-entry stack (RT_PATHS_PRIMARY=0: per lane;
 // read per call).
-// Lanes of a packed path wave walk on their own after the primary segment;
-// the wave resolves the finished walks together once at least this many
-// lanes wait (path_kernel.h, DYN); 0: every segment in lock step.
-int paths_refill() {
-    const char* e = getenv("RT_PATHS_REFILL");
-    return e ? atoi(e) : RT_PATHS_REFILL;
-}
-
 bool paths_primary_wave(const RtDevScene& sc) {
     const char* e = getenv("RT_PATHS_PRIMARY");
     if (e && e[0] == '0') return false;
@@ -1176,7 +1158,6 @@ bool paths_primary_wave(const RtDevScene& sc) {
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
                         int bounces, hipStream_t s, const hipEvent_t* ev) {
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
-    const int refill = paths_refill();
     if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.tile_ctr || !aux.spill || aux.grid <= 0 ||
         aux.spill_cap + kPathStack < sc.stack_bound)
         return hipErrorInvalidValue;
@@ -1185,33 +1166,27 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     const dim3 grid((unsigned)aux.grid), blk(256);
     if (ev) (void)hipEventRecord(ev[0], s);
     switch (sc.width) {
-        case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill); break;
-        case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill); break;
+        case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         case 8:
             // (fp.pack: a wave holds every sample of 64 / spp pixels)
             if (fp.pack && paths_primary_wave(sc)) {  // primary segments by the wave walk (path_kernel.h)
-                if (fp.counters && refill > 0)
-                    hipLaunchKernelGGL((k_paths<8, kPathStack, true, true, true, true>), grid, blk, 0, s, sc, fp, aux,
-                                       frame, bounces, refill);
-                else if (refill > 0)
-                    hipLaunchKernelGGL((k_paths<8, kPathStack, false, true, true, true>), grid, blk, 0, s, sc, fp, aux,
-                                       frame, bounces, refill);
-                else if (fp.counters)
+                if (fp.counters)
                     hipLaunchKernelGGL((k_paths<8, kPathStack, true, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
-                                       bounces, refill);
+                                       bounces);
                 else
                     hipLaunchKernelGGL((k_paths<8, kPathStack, false, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
-                                       bounces, refill);
+                                       bounces);
             } else if (fp.counters && fp.pack)  // the counting pass: fetch counts too
-                hipLaunchKernelGGL((k_paths<8, kPathStack, true, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
+                hipLaunchKernelGGL((k_paths<8, kPathStack, true, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
             else if (fp.counters)
-                hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
+                hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
             else if (fp.pack)
-                hipLaunchKernelGGL((k_paths<8, kPathStack, false, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
+                hipLaunchKernelGGL((k_paths<8, kPathStack, false, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
             else
-                hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill);
+                hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
             break;
-        case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces, refill); break;
+        case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
         default: return hipErrorInvalidValue;
     }
     if (ev) (void)hipEventRecord(ev[1], s);

@@ -75,11 +75,6 @@
 #ifndef RT_QNODE_BYTES
 #define RT_QNODE_BYTES 96
 #endif
-// Tuning builds only (0 in the product): the packet kernel stages the first
-// RT_LDS_NODES wide nodes in LDS, numbered breadth-first (bvh_build.cpp flatten).
-#ifndef RT_LDS_NODES
-#define RT_LDS_NODES 0
-#endif
 // tri32 is followed by this many zero records (chunked leaf fetches may read past the end)
 #define RT_TRI32_PAD 4
 

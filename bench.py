@@ -42,6 +42,7 @@ OUT_BYTES = 15         # u32 hit-id + f64 distance + 3 B rgb written per ray
 CAND_BYTES = 8         # one candidate entry {triangle, t bound} handed to the resolve kernel
 SAMPLE_BYTES = 37      # spp > 1, fused: u32 hit-id + f64 distance + the sample's f64 colour + status byte
 PACKED_SAMPLE_BYTES = 12  # spp 4 / 16, fused and packed (one wave holds a pixel's samples): hit-id + distance
+SETTLE_S = 0.1         # untimed render-only steps after the W warm-up steps: at least this much GPU work
 
 
 def host_cores():
@@ -91,6 +92,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-dropin", action="store_true", help="skip the rt_render_frame (drop-in path) rate")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="issue every step on one stream (no overlap of consecutive steps' launches)")
     p.add_argument("--shard-of", type=int, default=1,
                    help="diagnostic (one process): render only shard 0 of N interleaved row shards — the per-GPU "
                         "work of an N-rank run without its gather; not the headline")
@@ -209,21 +212,20 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
     gather_rgb = coll(rgb).new_empty((world,) + tuple(rgb.shape)) if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev)
 
-    def step(k, timing=False, count=False):
+    def render(k, timing=False, count=False):
         pos, d = path.circular_path(k % 36)
         for f in range(F):
             scene.render_paths_device(local, pos, d, W, H, rank, world, my_rows, frame=k % 36, spp=S, bounces=B,
                                       rgb=rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
                                       timing=timing, count=count)
+
+    def step(k, timing=False, count=False):
+        render(k, timing=timing, count=count)
         if world > 1:
             return gather_frames(coll(rgb), H, world, rank, out=gather_rgb, band=1)
         return rgb
 
-    for w in range(a.warmup):
-        step(w, timing=True)
-    torch.cuda.synchronize(dev)
-    scene.frame_stats(local, reset=True)
-    step(0, count=True)  # counting pass: segments traced (outside timing)
+    render(0, count=True)  # counting pass: segments traced (outside timing)
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
     segs_per_pose = cs["rays"] / F
@@ -236,6 +238,17 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
     # nodes and 48-B triangle records once per wave)
     alg_pose = (cs["node_fetches"] * 96 + cs["wave_nodes"] * 256 + cs["wave_tris"] * 48 + cs["tri_prefilter"] * 48
                 + cs["tri_tests"] * 72 + cs["chain_checks"] * 52 + cs["rays"] * 56) / F + my_rows * W * 3
+    # W warm-up steps, then render-only steps until SETTLE_S of GPU work (main())
+    for w in range(a.warmup):
+        step(w, timing=True)
+    torch.cuda.synchronize(dev)
+    settled = 0
+    t_set = time.perf_counter()
+    while time.perf_counter() - t_set < SETTLE_S:
+        render(settled, timing=True)
+        torch.cuda.synchronize(dev)
+        settled += 1
+    scene.frame_stats(local, reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -275,7 +288,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
         line = {
             "metric": f"Mrays/sec (primary + {B} diffuse bounces, {S}spp) on Sponza {W}x{H}",
             "value": round(nominal / elapsed / 1e6, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "warmup": a.warmup, "settle_steps": settled,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32 traversal + f64 exact hits",
             "data": f"synthetic: {label}",
             "config": {"workload": f"{label}, {W}x{H}x{S}spp, 1 + {B} bounce segments per sample, diffuse paths, "
@@ -418,13 +432,16 @@ def main():
     rows = rows_per_rank(H, sworld)            # rows per rank (padded)
     my_rows = len(shard_rows(srank, sworld, H))
     S = a.spp
-    # Two buffer sets: step k renders into set k % 2 while set (k - 1) % 2 is
-    # still being gathered (the gather of step k overlaps the render of step
-    # k + 1; the render of step k + 2 waits for the gather of step k).
-    NB = 2 if world > 1 else 1
+    # Two buffer sets and two streams: step k renders into set k % 2 on
+    # stream k % 2, so the library runs consecutive steps' launches
+    # concurrently (step k + 1's waves fill the CUs step k's tail leaves idle;
+    # include/rt.h "Device ordering"), and with N > 1 the gather of step k
+    # overlaps the render of step k + 1 (the render of step k + 2 waits for
+    # the gather of step k).  --no-overlap: one stream.
+    NB = 2
     ids = [torch.empty((F, rows, W, S), dtype=torch.int32, device=dev) for _ in range(NB)]
     # per-sample hit distance |hit - o| (stack_bvh.hpp:631), written in the timed region
-    dists = torch.empty((F, my_rows, W, S), dtype=torch.float64, device=dev)
+    dists = [torch.empty((F, my_rows, W, S), dtype=torch.float64, device=dev) for _ in range(NB)]
     rgb = [torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
     cnt = [torch.zeros((F,), dtype=torch.int64, device=dev) for _ in range(NB)]
     # the library writes frame f at f * W * my_rows: a short shard renders
@@ -439,6 +456,7 @@ def main():
     gather_cnt = [coll(cnt[0]).new_empty((world, F)) for _ in range(NB)] if root else None
     frames = [torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)] if root else None
     stream = torch.cuda.current_stream(dev)
+    streams = [stream, stream if a.no_overlap else torch.cuda.Stream(dev)]  # buffer set b renders on streams[b]
     post = torch.cuda.Stream(dev) if world > 1 else None  # gather + de-interleave
     shipped = [None] * NB                                 # event: set b's gather and copy done
     mode = a.mode
@@ -446,17 +464,19 @@ def main():
     def render(b, timing=False, count=False):
         # the whole camera orbit in one batched call (the library launches up
         # to 36 frames per walk / fix-up launch)
-        if shipped[b] is not None:
-            stream.wait_event(shipped[b])  # set b's previous gather has read it
-        cnt[b].zero_()
-        # the library's multi-GPU partition (rt_render_shard_device: bands of
-        # 8 rows interleaved over the ranks)
-        scene.render_shard_device(local, cams, W, H, srank, sworld, hit_id=r_ids[b].data_ptr(),
-                                  dist=dists.data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
-                                  stream=stream.cuda_stream, mode=mode, timing=timing, count=count, spp=S)
-        if padded:
-            ids[b][:, :my_rows] = r_ids[b]
-            rgb[b][:, :my_rows] = r_rgb[b]
+        sb = streams[b]
+        with torch.cuda.stream(sb):
+            if shipped[b] is not None:
+                sb.wait_event(shipped[b])  # set b's previous gather has read it
+            cnt[b].zero_()
+            # the library's multi-GPU partition (rt_render_shard_device: bands of
+            # 8 rows interleaved over the ranks)
+            scene.render_shard_device(local, cams, W, H, srank, sworld, hit_id=r_ids[b].data_ptr(),
+                                      dist=dists[b].data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
+                                      stream=sb.cuda_stream, mode=mode, timing=timing, count=count, spp=S)
+            if padded:
+                ids[b][:, :my_rows] = r_ids[b]
+                rgb[b][:, :my_rows] = r_rgb[b]
 
     def ship(b):
         # the step's framebuffers (rgb) and per-frame hit counts
@@ -464,7 +484,7 @@ def main():
         # de-interleaved there (image row j = r * world + rank) into frames[b]
         if world == 1:
             return
-        post.wait_stream(stream)
+        post.wait_stream(streams[b])
         with torch.cuda.stream(post):
             # (rehearsal: the same calls on host copies over gloo)
             w1 = dist.gather(coll(cnt[b]), list(gather_cnt[b].unbind(0)) if root else None, dst=0, async_op=True)
@@ -485,15 +505,6 @@ def main():
     def drain():
         if post is not None:
             stream.wait_stream(post)
-
-    # warm-up with kernel timing on, so the library's per-launch timing events
-    # exist before the timed region (they are recycled, not re-created)
-    ktiming = not os.environ.get("RT_BENCH_NO_KTIMING")
-    for k in range(a.warmup):
-        render_step(k, timing=ktiming)
-    drain()
-    torch.cuda.synchronize(dev)
-    scene.frame_stats(local, reset=True)
 
     # counting pass for algorithmic bytes (outside the timed region)
     render(0, count=True)
@@ -533,6 +544,24 @@ def main():
         trace_bytes = (cs["node_fetches"] * nb + cs["tri_prefilter"] * TRI32_BYTES + cs["tri_tests"] * TRI64_BYTES +
                        cs["chain_nodes"] * CHAIN_BYTES + cs["rays"] * OUT_BYTES)
     alg_bytes_per_frame = trace_bytes / F
+    # warm-up with kernel timing on, so the library's per-launch timing events
+    # exist before the timed region (they are recycled, not re-created): W
+    # steps, then render-only steps (no gather, so ranks may run different
+    # counts) until at least SETTLE_S of continuous GPU work has passed — the
+    # MI355X raises its clock over the first ~25 ms of load (tools/step_trace.py:
+    # 5.58 -> 4.55 ms per step over the first 5 steps), and the timed steps
+    # follow the settle with no idle gap but the barrier
+    ktiming = not os.environ.get("RT_BENCH_NO_KTIMING")
+    settled = 0
+    for k in range(a.warmup):
+        render_step(k, timing=ktiming)
+    drain()
+    t_set = time.perf_counter()
+    while time.perf_counter() - t_set < SETTLE_S:
+        render(settled % NB, timing=ktiming)
+        torch.cuda.synchronize(dev)
+        settled += 1
+    scene.frame_stats(local, reset=True)
 
     if world > 1:
         dist.barrier()
@@ -626,12 +655,13 @@ def main():
             gpu = None
             if S == 1 and sworld == 1 and F <= 36:
                 gpu = {"ids": ids[0][:, :H, :, 0].reshape(F, H * W).cpu().numpy(),
-                       "dist": dists[:, :H, :, 0].reshape(F, H * W).cpu().numpy(),
+                       "dist": dists[0][:, :H, :, 0].reshape(F, H * W).cpu().numpy(),
                        "rgb": rgb[0][:, :H].reshape(F, H * W, 3).cpu().numpy(), "cnt": cnt[0].cpu().numpy()}
             cpu = cpu_baseline(tris, a.algo, a.k, cams, W, H, a.cpu_seconds, gpu=gpu)
         line = {
             "metric": METRIC if S == 1 else METRIC.replace("1spp", f"{S}spp"), "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "warmup": a.warmup, "settle_steps": settled,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32 traversal + f64 exact resolve",
             "data": f"synthetic: {label}",
             "config": {"workload": f"{label}, {W}x{H}x{S}spp primary rays, {a.algo}-{a.k} (BVH{a.k}) k-way, "

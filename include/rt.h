@@ -23,8 +23,16 @@
  *
  * Threading: a scene's geometry is immutable after rt_scene_create.  Any
  * number of host threads may call the render and stats entry points on one
- * scene; the scene's lock serialises the calls that touch its per-device
- * buffers (a caller stream still runs its launches asynchronously).
+ * scene; the scene's lock serialises the host side of the calls (a caller
+ * stream still runs its launches asynchronously).
+ * Device ordering follows the caller's streams: launches issued on one
+ * stream run in order; launches issued on two different streams may run
+ * concurrently on the device (each device replica keeps two sets of launch
+ * state and alternates them), so a caller that issues consecutive batches on
+ * two streams overlaps one batch's tail with the next one's start.  Ordering
+ * between streams that read each other's outputs is the caller's, as for any
+ * HIP work.  Counting passes (RT_FLAG_COUNT) and the modes that use the
+ * replica-wide candidate lists are ordered after every earlier launch.
  * rt_scene_destroy must not race with other calls on the same scene.
  */
 #ifndef RT_MI355X_H

@@ -76,10 +76,36 @@ size_t align_up(size_t x) {
 
 // d_counters: RT_FLAG_COUNT counters (rt_frame_stats)
 constexpr size_t kCounterWords = 24;  // 18-23: RT_PROFILE builds (packet_kernel.h)
+#if defined(RT_PROFILE) && RT_PROFILE
+constexpr bool RT_PROFILE_BUILD = true;  // every timed launch writes the counters
+#else
+constexpr bool RT_PROFILE_BUILD = false;
+#endif
 // Candidate overflow pool: chunks of RT_POOL_CHUNK entries, one per lane whose
 // LDS list overflows in a launch (a dry pool falls back to the certified
 // dropped bound, so the size trades memory against fix-up work only).
 constexpr uint32_t kPoolChunks = 1u << 17;  // 24 MiB
+
+// One set of the device state a batch launch works in: the work-queue block
+// (tile queues, hit-count slots, redo count), the fix-up's redo list, the
+// candidate overflow pool and the per-lane kernels' stack spill.  A replica
+// holds kSlots of them and its launches take them in turn, so a launch waits
+// only for the earlier launch that used the same slot: launches the caller
+// issues on different streams run concurrently (the next launch's waves fill
+// the CUs the last one's tail leaves idle), launches on one
+// stream stay in order.
+constexpr int kSlots = 2;
+struct Slot {
+    uint32_t* d_tiles = nullptr;
+    uint64_t* d_spill = nullptr;
+    uint32_t* d_redo = nullptr;  // packet pipeline -> fix-up kernel pixel list
+    uint64_t redo_cap = 0;
+    uint64_t* d_pool = nullptr;  // candidate overflow pool (pool_chunks x RT_POOL_CHUNK entries)
+    hipStream_t last = nullptr;  // the stream of the slot's last launch
+    bool used = false;
+    bool fresh = true;  // work-queue block known to be zero (packet pipeline self-resets it)
+    hipEvent_t ev = nullptr;
+};
 
 struct Replica {
     int device = -1;
@@ -92,16 +118,12 @@ struct Replica {
     size_t frame_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    // persistent-kernel resources; every launch on this replica is serialised
-    // through `stream` (the work-queue head and the stack spill are shared)
-    uint32_t* d_tiles = nullptr;
-    uint64_t* d_spill = nullptr;
+    // persistent-kernel resources, per launch slot (above)
+    Slot slot[kSlots];
+    int next_slot = 0;
     uint32_t spill_cap = 0;
     int grid = 0;                // per-lane kernels: 256-thread workgroups
     int pgrid = 0;               // packet kernel: 64 * kPacketWaves-thread workgroups
-    uint32_t* d_redo = nullptr;  // packet pipeline -> fix-up kernel pixel list
-    uint64_t redo_cap = 0;
-    uint64_t* d_pool = nullptr;  // candidate overflow pool (pool_chunks x RT_POOL_CHUNK entries)
     uint32_t pool_chunks = 0;
     void* d_cand = nullptr;      // spp > 1 / wavefront paths: candidate lists in HBM
     uint64_t cand_cap = 0;       // pixels
@@ -111,13 +133,7 @@ struct Replica {
     // read and recycled by rt_frame_stats
     std::vector<std::array<hipEvent_t, 2>> tev;
     size_t tev_used = 0;
-    hipEvent_t ev_in = nullptr, ev_out = nullptr;
-    // Launches on a replica are ordered on the caller's stream; only when the
-    // stream changes does the new stream wait for the previous one (no
-    // per-frame cross-stream round trip).
-    hipStream_t last = nullptr;
-    bool used = false;
-    bool fresh = true;  // work-queue block known to be zero (packet pipeline self-resets it)
+    hipEvent_t ev_out = nullptr;
 };
 
 }  // namespace
@@ -219,15 +235,17 @@ void free_replica(Replica& r) {
     if (r.blob) hipFree(r.blob);
     if (r.d_counters) hipFree(r.d_counters);
     if (r.frame) hipFree(r.frame);
-    if (r.d_tiles) hipFree(r.d_tiles);
-    if (r.d_spill) hipFree(r.d_spill);
-    if (r.d_redo) hipFree(r.d_redo);
-    if (r.d_pool) hipFree(r.d_pool);
+    for (Slot& q : r.slot) {
+        if (q.d_tiles) hipFree(q.d_tiles);
+        if (q.d_spill) hipFree(q.d_spill);
+        if (q.d_redo) hipFree(q.d_redo);
+        if (q.d_pool) hipFree(q.d_pool);
+        if (q.ev) hipEventDestroy(q.ev);
+    }
     if (r.d_cand) hipFree(r.d_cand);
     if (r.d_pw) hipFree(r.d_pw);
     for (auto& a : r.tev)
         for (hipEvent_t e : a) hipEventDestroy(e);
-    if (r.ev_in) hipEventDestroy(r.ev_in);
     if (r.ev_out) hipEventDestroy(r.ev_out);
     if (r.ev0) hipEventDestroy(r.ev0);
     if (r.ev1) hipEventDestroy(r.ev1);
@@ -313,7 +331,6 @@ void upload_one(rt_scene* s, int device) {
     HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&r.ev0));
     HIP_TRY(hipEventCreate(&r.ev1));
-    HIP_TRY(hipEventCreateWithFlags(&r.ev_in, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&r.ev_out, hipEventDisableTiming));
     int bpc = rt::exact_blocks_per_cu(f.width, f.stack_bound);
     if (const char* e = std::getenv("RT_BLOCKS_PER_CU")) {  // diagnostic: lower the persistent grid
@@ -324,24 +341,31 @@ void upload_one(rt_scene* s, int device) {
     r.pgrid = prop.multiProcessorCount * rt::packet_blocks_per_cu(f.width);
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
-    HIP_TRY(hipMalloc(&r.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(r.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&r.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
     r.pool_chunks = kPoolChunks;
     if (const char* e = std::getenv("RT_POOL_CHUNKS")) {  // test hook: a small pool runs dry
         const long v = std::atol(e);
         if (v >= 1 && v <= (long)kPoolChunks) r.pool_chunks = (uint32_t)v;
     }
-    HIP_TRY(hipMalloc(&r.d_pool, (size_t)r.pool_chunks * RT_POOL_CHUNK * sizeof(uint64_t)));
+    for (Slot& q : r.slot) {
+        HIP_TRY(hipMalloc(&q.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
+        HIP_TRY(hipMemset(q.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&q.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
+        HIP_TRY(hipMalloc(&q.d_pool, (size_t)r.pool_chunks * RT_POOL_CHUNK * sizeof(uint64_t)));
+        HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+    }
     s->reps.push_back(std::move(rp));
 }
 
-// Waits for every launch issued on the replica so far (before its buffers
-// are replaced): only the replica's last stream, not the whole device.
+// Waits for every launch issued on a slot so far (before its buffers are
+// replaced): only the slot's last stream, not the whole device.
+void quiesce_slot(Slot& q) {
+    if (!q.used) return;
+    HIP_TRY(hipEventRecord(q.ev, q.last));
+    HIP_TRY(hipEventSynchronize(q.ev));
+}
+// ... and on every slot of the replica.
 void quiesce(Replica& r) {
-    if (!r.used) return;
-    HIP_TRY(hipEventRecord(r.ev_out, r.last));
-    HIP_TRY(hipEventSynchronize(r.ev_out));
+    for (Slot& q : r.slot) quiesce_slot(q);
 }
 
 // Redo list: a fixed pool of entries, not one per pose pixel (on the sponza
@@ -355,17 +379,17 @@ uint64_t redo_limit() {
     return v > 0 ? std::min<uint64_t>((uint64_t)v, kRedoEntries) : kRedoEntries;
 }
 
-// Redo list for a launch of `pixels` pose pixels (grown, never shrunk; at
-// most kRedoEntries).
-void ensure_redo(Replica& r, uint64_t pixels) {
+// Redo list of a slot for a launch of `pixels` pose pixels (grown, never
+// shrunk; at most kRedoEntries).
+void ensure_redo(Slot& q, uint64_t pixels) {
     pixels = std::min<uint64_t>(std::max<uint64_t>(pixels, 1), kRedoEntries);
-    if (r.redo_cap >= pixels) return;
-    quiesce(r);
-    if (r.d_redo) HIP_TRY(hipFree(r.d_redo));
-    r.d_redo = nullptr;
-    r.redo_cap = 0;
-    HIP_TRY(hipMalloc(&r.d_redo, pixels * sizeof(uint32_t)));
-    r.redo_cap = pixels;
+    if (q.redo_cap >= pixels) return;
+    quiesce_slot(q);
+    if (q.d_redo) HIP_TRY(hipFree(q.d_redo));
+    q.d_redo = nullptr;
+    q.redo_cap = 0;
+    HIP_TRY(hipMalloc(&q.d_redo, pixels * sizeof(uint32_t)));
+    q.redo_cap = pixels;
 }
 
 // Candidate lists in HBM for `pixels` sample pixels (spp > 1 resolve, the
@@ -494,30 +518,44 @@ int batch_frames() {
     return b;
 }
 
-// Order this launch after every earlier launch on the replica.
-void order_on(Replica& r, hipStream_t st) {
-    if (r.used && r.last != st) {
-        HIP_TRY(hipEventRecord(r.ev_in, r.last));
-        HIP_TRY(hipStreamWaitEvent(st, r.ev_in, 0));
+// The next launch slot of the replica for a launch on stream st, ordered
+// after the slot's earlier launches (a wait only when they were issued on
+// another stream).  shared: the launch also uses the replica-wide buffers
+// (HBM candidate lists, the wavefront workspace, the counting pass's
+// counters), so it follows the launches of every slot.
+Slot& take_slot(Replica& r, hipStream_t st, bool shared) {
+    Slot& q = r.slot[r.next_slot];
+    r.next_slot = (r.next_slot + 1) % kSlots;
+    auto follow = [&](Slot& o) {
+        if (o.used && o.last != st) {
+            HIP_TRY(hipEventRecord(o.ev, o.last));
+            HIP_TRY(hipStreamWaitEvent(st, o.ev, 0));
+        }
+    };
+    if (shared) {
+        for (Slot& o : r.slot) follow(o);
+    } else {
+        follow(q);
     }
-    r.last = st;
-    r.used = true;
+    q.last = st;
+    q.used = true;
+    return q;
 }
 
 // Runs the pipeline and tracks whether its work-queue block is left zeroed.
-void launch(const rt_scene* s, Replica& r, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
+void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
             const hipEvent_t* tev);
 
-RtLaunchAux aux_of(Replica& r) {
+RtLaunchAux aux_of(Replica& r, const Slot& q) {
     RtLaunchAux a{};
-    a.tile_ctr = r.d_tiles;
-    a.spill = r.d_spill;
+    a.tile_ctr = q.d_tiles;
+    a.spill = q.d_spill;
     a.spill_cap = r.spill_cap;
     a.grid = r.grid;
     a.pgrid = r.pgrid;
-    a.redo = r.d_redo;
-    a.redo_cap = std::min<uint64_t>(r.redo_cap, redo_limit());
-    a.pool = r.d_pool;
+    a.redo = q.d_redo;
+    a.redo_cap = std::min<uint64_t>(q.redo_cap, redo_limit());
+    a.pool = q.d_pool;
     a.pool_chunks = r.pool_chunks;
     a.cand = static_cast<uint64_t*>(r.d_cand);
     if (r.d_cand) {
@@ -546,12 +584,12 @@ uint32_t literal_stack_bound(const rt_scene* s) {
     return best + 1;
 }
 
-void launch(const rt_scene* s, Replica& r, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
+void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
             const hipEvent_t* tev) {
     bool fresh_after = false;
     const hipError_t e =
-        rt::launch_trace(r.dev, fp, aux_of(r), mode, count, st, s->literal_stack, tev, r.fresh, &fresh_after);
-    r.fresh = e == hipSuccess && fresh_after;
+        rt::launch_trace(r.dev, fp, aux_of(r, q), mode, count, st, s->literal_stack, tev, q.fresh, &fresh_after);
+    q.fresh = e == hipSuccess && fresh_after;
     HIP_TRY(e);
 }
 
@@ -580,10 +618,12 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
         while (per > 1 && fpix * (uint64_t)(per * spp) * kCandBytesPerPixel > avail / 2) per--;
         ensure_cand(*r, fpix * (uint64_t)(std::min(per, nframes) * spp));
     }
-    ensure_redo(*r, fpix * (uint64_t)std::min(per, nframes));
-    // serialise on the replica's stream: the caller's stream waits for it
-    order_on(*r, st);
+    const bool count = (flags & RT_FLAG_COUNT) != 0;
     for (int f0 = 0; f0 < nframes; f0 += per) {
+        // each launch in the next slot (a batch of more poses than one launch
+        // takes alternates slots too)
+        Slot& q = take_slot(*r, st, split || count || RT_PROFILE_BUILD);
+        ensure_redo(q, fpix * (uint64_t)std::min(per, nframes));
         const int n = std::min(per, nframes - f0);
         RtFrameParams fp = frame_params(s, cams + f0, n, row0, row_stride, nrows, spp, band);
         const uint64_t off = (uint64_t)f0 * fpix, soff = off * (uint64_t)spp;
@@ -606,7 +646,7 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
             }
             tev = r->tev[r->tev_used++].data();
         }
-        launch(s, *r, fp, mode, (flags & RT_FLAG_COUNT) != 0, st, tev);
+        launch(s, *r, q, fp, mode, count, st, tev);
     }
 }
 
@@ -767,7 +807,6 @@ void render_group(rt_scene* s, const rt_camera* cams, int nframes, int spp, int 
     HIP_TRY(hipEventRecord(gp.ev1, r0.stream));
     HIP_TRY(hipEventRecord(gp.ev_out, r0.stream));
     HIP_TRY(hipStreamWaitEvent(st0, gp.ev_out, 0));
-    order_on(r0, st0);  // later single-device launches on the first device follow the group
 }
 
 }  // namespace
@@ -1110,14 +1149,15 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows;
             ensure_cand(*r, P);  // candidate lists, stride P
             const PathWs ws = ensure_pw(*r, P);
-            order_on(*r, st);
+            Slot& q = take_slot(*r, st, true);
             HIP_TRY(hipMemsetAsync(ws.ctl, 0, 16 * sizeof(uint32_t), st));
-            e = rt::launch_paths_wf(r->dev, fp, aux_of(*r), ws, (uint32_t)frame, bounces, st, tev);
+            e = rt::launch_paths_wf(r->dev, fp, aux_of(*r, q), ws, (uint32_t)frame, bounces, st, tev);
+            q.fresh = false;  // the work queue is left dirty: the next packet launch clears it
         } else {
-            order_on(*r, st);
-            e = rt::launch_paths(r->dev, fp, aux_of(*r), (uint32_t)frame, bounces, st, tev);
+            Slot& q = take_slot(*r, st, (flags & RT_FLAG_COUNT) != 0);
+            e = rt::launch_paths(r->dev, fp, aux_of(*r, q), (uint32_t)frame, bounces, st, tev);
+            q.fresh = false;
         }
-        r->fresh = false;  // the work queue is left dirty: the next packet launch clears it
         HIP_TRY(e);
         return RT_OK;
     } catch (const rt::Error& e) {
@@ -1159,7 +1199,6 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         d.pos = out->pos ? reinterpret_cast<double*>(base + o_pos) : nullptr;
         d.rgb = reinterpret_cast<uint8_t*>(base + o_rgb);  // always shaded (shadeScreen)
         d.hit_count = reinterpret_cast<unsigned long long*>(base + o_cnt);
-        order_on(r, r.stream);
         HIP_TRY(hipMemsetAsync(d.hit_count, 0, 8, r.stream));
         RtFrameParams fp = frame_params(s, cam, 1, 0, 1, cam->height);
         fp.hit_id = d.hit_id;
@@ -1176,11 +1215,12 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
             e0 = s->grp.ev0;
             e1 = s->grp.ev1;
         } else {
-            ensure_redo(r, npx);
-            if (mode == RT_MODE_EXACT && rt::packet_split(1, false)) ensure_cand(r, npx);
-            order_on(r, r.stream);
+            const bool split = mode == RT_MODE_EXACT && rt::packet_split(1, false);
+            if (split) ensure_cand(r, npx);
+            Slot& q = take_slot(r, r.stream, split);
+            ensure_redo(q, npx);
             HIP_TRY(hipEventRecord(r.ev0, r.stream));
-            launch(s, r, fp, mode, false, r.stream, nullptr);
+            launch(s, r, q, fp, mode, false, r.stream, nullptr);
             HIP_TRY(hipEventRecord(r.ev1, r.stream));
         }
         if (out->hit_id) HIP_TRY(hipMemcpyAsync(out->hit_id, d.hit_id, npx * 4, hipMemcpyDeviceToHost, r.stream));

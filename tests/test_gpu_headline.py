@@ -97,6 +97,45 @@ def test_headline_orbit_full_size_matches_oracle(oracle, monkeypatch, rays):
           f"redo {fs['redo_rays']} (chain {fs['redo_chain']}) of {fs['rays']} rays")
 
 
+@pytest.mark.parametrize("shard_of", [1, 8])
+def test_consecutive_launches_on_two_streams_equal_one_stream(shard_of):
+    """bench.py's overlapped steps: consecutive orbit renders issued on two
+    streams (the library alternates its two launch slots, so launch k + 1
+    runs while launch k drains) into two buffer sets, hit counts zeroed on
+    each stream before its render; every set equals the one-stream render bit
+    for bit (hit ids, distances, PPM bytes, per-pose hit counts), also at the
+    per-GPU size of an 8-GPU run (shard 0 of 8)."""
+    tris, s = proxy()
+    cams = orbit(tris)
+    R = rt.shard_height(H, shard_of, 0) if shard_of > 1 else H
+    F = len(cams)
+
+    def bufs():
+        return (torch.empty((F, R, W), dtype=torch.int32, device="cuda:0"),
+                torch.empty((F, R, W), dtype=torch.float64, device="cuda:0"),
+                torch.empty((F, R, W, 3), dtype=torch.uint8, device="cuda:0"),
+                torch.zeros(F, dtype=torch.int64, device="cuda:0"))
+
+    def render(b, st):
+        with torch.cuda.stream(st):
+            b[3].zero_()
+            s.render_shard_device(0, cams, W, H, 0, shard_of, hit_id=b[0].data_ptr(), dist=b[1].data_ptr(),
+                                  rgb=b[2].data_ptr(), hit_count=b[3].data_ptr(), stream=st.cuda_stream)
+
+    ref = bufs()
+    render(ref, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    sets = [bufs(), bufs()]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for k in range(6):
+        render(sets[k % 2], streams[k % 2])
+    torch.cuda.synchronize()
+    for b in sets:
+        for x, y in zip(b, ref):
+            assert torch.equal(x, y)
+    assert int(ref[3].sum()) > 0
+
+
 def test_config_c4_spp4_full_frames_match_oracle(oracle):
     """Config c4 (2x2 stratified samples) on full 1080p frames of 6 poses (one
     launch of 24 sample frames: each sample resolved in the walk kernel,
@@ -152,6 +191,16 @@ def test_overflow_pool_and_dry_pool(oracle, monkeypatch, chunks):
     assert fs["dropped_rays"] > 0
     if chunks:
         assert fs["spilled_rays"] == 1  # the one chunk; every other lane dropped straight away
+    # the same frame from two streams at once: the two launch slots each have
+    # their own pool, redo list and work queue
+    outs = [torch.empty(96 * 72, dtype=torch.int32, device="cuda:0") for _ in range(2)]
+    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for k in range(4):
+        s.render_rows_device(0, [0.0, 0.0, 3.0], [0.0, 0.0, -1.0], 96, 72, 0, 1, 72, hit_id=outs[k % 2].data_ptr(),
+                             stream=sts[k % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for o2 in outs:
+        assert torch.equal(o2, ids)
     # 4 spp through the fused resolve: samples that overflow or cannot be
     # certified send their whole pixel to k_fixup via k_average
     sp = torch.empty(96 * 72 * 4, dtype=torch.int32, device="cuda:0")

@@ -27,6 +27,7 @@ for s in $STEPS; do
         tests) run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
         bench) run bench 600 python bench.py ;;
         quick) run bench_quick 300 python bench.py --no-cpu --steps 10 ;;
+        frames) for f in 4 9 36; do run bench_f$f 300 python bench.py --no-cpu --no-dropin --steps 20 --frames $f || exit 1; done ;;
         split) RT_RESOLVE=split run bench_split 300 python bench.py --no-cpu --steps 10 ;;
         shard8) run bench_shard8 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of 8 ;;
         shards) for n in 2 4 8; do run bench_shard$n 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of $n || exit 1; done ;;
@@ -50,7 +51,7 @@ for s in $STEPS; do
         paths0) RT_PATHS_PRIMARY=0 run bench_paths0 300 python bench.py --paths --no-cpu --steps 3 --warmup 1 ;;
         paths) run bench_paths 300 python bench.py --paths --steps 3 --warmup 1 ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
-                   -- python bench.py --steps 3 --warmup 1 --no-cpu --no-dropin ;;
+                   -- python bench.py --steps 10 --warmup 2 --no-cpu --no-dropin ;;
         pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
                    -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin --key-out gpurun_out/pmc_key.txt && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \
@@ -118,6 +119,16 @@ for s in $STEPS; do
                run hdiv 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
                    SQ_BUSY_CYCLES --output-format csv -d gpurun_out/hdiv -o head \
                    -- python bench.py --steps 1 --warmup 0 --no-cpu --no-dropin ;;
+        ovl)   # consecutive steps on two streams (default) vs one (--no-overlap): full size and shard of 8
+               i=0
+               for o in "" --no-overlap "" --no-overlap; do i=$((i+1))
+                   for sh in 1 8; do
+                       timeout -k 10 200 python bench.py --no-cpu --no-dropin --steps 40 --shard-of $sh $o \
+                           > gpurun_out/ovl${i}_s$sh.log 2>&1
+                       rc=$?; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/ovl${i}_s$sh.log; exit $rc; }
+                       python -c "import json; l=[x for x in open('gpurun_out/ovl${i}_s$sh.log') if x.startswith('{')][-1]; d=json.loads(l); print('RESULT', 'shard-of $sh', '$o', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'], d['settle_steps'])" || true
+                   done
+               done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

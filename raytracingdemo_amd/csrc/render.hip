@@ -834,7 +834,11 @@ constexpr int kPathStack = RT_PATHS_STACK;  // path kernel: LDS ring entries per
 constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (4 B each)
 constexpr int kCandidates = RT_CAND_LDS;  // packet kernel: LDS candidate list entries per lane (8 B each)
 static_assert(RT_PW_K <= RT_CAND_LDS, "wavefront walk lists share the candidate buffers");
-constexpr int kFixupGrid = 256;    // k_fixup blocks (the redo list is short)
+// k_fixup blocks: the redo list is short (~0 entries on the sponza proxy), and
+// 32 blocks (32 KB of LDS each) start on the first CUs the launch frees, while
+// the next launch on the other stream fills the rest (256 blocks: -1.2% at
+// the per-GPU size of 8 GPUs)
+constexpr int kFixupGrid = 32;
 
 // Rays per lane of the spp = 1 packet kernel: 1 (8x8 tiles, k_trace_packet)
 // or 2 (16x8 tiles, k_trace_packet_r).  RT_PACKET_RAYS, read per call.
@@ -908,7 +912,9 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     // rest of the pipeline is timed as frame minus traversal by the caller)
     if (ev) (void)hipEventRecord(ev[0], s);
     if (use_packet(sc.stack_bound)) {
-        const dim3 fgrid((unsigned)(aux.grid < kFixupGrid ? aux.grid : kFixupGrid));
+        int fg = kFixupGrid;
+        if (const char* e = getenv("RT_FIXUP_GRID")) fg = atoi(e) > 0 ? atoi(e) : fg;  // tuning hook, read per call
+        const dim3 fgrid((unsigned)(aux.grid < fg ? aux.grid : fg));
         if (!split_resolve(fp.spp)) {
             // packed samples (fp.pack, 8-wide walk trees) in their own
             // instantiation: its epilogue's registers stay out of spp = 1's

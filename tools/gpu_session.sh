@@ -93,7 +93,7 @@ for s in $STEPS; do
                i=0; IFS=';' read -ra cfgs <<< "${AB_ENVS:-}"
                for c in "${cfgs[@]}"; do i=$((i+1))
                    echo "--- ab$i: $c"
-                   env $c timeout -k 10 300 python bench.py --no-cpu --no-dropin --steps 10 > gpurun_out/ab$i.log 2>&1
+                   env $c timeout -k 10 300 python bench.py --no-cpu --no-dropin --steps ${AB_STEPS:-20} --shard-of ${AB_SHARD:-1} > gpurun_out/ab$i.log 2>&1
                    rc=$?; echo "ab$i exit=$rc"; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/ab$i.log; exit $rc; }
                    python -c "import json; l=[x for x in open('gpurun_out/ab$i.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']; q=r['per_ray']; print('RESULT', '$c', d['value'], r['kernel_ms_avg'], q['wave_nodes_per_tile'], q['wave_leaves_per_tile'], q['wave_tris_per_tile'], q['tri_tests_fp64'])" || true
                done ;;

@@ -377,7 +377,12 @@ def main():
         if rehearse:
             dist.init_process_group("gloo")
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            # the gathers run on a high-priority RCCL stream: the persistent
+            # render grid holds every CU's wave slots, and a collective's
+            # workgroups should take the first ones a launch frees
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=dev, pg_options=opts)
     coll = (lambda t: t.cpu()) if rehearse else (lambda t: t)  # collective-side tensors
 
     if a.scene == "armadillo":
@@ -452,19 +457,45 @@ def main():
     # rank 0's gather buffers, allocated once: [world, F, rows, W, 3], and the
     # de-interleaved frames [F, H, W, 3] (the step's framebuffers) and counts
     root = world > 1 and rank == 0
-    gather_rgb = [coll(rgb[0]).new_empty((world,) + tuple(rgb[0].shape)) for _ in range(NB)] if root else None
+    # diagnostic (RT_BENCH_SHIP_SIM=1 with --shard-of N at one process): rank
+    # 0's side of the gather on this one GPU — the N shards' rgb copied into
+    # the gather buffer on the side stream, then the de-interleave — to see
+    # whether side-stream work keeps pace with the overlapped renders
+    # (=1: every shard copied by rank 0's CUs; =2: only its own shard, the
+    # peers' shards written over xGMI by their senders, as RCCL's P2P
+    # transport does; =3: no de-interleave either)
+    ship_sim = int(os.environ.get("RT_BENCH_SHIP_SIM", "0")) if world == 1 and sworld > 1 else 0
+    ng = sworld if ship_sim else world
+    gather_rgb = [coll(rgb[0]).new_empty((ng,) + tuple(rgb[0].shape)) for _ in range(NB)] if root or ship_sim else None
     gather_cnt = [coll(cnt[0]).new_empty((world, F)) for _ in range(NB)] if root else None
-    frames = [torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)] if root else None
+    frames = ([torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
+              if root or ship_sim else None)
     stream = torch.cuda.current_stream(dev)
     streams = [stream, stream if a.no_overlap else torch.cuda.Stream(dev)]  # buffer set b renders on streams[b]
-    post = torch.cuda.Stream(dev) if world > 1 else None  # gather + de-interleave
+    post = torch.cuda.Stream(dev, priority=-1) if world > 1 or ship_sim else None  # gather + de-interleave
     shipped = [None] * NB                                 # event: set b's gather and copy done
+    # Rank 0 de-interleaves step k's gathered shards inside the render of step
+    # k + 2 (the next render into the same buffer set, which waits for that
+    # gather anyway): the render's traversal waves copy the rows between their
+    # tiles (rt_render_shard_device_job), where a separate kernel would wait
+    # for the persistent grid to drain and then hold the GPU (RT_BENCH_SHIP_SIM
+    # on one GPU: -10% at the per-GPU size of 8 GPUs).  pending[b]: set b's
+    # gathered shards are not de-interleaved yet; the timed region ends after
+    # the last ones are.  RT_BENCH_FUSED_DEINT=0: a de-interleave kernel per step.
+    fused_deint = os.environ.get("RT_BENCH_FUSED_DEINT", "1") != "0" and not rehearse
+    pending = [False] * NB
     mode = a.mode
 
     def render(b, timing=False, count=False):
         # the whole camera orbit in one batched call (the library launches up
         # to 36 frames per walk / fix-up launch)
         sb = streams[b]
+        job = None
+        if pending[b]:
+            job = dict(gathered=gather_rgb[b].data_ptr(), block_bytes=F * rows * W * 3, section_offset=0,
+                       shards=gather_rgb[b].shape[0], frames=F, height=H, width=W, elem_bytes=3, frame_rows=rows,
+                       frames_out=frames[b].data_ptr())
+            pending[b] = False
         with torch.cuda.stream(sb):
             if shipped[b] is not None:
                 sb.wait_event(shipped[b])  # set b's previous gather has read it
@@ -473,7 +504,7 @@ def main():
             # 8 rows interleaved over the ranks)
             scene.render_shard_device(local, cams, W, H, srank, sworld, hit_id=r_ids[b].data_ptr(),
                                       dist=dists[b].data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
-                                      stream=sb.cuda_stream, mode=mode, timing=timing, count=count, spp=S)
+                                      stream=sb.cuda_stream, mode=mode, timing=timing, count=count, spp=S, job=job)
             if padded:
                 ids[b][:, :my_rows] = r_ids[b]
                 rgb[b][:, :my_rows] = r_rgb[b]
@@ -482,6 +513,19 @@ def main():
         # the step's framebuffers (rgb) and per-frame hit counts
         # to rank 0 with RCCL, issued on a side stream after the render, and
         # de-interleaved there (image row j = r * world + rank) into frames[b]
+        if ship_sim:
+            post.wait_stream(streams[b])
+            with torch.cuda.stream(post):
+                for g in range(sworld if ship_sim == 1 else 1):
+                    gather_rgb[b][g].copy_(rgb[b])
+                if ship_sim != 3 and fused_deint:
+                    pending[b] = True
+                elif ship_sim != 3:
+                    deinterleave_into(gather_rgb[b], H, frames[b])
+                ev = torch.cuda.Event()
+                ev.record(post)
+            shipped[b] = ev
+            return
         if world == 1:
             return
         post.wait_stream(streams[b])
@@ -491,7 +535,9 @@ def main():
             w2 = dist.gather(coll(rgb[b]), list(gather_rgb[b].unbind(0)) if root else None, dst=0, async_op=True)
             w1.wait()
             w2.wait()
-            if root:
+            if root and fused_deint:
+                pending[b] = True  # de-interleaved by the render of step k + 2 (or drain())
+            elif root:
                 deinterleave_into(gather_rgb[b], H, frames[b])
             ev = torch.cuda.Event()
             ev.record(post)
@@ -504,6 +550,11 @@ def main():
 
     def drain():
         if post is not None:
+            with torch.cuda.stream(post):
+                for b in range(NB):
+                    if pending[b]:
+                        deinterleave_into(gather_rgb[b], H, frames[b])
+                        pending[b] = False
             stream.wait_stream(post)
 
     # counting pass for algorithmic bytes (outside the timed region)
@@ -669,6 +720,7 @@ def main():
                        "width": W, "height": H, "spp": S, "bvh": f"{a.algo}-{a.k}", "frames_per_step": F,
                        "triangles": int(st["triangles"]), "mode": mode,
                        **({"diagnostic_shard_of": sworld} if sworld != world else {}),
+                       **({"diagnostic_ship_sim": ship_sim} if ship_sim else {}),
                        "parallelism": f"8-row image bands interleaved x{world}" +
                                       (" + RCCL gather of rgb (overlapped)" if world > 1 else ""),
                        **({"gather_verified": verified} if world > 1 else {}),

@@ -234,6 +234,35 @@ int rt_render_frame(rt_scene *s, const rt_camera *cam, int mode, rt_frame_out *o
 int rt_render_shard_device(rt_scene *s, int device, const rt_camera *cams, int nframes, int spp, int mode, int shard,
                            int nshards, const rt_device_out *out, void *stream, uint32_t flags);
 
+/* A de-interleave of gathered shards into full frames, done by the traversal
+ * kernel of a render on the side (rank 0 of a one-process-per-GPU driver:
+ * the previous step's gathered framebuffers, while this step renders).
+ * `gathered` holds `shards` blocks of block_bytes; image row j of frame f
+ * comes from shard g = (j / 8) % shards, row r = ((j / 8) / shards) * 8 + j % 8
+ * of it, at g * block_bytes + section_offset + (f * rows + r) * width *
+ * elem_bytes, rows = frame_rows, or rt_shard_height(height, shards, g) when
+ * frame_rows is 0 (rt_render_batch_multi's own layout).  Writes
+ * frames_out[frames][height][width] elements of elem_bytes.  The caller
+ * orders the gather that fills `gathered` before the render, and keeps both
+ * buffers alive until the render is done. */
+typedef struct rt_deinterleave_job {
+    const void *gathered;
+    uint64_t block_bytes;
+    uint64_t section_offset;
+    int shards, frames, height, width, elem_bytes;
+    int frame_rows;
+    void *frames_out;
+} rt_deinterleave_job;
+
+/* rt_render_shard_device plus a de-interleave job (NULL: none) that the
+ * render's persistent traversal waves carry out between and after their
+ * tiles — memory-bound copies beside the latency-bound walk — instead of a
+ * separate kernel that waits for the render's grid to drain.
+ * Pipelines whose kernel does not take the job run it after the render. */
+int rt_render_shard_device_job(rt_scene *s, int device, const rt_camera *cams, int nframes, int spp, int mode,
+                               int shard, int nshards, const rt_device_out *out, const rt_deinterleave_job *job,
+                               void *stream, uint32_t flags);
+
 /* Rows of shard `shard` of `nshards` of an image `height` rows high (-1 on bad
  * arguments). */
 int rt_shard_height(int height, int nshards, int shard);

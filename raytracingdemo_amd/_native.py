@@ -35,7 +35,7 @@ EXPORTS = [
     "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_render_paths_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
     "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
     "rt_render_batch_multi", "rt_deinterleave_rows", "rt_scene_create_on_device", "rt_scene_build_times",
-    "rt_render_shard_device", "rt_shard_height",
+    "rt_render_shard_device", "rt_shard_height", "rt_render_shard_device_job",
 ]
 
 
@@ -60,6 +60,12 @@ class rt_frame_out(C.Structure):
 class rt_device_out(C.Structure):
     _fields_ = [("hit_id", C.c_void_p), ("dist", C.c_void_p), ("pos", C.c_void_p), ("rgb", C.c_void_p),
                 ("hit_count", C.c_void_p)]
+
+
+class rt_deinterleave_job(C.Structure):
+    _fields_ = [("gathered", C.c_void_p), ("block_bytes", C.c_uint64), ("section_offset", C.c_uint64),
+                ("shards", C.c_int), ("frames", C.c_int), ("height", C.c_int), ("width", C.c_int),
+                ("elem_bytes", C.c_int), ("frame_rows", C.c_int), ("frames_out", C.c_void_p)]
 
 
 class rt_scene_stats_t(C.Structure):
@@ -146,6 +152,10 @@ def lib() -> C.CDLL:
                                          C.c_int, C.c_int, C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
     L.rt_render_shard_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_int, C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]
+    if hasattr(L, "rt_render_shard_device_job"):  # (RT_LIB tuning builds of earlier sources may lack it)
+        L.rt_render_shard_device_job.argtypes = [C.c_void_p, C.c_int, C.POINTER(rt_camera), C.c_int, C.c_int,
+                                                 C.c_int, C.c_int, C.c_int, C.POINTER(rt_device_out),
+                                                 C.POINTER(rt_deinterleave_job), C.c_void_p, C.c_uint32]
     L.rt_shard_height.argtypes = [C.c_int, C.c_int, C.c_int]
     L.rt_render_batch_multi.argtypes = [C.c_void_p, C.POINTER(rt_camera), C.c_int, C.c_int, C.c_int,
                                         C.POINTER(rt_device_out), C.c_void_p, C.c_uint32]

@@ -1016,6 +1016,52 @@ constexpr int kPacketWaves = RT_PACKET_WAVES;
 #define RT_PACKET_ATTR
 #endif
 
+// One row of the launch's side de-interleave job (RtLaunchAux::job_*, rank 0
+// of a one-process-per-GPU driver: the previous step's gathered shards into
+// full frames): row c of the [F][H] frames, 16 B per lane per access when
+// both sides allow it.  The copy is memory-bound and the walk is not, so a
+// wave that takes a row after a tile (and the waves whose tiles have run
+// out) move the frames while the other waves trace, in place of a separate
+// kernel that would wait for the persistent grid to drain.
+__device__ __forceinline__ void side_copy_row(const RtLaunchAux& a, uint32_t c, int lane) {
+    const uint32_t f = c / (uint32_t)a.job_H, j = c - f * (uint32_t)a.job_H;
+    const uint64_t n = (uint64_t)a.job_W * (uint64_t)a.job_eb;
+    const RT_G uint8_t* src = a.job_src + rt_job_src_row(a, (int)j, (int)f);
+    RT_G uint8_t* dst = a.job_dst + ((uint64_t)f * (uint64_t)a.job_H + j) * n;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if ((((uintptr_t)src | (uintptr_t)dst | n) & 15u) == 0) {
+        const RT_G u32x4* s4 = reinterpret_cast<const RT_G u32x4*>(src);
+        RT_G u32x4* d4 = reinterpret_cast<RT_G u32x4*>(dst);
+        const uint32_t n16 = (uint32_t)(n / 16);
+        for (uint32_t k0 = 0; k0 < n16; k0 += 4 * 64) {
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
+                v[u] = k < n16 ? s4[k] : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
+                if (k < n16) out_store(d4 + k, v[u]);
+            }
+        }
+    } else {
+        for (uint64_t k = (uint64_t)lane; k < n; k += 64) out_store(dst + k, src[k]);
+    }
+}
+// Claims and copies one row of the side job; false once every row is taken.
+__device__ __forceinline__ bool side_copy(args_p A, int lane) {
+    A = launder(A);
+    const RtLaunchAux a = kload(&A->aux);
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(a.tile_ctr + RT_COPY_COUNT, 1u);
+    c = __builtin_amdgcn_readfirstlane(c);
+    if (c >= (uint32_t)a.job_F * (uint32_t)a.job_H) return false;
+    side_copy_row(a, c, lane);
+    return true;
+}
+
 template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK = false>
 __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_packet(PacketArgs args) {
     __shared__ uint32_t stacks[kPacketWaves][SP];
@@ -1046,6 +1092,7 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     uint32_t hacc = 0;
     int hf = -1;
     const uint32_t hslot = (blockIdx.x * kPacketWaves + (uint32_t)wv) % RT_HIT_SLOTS;
+    bool job = kload(&A->aux.job_src) != nullptr;  // rows of the side job may be left
     for (;;) {
         A = launder(A);
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
@@ -1082,7 +1129,10 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             pend = tile + RT_QUEUES;
             pend_n = 1;
         }
-        if (tile >= tiles) break;
+        if (tile >= tiles) {
+            while (job) job = side_copy(A, lane);  // the job's rows the tiles left
+            break;
+        }
         const int fr = tile / tiles_f;  // frame of the batch (pose when packed)
         const int ft = tile - fr * tiles_f;
         const int ty = ft / tiles_x, tx = ft - ty * tiles_x;
@@ -1114,6 +1164,7 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             }
             hacc += h;
         }
+        if (job) job = side_copy(A, lane);  // one row of the side job per tile
     }
     if (FUSED && hacc != 0 && lane == 0)
         atomicAdd(kload(&launder(A)->aux.tile_ctr) + RT_HIT_BASE + (hf * RT_HIT_SLOTS + hslot) * RT_QUEUE_STRIDE,

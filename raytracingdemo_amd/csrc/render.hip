@@ -696,6 +696,7 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
         }
         if (tid < RT_QUEUES) aux.tile_ctr[tid * RT_QUEUE_STRIDE] = 0;
         if (tid == 0) aux.tile_ctr[RT_POOL_COUNT] = 0;
+        if (tid == 0) aux.tile_ctr[RT_COPY_COUNT] = 0;
         __syncthreads();
         if (!retry && fp.hit_count && tid < poses && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
     }
@@ -1018,6 +1019,7 @@ hipError_t launch_literal_s(const RtDevScene& sc, const RtFrameParams& fp, bool 
 }  // namespace
 
 namespace rt {
+hipError_t launch_job(const RtLaunchAux& a, hipStream_t s);
 
 // Blocks per CU the persistent exact kernel is launched with.
 int exact_blocks_per_cu(int width, uint32_t stack_bound) {
@@ -1054,8 +1056,32 @@ uint32_t params_bytes() { return (uint32_t)sizeof(RtFrameParams); }
 // fresh: the work-queue block is known to be zero (no memset needed);
 // *fresh_after: whether it will be zero again once this launch completes
 // (the packet pipeline clears it itself; the per-lane kernel does not).
+hipError_t launch_trace_core(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode,
+                             bool count, hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh,
+                             bool* fresh_after);
+
+// The kernels that take the side job (aux.job_*) themselves: the packet
+// kernel of 8x8 tiles in every resolve placement.  Otherwise it runs after
+// the pipeline as k_deinterleave.
+bool packet_takes_job(const RtDevScene& sc, const RtFrameParams& fp, int mode) {
+    if (mode == 1 || !use_packet(sc.stack_bound)) return false;
+    return !(sc.width == 8 && !split_resolve(fp.spp) && !fp.pack && fp.spp == 1 && packet_rays() == 2);
+}
+
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
                         hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after) {
+    const bool empty = fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0;
+    const bool own = aux.job_src && (empty || !packet_takes_job(sc, fp, mode));
+    RtLaunchAux a = aux;
+    if (own) a.job_src = nullptr;
+    hipError_t e = launch_trace_core(sc, fp, a, mode, count, s, literal_stack, ev, fresh, fresh_after);
+    if (e == hipSuccess && own) e = launch_job(aux, s);
+    return e;
+}
+
+hipError_t launch_trace_core(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode,
+                             bool count, hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh,
+                             bool* fresh_after) {
     *fresh_after = fresh;
     if (fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0) return hipSuccess;
     if (fp.nframes > RT_MAX_BATCH || fp.spp < 1 || fp.nframes % fp.spp != 0 ||
@@ -1105,14 +1131,13 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 // bytes) become full frames.  One block per image row of a frame copies the
 // row's W * eb bytes from its shard (rt_gathered_row), in words when both
 // sides allow it.
-__global__ void __launch_bounds__(256) k_deinterleave(const uint8_t* __restrict__ gather, uint64_t block,
-                                                      uint64_t sec_off, int G, int F, int H, int W, int eb,
-                                                      uint8_t* __restrict__ dst) {
+__global__ void __launch_bounds__(256) k_deinterleave(RtLaunchAux a) {
+    const int H = a.job_H;
     const int f = (int)(blockIdx.x / (unsigned)H), j = (int)(blockIdx.x % (unsigned)H);
-    if (f >= F) return;
-    const uint64_t n = (uint64_t)W * eb;
-    const uint8_t* src = gather + rt_gathered_row(j, f, G, H, W, eb, block, sec_off);
-    uint8_t* d = dst + ((uint64_t)f * H + j) * n;
+    if (f >= a.job_F) return;
+    const uint64_t n = (uint64_t)a.job_W * a.job_eb;
+    const uint8_t* src = a.job_src + rt_job_src_row(a, j, f);
+    uint8_t* d = a.job_dst + ((uint64_t)f * H + j) * n;
     if (((uintptr_t)src | (uintptr_t)d | n) % 4 == 0) {
         const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
         uint32_t* d4 = reinterpret_cast<uint32_t*>(d);
@@ -1135,10 +1160,24 @@ __global__ void k_sum_counts(const uint8_t* __restrict__ gather, uint64_t block,
 
 hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_off, int G, int F, int H, int W,
                                int eb, void* dst, hipStream_t s) {
-    if (F <= 0 || H <= 0 || W <= 0 || G <= 0 || eb <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)((uint64_t)F * H)), dim3(256), 0, s,
-                       static_cast<const uint8_t*>(gather), block, sec_off, G, F, H, W, eb,
-                       static_cast<uint8_t*>(dst));
+    RtLaunchAux a{};
+    a.job_src = (decltype(a.job_src))gather;
+    a.job_dst = (decltype(a.job_dst))dst;
+    a.job_block = block;
+    a.job_sec = sec_off;
+    a.job_G = G;
+    a.job_F = F;
+    a.job_H = H;
+    a.job_W = W;
+    a.job_eb = eb;
+    a.job_rows = 0;
+    return launch_job(a, s);
+}
+
+// A side job on its own (the pipelines whose kernel does not take it).
+hipError_t launch_job(const RtLaunchAux& a, hipStream_t s) {
+    if (!a.job_src || a.job_F <= 0 || a.job_H <= 0 || a.job_W <= 0 || a.job_G <= 0 || a.job_eb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)((uint64_t)a.job_F * a.job_H)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

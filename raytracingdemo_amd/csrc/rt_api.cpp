@@ -39,6 +39,7 @@ hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_
                                int eb, void* dst, hipStream_t s);
 hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_off, int G, int F,
                              unsigned long long* out, hipStream_t s);
+hipError_t launch_job(const RtLaunchAux& a, hipStream_t s);
 }
 
 namespace {
@@ -544,7 +545,22 @@ Slot& take_slot(Replica& r, hipStream_t st, bool shared) {
 
 // Runs the pipeline and tracks whether its work-queue block is left zeroed.
 void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
-            const hipEvent_t* tev);
+            const hipEvent_t* tev, const rt_deinterleave_job* job = nullptr);
+
+// A side de-interleave job (include/rt.h) in the launch's aux block.
+void set_job(RtLaunchAux& a, const rt_deinterleave_job* j) {
+    if (!j || j->frames <= 0) return;
+    a.job_src = static_cast<const uint8_t*>(j->gathered);
+    a.job_dst = static_cast<uint8_t*>(j->frames_out);
+    a.job_block = j->block_bytes;
+    a.job_sec = j->section_offset;
+    a.job_G = j->shards;
+    a.job_F = j->frames;
+    a.job_H = j->height;
+    a.job_W = j->width;
+    a.job_eb = j->elem_bytes;
+    a.job_rows = j->frame_rows;
+}
 
 RtLaunchAux aux_of(Replica& r, const Slot& q) {
     RtLaunchAux a{};
@@ -585,10 +601,11 @@ uint32_t literal_stack_bound(const rt_scene* s) {
 }
 
 void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
-            const hipEvent_t* tev) {
+            const hipEvent_t* tev, const rt_deinterleave_job* job) {
     bool fresh_after = false;
-    const hipError_t e =
-        rt::launch_trace(r.dev, fp, aux_of(r, q), mode, count, st, s->literal_stack, tev, q.fresh, &fresh_after);
+    RtLaunchAux a = aux_of(r, q);
+    set_job(a, job);
+    const hipError_t e = rt::launch_trace(r.dev, fp, a, mode, count, st, s->literal_stack, tev, q.fresh, &fresh_after);
     q.fresh = e == hipSuccess && fresh_after;
     HIP_TRY(e);
 }
@@ -598,7 +615,7 @@ void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int
 // batch_frames() sample frames per launch.
 void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nframes, int spp, int mode, int row0,
                          int row_stride, int nrows, const rt_device_out* out, hipStream_t st, uint32_t flags,
-                         int band = 1) {
+                         int band = 1, const rt_deinterleave_job* job = nullptr) {
     Replica* r = &rr;
     const rt_camera* cam = &cams[0];
     const uint64_t fpix = (uint64_t)cam->width * (uint64_t)nrows;  // pixels per frame
@@ -646,7 +663,7 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
             }
             tev = r->tev[r->tev_used++].data();
         }
-        launch(s, *r, q, fp, mode, count, st, tev);
+        launch(s, *r, q, fp, mode, count, st, tev, f0 == 0 ? job : nullptr);  // (the job rides the first launch)
     }
 }
 
@@ -1068,6 +1085,18 @@ int rt_render_batch_multi(rt_scene* s, const rt_camera* cams, int nframes, int s
 
 int rt_render_shard_device(rt_scene* s, int device, const rt_camera* cams, int nframes, int spp, int mode, int shard,
                            int nshards, const rt_device_out* out, void* stream, uint32_t flags) {
+    return rt_render_shard_device_job(s, device, cams, nframes, spp, mode, shard, nshards, out, nullptr, stream, flags);
+}
+
+int rt_render_shard_device_job(rt_scene* s, int device, const rt_camera* cams, int nframes, int spp, int mode,
+                               int shard, int nshards, const rt_device_out* out, const rt_deinterleave_job* job,
+                               void* stream, uint32_t flags) {
+    if (job && job->frames > 0 &&
+        (!job->gathered || !job->frames_out || job->shards < 1 || job->height < 1 || job->width < 1 ||
+         job->elem_bytes < 1 || job->frame_rows < 0 ||
+         (job->frame_rows > 0 && job->frame_rows < rt_shard_rows(job->height, job->shards, 0)) ||
+         (uint64_t)job->frames * (uint64_t)job->height >= (1ull << 32)))
+        return fail(RT_ERR_INVALID_ARGUMENT, "bad de-interleave job");
     if (!s || !out || (nframes > 0 && !cams)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     if (nframes < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative frame count");
     if (spp < 1 || spp > RT_MAX_BATCH || spp_grid(spp) * spp_grid(spp) != spp)
@@ -1080,14 +1109,20 @@ int rt_render_shard_device(rt_scene* s, int device, const rt_camera* cams, int n
             if (cams[f].width != cams[0].width || cams[f].height != cams[0].height)
                 return fail(RT_ERR_INVALID_ARGUMENT, "frames of a batch must share the image size");
         }
-        if (nframes == 0) return RT_OK;
-        const int nrows = rt_shard_rows(cams[0].height, nshards, shard);
-        if (nrows == 0) return RT_OK;
+        const int nrows = nframes > 0 ? rt_shard_rows(cams[0].height, nshards, shard) : 0;
         std::lock_guard<std::mutex> lk(s->mu);
         Replica* r = &replica_for(s, device);
         DevGuard g(device);
+        if (nframes == 0 || nrows == 0) {  // nothing to render: the job on its own
+            if (job && job->frames > 0) {
+                RtLaunchAux a{};
+                set_job(a, job);
+                HIP_TRY(rt::launch_job(a, (hipStream_t)stream));
+            }
+            return RT_OK;
+        }
         render_batch_locked(s, *r, cams, nframes, spp, mode, shard, nshards, nrows, out, (hipStream_t)stream, flags,
-                            RT_SHARD_BAND);
+                            RT_SHARD_BAND, job);
         return RT_OK;
     } catch (const rt::Error& e) {
         return fail(e.status, e.msg);

@@ -47,6 +47,8 @@
 #define RT_POOL_COUNT (RT_REDO_COUNT + RT_QUEUE_STRIDE)
 // k_fixup blocks that have read the redo count (the last one clears it)
 #define RT_FIXUP_DONE (RT_REDO_COUNT + 2 * RT_QUEUE_STRIDE)
+// rows of the side de-interleave job (RtLaunchAux::job_*) claimed so far
+#define RT_COPY_COUNT (RT_REDO_COUNT + 3 * RT_QUEUE_STRIDE)
 // then, per frame of the launch, RT_HIT_SLOTS hit-count partial sums
 // RT_QUEUE_STRIDE words apart (frame f's slot s at RT_HIT_BASE + (f *
 // RT_HIT_SLOTS + s) * RT_QUEUE_STRIDE)
@@ -178,7 +180,26 @@ struct RtLaunchAux {
     uint64_t cand_cap;         // pixels the candidate buffers hold
     RT_G float* cand_drop;     // per pixel: smallest t bound of a dropped candidate (if flagged)
     RT_G uint32_t* cand_ovf;   // per pixel: its overflow pool chunk (if flagged)
+    // A de-interleave done on the side (include/rt.h rt_deinterleave_job):
+    // the packet kernel's waves copy its rows between and after their tiles.
+    // Row j of frame f comes from shard g = (j / RT_SHARD_BAND) % job_G of
+    // the gathered [job_G][job_block] buffer (job_rows rows per frame in each
+    // block, 0: rt_shard_rows, the library's own group layout).  job_src NULL:
+    // no job.
+    RT_G const uint8_t* job_src;
+    RT_G uint8_t* job_dst;
+    uint64_t job_block, job_sec;
+    int32_t job_G, job_F, job_H, job_W, job_eb, job_rows;
 };
+// Byte offsets of row j of frame f of a side job: in the gathered buffer and
+// in the frames [F][H][W][eb].
+static inline RT_HD uint64_t rt_job_src_row(const RtLaunchAux& a, int j, int f) {
+    if (a.job_rows <= 0) return rt_gathered_row(j, f, a.job_G, a.job_H, a.job_W, a.job_eb, a.job_block, a.job_sec);
+    const int b = j / RT_SHARD_BAND, g = b % a.job_G;
+    const int r = (b / a.job_G) * RT_SHARD_BAND + j % RT_SHARD_BAND;
+    return (uint64_t)g * a.job_block + a.job_sec +
+           ((uint64_t)f * (uint64_t)a.job_rows + (uint64_t)r) * (uint64_t)a.job_W * (uint64_t)a.job_eb;
+}
 
 // One camera pose of a launch (Camera, camera.hpp:20-38: position, view
 // direction and the basis main.cpp:325-329 derives from it).

@@ -66,16 +66,36 @@ def deinterleave(gathered, H: int, band: int = BAND):
     return stack.index_select(1, _index(H, world, rows, gathered.device, band))
 
 
-def deinterleave_into(gathered, H: int, out, band: int = BAND):
-    """deinterleave() written into `out` ([F, H, W, ...]) with one gather kernel."""
-    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
-    rest = tuple(gathered.shape[3:])
-    stack = gathered.transpose(0, 1).reshape((F, world * rows) + rest)
+_FLAT: dict = {}
+
+
+def _flat_index(H: int, world: int, F: int, rows: int, device, band: int):
+    """For every (frame f, image row j), f-major: the row of the gathered
+    [world, F, rows] block that holds it, (g F + f) rows + r for source row
+    g rows + r (source_rows) — so the de-interleave is one row gather of the
+    gathered buffer as it lies, without first transposing it."""
     import torch
+    key = (H, world, F, rows, str(device), band)
+    if key not in _FLAT:
+        src = _index(H, world, rows, device, band)
+        g, r = src // rows, src % rows
+        f = torch.arange(F, dtype=torch.long, device=device)[:, None]
+        _FLAT[key] = ((g[None, :] * F + f) * rows + r[None, :]).reshape(-1)
+    return _FLAT[key]
+
+
+def deinterleave_into(gathered, H: int, out, band: int = BAND):
+    """deinterleave() written into `out` ([F, H, W, ...]) with one row-gather
+    kernel straight from the gathered [world, F, rows, W, ...] buffer (one
+    read and one write of the frames)."""
+    world, F, rows = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+    import torch
+    flat = gathered.reshape((world * F * rows, -1))
+    idx = _flat_index(H, world, F, rows, gathered.device, band)
     if out.device != gathered.device:  # (host-side gathers: one copy across)
-        out.copy_(stack.index_select(1, _index(H, world, rows, gathered.device, band)))
+        out.copy_(flat.index_select(0, idx).reshape(out.shape))
     else:
-        torch.index_select(stack, 1, _index(H, world, rows, gathered.device, band), out=out)
+        torch.index_select(flat, 0, idx, out=out.view(F * H, -1))
     return out
 
 

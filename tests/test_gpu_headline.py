@@ -136,6 +136,50 @@ def test_consecutive_launches_on_two_streams_equal_one_stream(shard_of):
     assert int(ref[3].sum()) > 0
 
 
+@pytest.mark.parametrize("env", [{}, {"RT_PACKET_RAYS": "2"}, {"RT_RESOLVE": "split"}])
+def test_render_with_side_deinterleave_job(monkeypatch, env):
+    """rt_render_shard_device_job: the shard render's traversal waves also
+    de-interleave a gathered buffer into full frames (bench.py's rank 0).
+    Random bytes laid out as 8 padded shards of [F][rows][W][3] (frame_rows =
+    rows) and as the library's compact group layout (frame_rows = 0) must come
+    out as shards.deinterleave's frames, while the render itself still equals
+    the plain call; with RT_PACKET_RAYS=2 the job runs as its own kernel."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from raytracingdemo_amd.shards import deinterleave, rows_per_rank
+    tris, s = proxy()
+    cams = orbit(tris, 6)
+    F, G = len(cams), 8
+    R = rt.shard_height(H, G, 3)
+    rows = rows_per_rank(H, G)
+    g = torch.randint(0, 256, (G, F, rows, W, 3), dtype=torch.uint8, device="cuda:0")
+    want = deinterleave(g, H)
+    # the library's group layout: shard k holds rt_shard_height rows per frame
+    blocks = [g[k, :, :rt.shard_height(H, G, k)].contiguous().reshape(-1) for k in range(G)]
+    blk = max(b.numel() for b in blocks)
+    compact = torch.zeros((G, blk), dtype=torch.uint8, device="cuda:0")
+    for k in range(G):
+        compact[k, :blocks[k].numel()] = blocks[k]
+    ref_ids = torch.empty((F, R, W), dtype=torch.int32, device="cuda:0")
+    st = torch.cuda.current_stream()
+    s.render_shard_device(0, cams, W, H, 3, G, hit_id=ref_ids.data_ptr(), stream=st.cuda_stream)
+    for gathered, block, frows in ((g, F * rows * W * 3, rows), (compact, blk, 0)):
+        out = torch.zeros((F, H, W, 3), dtype=torch.uint8, device="cuda:0")
+        ids = torch.empty((F, R, W), dtype=torch.int32, device="cuda:0")
+        job = dict(gathered=gathered.data_ptr(), block_bytes=block, section_offset=0, shards=G, frames=F, height=H,
+                   width=W, elem_bytes=3, frame_rows=frows, frames_out=out.data_ptr())
+        s.render_shard_device(0, cams, W, H, 3, G, hit_id=ids.data_ptr(), stream=st.cuda_stream, job=job)
+        torch.cuda.synchronize()
+        assert torch.equal(out, want), frows
+        assert torch.equal(ids, ref_ids), frows
+    # nothing to render: the job alone
+    out = torch.zeros((F, H, W, 3), dtype=torch.uint8, device="cuda:0")
+    job["gathered"], job["block_bytes"], job["frame_rows"], job["frames_out"] = g.data_ptr(), F * rows * W * 3, rows, out.data_ptr()
+    s.render_shard_device(0, [], W, H, 3, G, stream=st.cuda_stream, job=job)
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)
+
+
 def test_config_c4_spp4_full_frames_match_oracle(oracle):
     """Config c4 (2x2 stratified samples) on full 1080p frames of 6 poses (one
     launch of 24 sample frames: each sample resolved in the walk kernel,

@@ -1033,15 +1033,16 @@ __device__ __forceinline__ void side_copy_row(const RtLaunchAux& a, uint32_t c, 
         const RT_G u32x4* s4 = reinterpret_cast<const RT_G u32x4*>(src);
         RT_G u32x4* d4 = reinterpret_cast<RT_G u32x4*>(dst);
         const uint32_t n16 = (uint32_t)(n / 16);
-        for (uint32_t k0 = 0; k0 < n16; k0 += 4 * 64) {
-            u32x4 v[4];
+        // (6 x 1 KB per round trip: a 1920-pixel rgb row in one)
+        for (uint32_t k0 = 0; k0 < n16; k0 += 6 * 64) {
+            u32x4 v[6];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 6; u++) {
                 const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
                 v[u] = k < n16 ? s4[k] : u32x4{0u, 0u, 0u, 0u};
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < 6; u++) {
                 const uint32_t k = k0 + (uint32_t)(u * 64 + lane);
                 if (k < n16) out_store(d4 + k, v[u]);
             }
@@ -1050,19 +1051,22 @@ __device__ __forceinline__ void side_copy_row(const RtLaunchAux& a, uint32_t c, 
         for (uint64_t k = (uint64_t)lane; k < n; k += 64) out_store(dst + k, src[k]);
     }
 }
-// Claims and copies one row of the side job; false once every row is taken.
-__device__ __forceinline__ bool side_copy(args_p A, int lane) {
+// Claims and copies one row of the side job from the wave's XCD queue xq
+// (rows xq, xq + RT_QUEUES, ...); false once the queue's rows are taken.
+__device__ __forceinline__ bool side_copy(args_p A, int lane, uint32_t xq) {
     A = launder(A);
     const RtLaunchAux a = kload(&A->aux);
     uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(a.tile_ctr + RT_COPY_COUNT, 1u);
+    if (lane == 0) c = xq + RT_QUEUES * atomicAdd(a.tile_ctr + RT_COPY_BASE + xq * RT_QUEUE_STRIDE, 1u);
     c = __builtin_amdgcn_readfirstlane(c);
     if (c >= (uint32_t)a.job_F * (uint32_t)a.job_H) return false;
     side_copy_row(a, c, lane);
     return true;
 }
 
-template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK = false>
+// JOB: the launch carries a side de-interleave job (RtLaunchAux::job_*; its
+// own instantiation, so the kernels without one keep their registers).
+template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK = false, bool JOB = false>
 __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_packet(PacketArgs args) {
     __shared__ uint32_t stacks[kPacketWaves][SP];
     __shared__ uint2 cands[kPacketWaves][K * 64];
@@ -1092,7 +1096,7 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     uint32_t hacc = 0;
     int hf = -1;
     const uint32_t hslot = (blockIdx.x * kPacketWaves + (uint32_t)wv) % RT_HIT_SLOTS;
-    bool job = kload(&A->aux.job_src) != nullptr;  // rows of the side job may be left
+    bool job = JOB;  // rows of the side job may be left
     for (;;) {
         A = launder(A);
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
@@ -1130,7 +1134,8 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             pend_n = 1;
         }
         if (tile >= tiles) {
-            while (job) job = side_copy(A, lane);  // the job's rows the tiles left
+            if constexpr (JOB)
+                while (job) job = side_copy(A, lane, xq);  // the job's rows the tiles left
             break;
         }
         const int fr = tile / tiles_f;  // frame of the batch (pose when packed)
@@ -1164,7 +1169,8 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             }
             hacc += h;
         }
-        if (job) job = side_copy(A, lane);  // one row of the side job per tile
+        if constexpr (JOB)
+            if (job) job = side_copy(A, lane, xq);  // one row of the side job per tile
     }
     if (FUSED && hacc != 0 && lane == 0)
         atomicAdd(kload(&launder(A)->aux.tile_ctr) + RT_HIT_BASE + (hf * RT_HIT_SLOTS + hslot) * RT_QUEUE_STRIDE,

@@ -696,7 +696,7 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
         }
         if (tid < RT_QUEUES) aux.tile_ctr[tid * RT_QUEUE_STRIDE] = 0;
         if (tid == 0) aux.tile_ctr[RT_POOL_COUNT] = 0;
-        if (tid == 0) aux.tile_ctr[RT_COPY_COUNT] = 0;
+        if (tid < RT_QUEUES) aux.tile_ctr[RT_COPY_BASE + tid * RT_QUEUE_STRIDE] = 0;
         __syncthreads();
         if (!retry && fp.hit_count && tid < poses && frame_sum[tid]) atomicAdd(fp.hit_count + tid, frame_sum[tid]);
     }
@@ -921,7 +921,15 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
             // instantiation: its epilogue's registers stay out of spp = 1's
             bool packed = false;
             if constexpr (W == 8) {
-                if (fp.pack) {
+                if (aux.job_src) {  // (packet_takes_job: fused, not counting, 8 x 8 tiles or packed samples)
+                    packed = true;
+                    if (fp.pack)
+                        hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true, true, true>),
+                                           pgrid, pblk, 0, s, PacketArgs{sc, fp, aux});
+                    else
+                        hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, false, true, false, true>),
+                                           pgrid, pblk, 0, s, PacketArgs{sc, fp, aux});
+                } else if (fp.pack) {
                     packed = true;
                     if (count)
                         hipLaunchKernelGGL((k_trace_packet<W, kPacketStack, kCandidates, true, true, true>), pgrid,
@@ -1060,18 +1068,20 @@ hipError_t launch_trace_core(const RtDevScene& sc, const RtFrameParams& fp, cons
                              bool count, hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh,
                              bool* fresh_after);
 
-// The kernels that take the side job (aux.job_*) themselves: the packet
-// kernel of 8x8 tiles in every resolve placement.  Otherwise it runs after
+// The kernels that take the side job (aux.job_*) themselves: the fused
+// packet kernel on 8-wide trees, 8x8 tiles or packed samples, outside the
+// counting pass (k_trace_packet<..., JOB = true>).  Otherwise it runs after
 // the pipeline as k_deinterleave.
-bool packet_takes_job(const RtDevScene& sc, const RtFrameParams& fp, int mode) {
-    if (mode == 1 || !use_packet(sc.stack_bound)) return false;
-    return !(sc.width == 8 && !split_resolve(fp.spp) && !fp.pack && fp.spp == 1 && packet_rays() == 2);
+bool packet_takes_job(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count) {
+    if (mode == 1 || count || !use_packet(sc.stack_bound) || sc.width != 8 || split_resolve(fp.spp)) return false;
+    if (fp.pack) return true;
+    return fp.spp == 1 && packet_rays() == 1;
 }
 
 hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, int mode, bool count,
                         hipStream_t s, uint32_t literal_stack, const hipEvent_t* ev, bool fresh, bool* fresh_after) {
     const bool empty = fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0;
-    const bool own = aux.job_src && (empty || !packet_takes_job(sc, fp, mode));
+    const bool own = aux.job_src && (empty || !packet_takes_job(sc, fp, mode, count));
     RtLaunchAux a = aux;
     if (own) a.job_src = nullptr;
     hipError_t e = launch_trace_core(sc, fp, a, mode, count, s, literal_stack, ev, fresh, fresh_after);

@@ -47,8 +47,10 @@
 #define RT_POOL_COUNT (RT_REDO_COUNT + RT_QUEUE_STRIDE)
 // k_fixup blocks that have read the redo count (the last one clears it)
 #define RT_FIXUP_DONE (RT_REDO_COUNT + 2 * RT_QUEUE_STRIDE)
-// rows of the side de-interleave job (RtLaunchAux::job_*) claimed so far
-#define RT_COPY_COUNT (RT_REDO_COUNT + 3 * RT_QUEUE_STRIDE)
+// rows of the side de-interleave job (RtLaunchAux::job_*) claimed so far,
+// one counter per XCD queue (queue x takes rows x, x + RT_QUEUES, ...: a
+// counter shared by all XCDs would serialise on cross-XCD atomics)
+#define RT_COPY_BASE 256
 // then, per frame of the launch, RT_HIT_SLOTS hit-count partial sums
 // RT_QUEUE_STRIDE words apart (frame f's slot s at RT_HIT_BASE + (f *
 // RT_HIT_SLOTS + s) * RT_QUEUE_STRIDE)

@@ -447,8 +447,14 @@ def main():
     ids = [torch.empty((F, rows, W, S), dtype=torch.int32, device=dev) for _ in range(NB)]
     # per-sample hit distance |hit - o| (stack_bvh.hpp:631), written in the timed region
     dists = [torch.empty((F, my_rows, W, S), dtype=torch.float64, device=dev) for _ in range(NB)]
-    rgb = [torch.zeros((F, rows, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
-    cnt = [torch.zeros((F,), dtype=torch.int64, device=dev) for _ in range(NB)]
+    # a step's payload per buffer set: the rgb frames, then the per-frame hit
+    # counts (8-B aligned), so that a step ships with ONE collective
+    rgb_bytes = F * rows * W * 3
+    cnt_off = (rgb_bytes + 7) // 8 * 8
+    pay_bytes = cnt_off + F * 8
+    pay = [torch.zeros(pay_bytes, dtype=torch.uint8, device=dev) for _ in range(NB)]
+    rgb = [p[:rgb_bytes].view(F, rows, W, 3) for p in pay]
+    cnt = [p[cnt_off:].view(torch.int64) for p in pay]
     # the library writes frame f at f * W * my_rows: a short shard renders
     # into contiguous buffers and is copied into the padded gather layout
     padded = my_rows != rows
@@ -466,8 +472,11 @@ def main():
     # transport does; =3: no de-interleave either)
     ship_sim = int(os.environ.get("RT_BENCH_SHIP_SIM", "0")) if world == 1 and sworld > 1 else 0
     ng = sworld if ship_sim else world
-    gather_rgb = [coll(rgb[0]).new_empty((ng,) + tuple(rgb[0].shape)) for _ in range(NB)] if root or ship_sim else None
-    gather_cnt = [coll(cnt[0]).new_empty((world, F)) for _ in range(NB)] if root else None
+    # rank 0's gathered payloads [ng, pay_bytes], seen as rgb [ng, F, rows, W, 3]
+    # and counts [ng, F]
+    gather_pay = [coll(pay[0]).new_empty((ng, pay_bytes)) for _ in range(NB)] if root or ship_sim else None
+    gather_rgb = [g[:, :rgb_bytes].view(ng, F, rows, W, 3) for g in gather_pay] if gather_pay else None
+    gather_cnt = [g[:, cnt_off:].view(torch.int64) for g in gather_pay] if gather_pay else None
     frames = ([torch.empty((F, H, W, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
               if root or ship_sim else None)
     stream = torch.cuda.current_stream(dev)
@@ -492,9 +501,7 @@ def main():
         sb = streams[b]
         job = None
         if pending[b]:
-            job = dict(gathered=gather_rgb[b].data_ptr(), block_bytes=F * rows * W * 3, section_offset=0,
-                       shards=gather_rgb[b].shape[0], frames=F, height=H, width=W, elem_bytes=3, frame_rows=rows,
-                       frames_out=frames[b].data_ptr())
+            job = deint_job(b)
             pending[b] = False
         with torch.cuda.stream(sb):
             if shipped[b] is not None:
@@ -509,6 +516,20 @@ def main():
                 ids[b][:, :my_rows] = r_ids[b]
                 rgb[b][:, :my_rows] = r_rgb[b]
 
+    def deint_job(b):
+        # rank 0's de-interleave of set b's gathered payloads into frames[b]
+        # (include/rt.h rt_deinterleave_job: block = one rank's payload)
+        return dict(gathered=gather_pay[b].data_ptr(), block_bytes=pay_bytes, section_offset=0, shards=ng, frames=F,
+                    height=H, width=W, elem_bytes=3, frame_rows=rows, frames_out=frames[b].data_ptr())
+
+    def deinterleave_now(b, st):
+        # the same de-interleave as its own kernel on stream st (the library's
+        # job with nothing to render), or on the host copies of a rehearsal
+        if gather_pay[b].is_cuda:
+            scene.render_shard_device(local, [], W, H, 0, 1, stream=st.cuda_stream, job=deint_job(b))
+        else:
+            deinterleave_into(gather_rgb[b], H, frames[b])
+
     def ship(b):
         # the step's framebuffers (rgb) and per-frame hit counts
         # to rank 0 with RCCL, issued on a side stream after the render, and
@@ -517,11 +538,11 @@ def main():
             post.wait_stream(streams[b])
             with torch.cuda.stream(post):
                 for g in range(sworld if ship_sim == 1 else 1):
-                    gather_rgb[b][g].copy_(rgb[b])
+                    gather_pay[b][g].copy_(pay[b])
                 if ship_sim != 3 and fused_deint:
                     pending[b] = True
                 elif ship_sim != 3:
-                    deinterleave_into(gather_rgb[b], H, frames[b])
+                    deinterleave_now(b, post)
                 ev = torch.cuda.Event()
                 ev.record(post)
             shipped[b] = ev
@@ -530,15 +551,13 @@ def main():
             return
         post.wait_stream(streams[b])
         with torch.cuda.stream(post):
-            # (rehearsal: the same calls on host copies over gloo)
-            w1 = dist.gather(coll(cnt[b]), list(gather_cnt[b].unbind(0)) if root else None, dst=0, async_op=True)
-            w2 = dist.gather(coll(rgb[b]), list(gather_rgb[b].unbind(0)) if root else None, dst=0, async_op=True)
-            w1.wait()
-            w2.wait()
+            # (rehearsal: the same call on host copies over gloo)
+            w = dist.gather(coll(pay[b]), list(gather_pay[b].unbind(0)) if root else None, dst=0, async_op=True)
+            w.wait()
             if root and fused_deint:
                 pending[b] = True  # de-interleaved by the render of step k + 2 (or drain())
             elif root:
-                deinterleave_into(gather_rgb[b], H, frames[b])
+                deinterleave_now(b, post)
             ev = torch.cuda.Event()
             ev.record(post)
         shipped[b] = ev
@@ -553,7 +572,7 @@ def main():
             with torch.cuda.stream(post):
                 for b in range(NB):
                     if pending[b]:
-                        deinterleave_into(gather_rgb[b], H, frames[b])
+                        deinterleave_now(b, post)
                         pending[b] = False
             stream.wait_stream(post)
 

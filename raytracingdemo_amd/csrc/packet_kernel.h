@@ -143,6 +143,16 @@ constexpr bool kSpecWin = RT_SPEC_WIN != 0;
 #ifndef RT_PIN_REC
 #define RT_PIN_REC 1
 #endif
+// Wave priority (s_setprio) outside the walk: a wave's tile epilogue (the
+// fp64 resolve, shading, stores), the next tile's claim and its ray set-up
+// run at RT_EPI_PRIO, the walk at 0, so the SIMD's arbiter issues those
+// phases ahead of the other waves' node steps.  One box, two pairs: 17.09 /
+// 17.10 vs 16.65 / 16.71 Grays/s (+2.5%); the resolve alone raised (to the
+// next tile's start): +1.4% at levels 1-3; the walk raised instead: -3.7%
+// (DESIGN.md §7).  0: off.
+#ifndef RT_EPI_PRIO
+#define RT_EPI_PRIO 2
+#endif
 __device__ __forceinline__ void pin_rec(const ChildRec& r) {
     if constexpr (RT_PIN_REC)
         asm volatile("" ::"s"(r.lx), "s"(r.hx), "s"(r.ly), "s"(r.hy), "s"(r.lz), "s"(r.hz), "s"(r.ref), "s"(r.pad));
@@ -646,6 +656,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
             cur = uni(wstack[sp]);
         }
     };
+    if constexpr (RT_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(0);  // the walk at the lowest priority
     switch (oct) {
         case 0: walk.template operator()<0>(); break;
         case 1: walk.template operator()<1>(); break;
@@ -657,6 +668,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         case 7: walk.template operator()<7>(); break;
         default: walk.template operator()<-1>(); break;
     }
+    if constexpr (RT_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(RT_EPI_PRIO);  // epilogue, claim, next set-up
     uint64_t p2 = 0;
     if constexpr (kProfile) {
         p2 = prof_clock();

@@ -543,11 +543,6 @@ __device__ __forceinline__ int resolve_cands(const RtDevScene& sc, const Ray64& 
     return 1;
 }
 
-// RT_PATHS_PRIO (tuning): the per-lane walk at wave priority 0, the rest of
-// a segment (resolve, shading, bounce, set-up) at this priority
-#ifndef RT_PATHS_PRIO
-#define RT_PATHS_PRIO 0
-#endif
 template <int W, int S, int K, bool COUNT, bool QN = false, class RayFn>
 __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S>& st,
                                               uint2 (*cand)[256], LaneCounts& lc) {
@@ -561,9 +556,7 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
     float tcull;
     int nc;
     bool over;
-    if constexpr (RT_PATHS_PRIO > 0) __builtin_amdgcn_s_setprio(0);  // the walk lowest (packet_kernel.h RT_EPI_PRIO)
     lane_walk<W, S, K, COUNT, QN>(sc, q, tsl, st, cand, lc, tcull, nc, over);
-    if constexpr (RT_PATHS_PRIO > 0) __builtin_amdgcn_s_setprio(RT_PATHS_PRIO);
     if (over) return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 0, lc);
     Win best;
     const int tid = st.tid;

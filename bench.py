@@ -380,8 +380,11 @@ def main():
             # the gathers run on a high-priority RCCL stream: the persistent
             # render grid holds every CU's wave slots, and a collective's
             # workgroups should take the first ones a launch frees
-            opts = dist.ProcessGroupNCCL.Options()
-            opts.is_high_priority_stream = True
+            try:
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+            except (AttributeError, RuntimeError):  # (a build without the option: default streams)
+                opts = None
             dist.init_process_group("nccl", device_id=dev, pg_options=opts)
     coll = (lambda t: t.cpu()) if rehearse else (lambda t: t)  # collective-side tensors
 

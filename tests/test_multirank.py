@@ -104,6 +104,32 @@ def test_deinterleave_single_process():
         assert torch.equal(deinterleave_into(sh, H, torch.empty_like(full)), full)
 
 
+def test_deinterleave_from_combined_payloads():
+    """bench.py ships one payload per rank and step — the rgb frames, then the
+    per-frame hit counts 8-B aligned — and rank 0 de-interleaves the rgb part
+    of the gathered [world, payload] buffer as a strided view (the host path
+    of a rehearsal; on the GPU the same layout is the library's de-interleave
+    job with block_bytes = payload)."""
+    H, W, F = 37, 6, 3
+    full = torch.randint(0, 256, (F, H, W, 3), dtype=torch.uint8)
+    for world in (1, 2, 3, 8):
+        rows = rows_per_rank(H, world)
+        rgb_bytes = F * rows * W * 3
+        cnt_off = (rgb_bytes + 7) // 8 * 8
+        pay_bytes = cnt_off + F * 8
+        g = torch.zeros((world, pay_bytes), dtype=torch.uint8)
+        for r in range(world):
+            idx = shard_rows(r, world, H)
+            shard = torch.zeros((F, rows, W, 3), dtype=torch.uint8)
+            shard[:, :len(idx)] = full[:, idx]
+            g[r, :rgb_bytes] = shard.reshape(-1)
+            g[r, cnt_off:].view(torch.int64)[:] = torch.arange(F) + 100 * r
+        view = g[:, :rgb_bytes].view(world, F, rows, W, 3)
+        assert torch.equal(deinterleave_into(view, H, torch.empty_like(full)), full)
+        cnt = g[:, cnt_off:].view(torch.int64)
+        assert torch.equal(cnt.sum(0), world * torch.arange(F) + 100 * sum(range(world)))
+
+
 def test_python_shards_match_the_library_layout():
     """shards.py (bench.py's partition) and the library's rt_shard_height /
     rt_deinterleave_rows (rt_render_shard_device's layout) agree."""

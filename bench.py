@@ -703,7 +703,7 @@ def main():
 
     if rank == 0:
         key = (f"{label}|{W}x{H}|{a.algo}-{a.k}|{mode}|n{world}|fpl{frames_per_launch:g}" + (f"|spp{S}" if S > 1 else "")
-               + ("|fused" if fused else ""))
+               + ("|fused" if fused else "") + (f"|shard-of{sworld}" if sworld != world else ""))
         if a.key_out:
             with open(a.key_out, "w") as fh:
                 fh.write(key + "\n")

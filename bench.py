@@ -81,6 +81,8 @@ def parse():
     p.add_argument("--paths", action="store_true",
                    help="config c5: diffuse path tracing (secondary rays), 16 spp x (1 + 4 bounces) by default")
     p.add_argument("--bounces", type=int, default=4, help="paths: secondary bounces per sample")
+    p.add_argument("--no-shadow", action="store_true",
+                   help="paths: no occlusion rays toward the head-light at the bounce vertices (RT_FLAG_SHADOW)")
     p.add_argument("--scene", default="sponza", choices=["sponza", "armadillo"],
                    help="sponza: configs c4/c5 (the headline; proxy unless RT_SPONZA_OBJ); "
                         "armadillo: config c3 (needs RT_ARMADILLO_OBJ, the geometry is stripped from the reference)")
@@ -204,6 +206,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
     from raytracingdemo_amd.shards import gather_frames, rows_per_rank, shard_rows
 
     W, H, S, B, F = a.width, a.height, a.spp, a.bounces, a.frames
+    shadow = not a.no_shadow
     path = rt.CameraPath(rt.scene_center(tris), 36)
     rows = rows_per_rank(H, world, band=1)  # the paths kernel takes single interleaved rows
     my_rows = len(shard_rows(rank, world, H, band=1))
@@ -217,7 +220,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
         for f in range(F):
             scene.render_paths_device(local, pos, d, W, H, rank, world, my_rows, frame=k % 36, spp=S, bounces=B,
                                       rgb=rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
-                                      timing=timing, count=count)
+                                      timing=timing, count=count, shadow=shadow)
 
     def step(k, timing=False, count=False):
         render(k, timing=timing, count=count)
@@ -272,8 +275,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu:
-            cpu = paths_cpu_baseline(tris, a, path, W, H, S, B)
-        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|paths|spp{S}|b{B}|n{world}"
+            cpu = paths_cpu_baseline(tris, a, path, W, H, S, B, shadow)
+        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|paths|spp{S}|b{B}|n{world}" + ("|shadow" if shadow else "")
         if a.key_out:
             with open(a.key_out, "w") as fh:
                 fh.write(key + "\n")
@@ -293,12 +296,18 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
             "scaling": "strong", "vs_baseline": None, "dtype": "f32 traversal + f64 exact hits",
             "data": f"synthetic: {label}",
             "config": {"workload": f"{label}, {W}x{H}x{S}spp, 1 + {B} bounce segments per sample, diffuse paths, "
-                                   f"{a.algo}-{a.k} reference tree, SAH walk tree, {F} pose(s) per step",
+                                   f"{a.algo}-{a.k} reference tree, SAH walk tree, {F} pose(s) per step"
+                                   + (", one head-light occlusion ray per bounce vertex" if shadow else ""),
                        "width": W, "height": H, "spp": S, "bounces": B, "frames_per_step": F,
                        "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else ""),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "segments_traced_per_s_M": round(segs_per_pose * a.steps * F / elapsed / 1e6, 2),
             "segments_per_sample": round(segs_per_pose / (W * H * S), 3),
+            "shadow": {"on": shadow, "rays_per_pose": round(cs["shadow_rays"] / F),
+                       "occluded_per_pose": round(cs["shadow_occluded"] / F),
+                       "rays_per_sample": round(cs["shadow_rays"] / F / (W * my_rows * S), 3),
+                       "note": "one occlusion ray toward the head-light per bounce vertex (RT_FLAG_SHADOW); not "
+                               "counted in value's nominal W*H*spp*(1+bounces)"},
             "kernel_ms_avg": round(ks["trace_ms"] / max(ks["timed_launches"], 1), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_paths",
@@ -317,7 +326,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
         dist.destroy_process_group()
 
 
-def paths_cpu_baseline(tris, a, path, W, H, S, B):
+def paths_cpu_baseline(tris, a, path, W, H, S, B, shadow=True):
     """The oracle's path tracer (the reference has none: kind "port") on host
     cores over whole rows of the same pose until ~cpu_seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -332,7 +341,7 @@ def paths_cpu_baseline(tris, a, path, W, H, S, B):
         n = max(1, nthreads // 4)  # whole rows per call, spread over the image
         while spent < budget_s and rows < H:
             t0 = time.perf_counter()
-            b.render_paths(pos, d, W, H, 0, S, B, row0=j, nrows=min(n, H - j), threads=nthreads)
+            b.render_paths(pos, d, W, H, 0, S, B, row0=j, nrows=min(n, H - j), threads=nthreads, shadow=shadow)
             spent += time.perf_counter() - t0
             rows += min(n, H - j)
             j = (j + 97 * n) % (H - n)

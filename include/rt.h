@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* status codes */
 #define RT_OK 0
@@ -68,6 +68,8 @@ extern "C" {
 #define RT_FLAG_COUNT 1u  /* also count node/triangle fetches (rt_frame_stats) */
 #define RT_FLAG_TIMING 2u /* time the pipeline kernels with HIP events on the
                              launching stream (rt_frame_stats)              */
+#define RT_FLAG_SHADOW 4u /* rt_render_paths_device: one occlusion ray toward the
+                             head-light from every bounce vertex            */
 
 #define RT_MISS 0xFFFFFFFFu
 
@@ -146,7 +148,9 @@ typedef struct {
                                 tested, counted once per wave (distinct over its
                                 lanes; tri_tests counts them per lane)     */
     uint64_t wave_winners;   /*   winners' shading records, once per wave  */
-    uint64_t reserved[7];
+    uint64_t shadow_rays;    /* paths with RT_FLAG_SHADOW: occlusion rays cast  */
+    uint64_t shadow_occluded;/*   of which occluded                            */
+    uint64_t reserved[5];
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */

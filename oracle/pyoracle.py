@@ -118,7 +118,7 @@ class Oracle(_Lib):
                                      _i32p, _dp, _dp, _u8p]
         L.orc_render_spp.restype = C.c_longlong
         L.orc_render_paths.argtypes = [C.c_void_p, _dp, _dp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                       C.c_int, C.c_int, _i32p, _dp, _dp, _u8p]
+                                       C.c_int, C.c_int, C.c_int, _i32p, _dp, _dp, _u8p, _i64p]
         L.orc_render_paths.restype = C.c_longlong
         L.orc_max_threads.restype = C.c_int
 
@@ -200,22 +200,26 @@ class OracleBVH:
 
 
     def render_paths(self, cam_pos, cam_dir, W: int, H: int, frame: int, spp: int, bounces: int, row0: int = 0,
-                     nrows: int | None = None, threads: int = 0):
+                     nrows: int | None = None, threads: int = 0, shadow: bool = False):
         """Diffuse paths (orc_render_paths): rgb per pixel, primary id / pos /
-        dist per sample."""
+        dist per sample; shadow: head-light occlusion rays at the bounce
+        vertices (shadow_cast / shadow_occluded counts)."""
         nrows = H - row0 if nrows is None else nrows
         n = W * nrows
         out = {"id": np.empty((n, spp), np.int32), "pos": np.empty((n, spp, 3)), "dist": np.empty((n, spp)),
                "rgb": np.empty((n, 3), np.uint8)}
         p = np.ascontiguousarray(cam_pos, dtype=np.float64)
         d = np.ascontiguousarray(cam_dir, dtype=np.float64)
+        sc = np.zeros(2, dtype=np.int64)
         hits = self.lib.lib.orc_render_paths(self.h, _ptr(p, _dp), _ptr(d, _dp), W, H, row0, nrows, int(frame),
-                                             int(spp), int(bounces), threads or self.lib.max_threads(),
+                                             int(spp), int(bounces), int(bool(shadow)),
+                                             threads or self.lib.max_threads(),
                                              _ptr(out["id"], _i32p), _ptr(out["pos"], _dp), _ptr(out["dist"], _dp),
-                                             _ptr(out["rgb"], _u8p))
+                                             _ptr(out["rgb"], _u8p), _ptr(sc, _i64p))
         if hits < 0:
             raise RuntimeError(self.lib.err())
         out["hits"] = int(hits)
+        out["shadow_cast"], out["shadow_occluded"] = int(sc[0]), int(sc[1])
         return out
 
 

@@ -1019,19 +1019,66 @@ V3 bounce_dir(V3 n, const V3& din, double u1, double u2) {
     if (len > 0.0) e = {e.x / len, e.y / len, e.z / len};
     return e;
 }
+
+// Head-light occlusion ray of a bounce vertex p (build-defined):
+// the segment from the light (at the camera C, main.cpp:356-377) to p — ray
+// o = C, d = e / |e| with e = p - C (Vector3::normalize's division,
+// vector3.hpp:91-95), length len = |e|.  Occluded iff some triangle of the
+// scene passes the reference's Moller-Trumbore test (triangle.hpp:40-62,
+// EPS 1e-8) with t < len * (1 - 2^-20) — any triangle, whatever the tree: the
+// test is tree-independent (no ancestor-box semantics), and the 2^-20 margin
+// keeps p's own triangle (t = len up to rounding) and its neighbours through p
+// out.  The traversal only prunes: boxes widened by wpad (far above any fp64
+// rounding of a passing test), interval unclipped.  len = 0: lit.
+constexpr double kShadowScale = 1.0 - 0x1p-20;
+inline bool box_hit_wide(const V3& mn, const V3& mx, const Ray& r, double w) {
+    return box_hit(V3{mn.x - w, mn.y - w, mn.z - w}, V3{mx.x + w, mx.y + w, mx.z + w}, r);
+}
+bool occluded(const BVH& b, const V3& C, const V3& p, double wpad, std::vector<int>& st) {
+    const V3 e = sub(p, C);
+    const double len = length(e);
+    if (!(len > 0.0)) return false;
+    const Ray r = make_ray(C, V3{e.x / len, e.y / len, e.z / len});
+    const double tmax = len * kShadowScale;
+    st.clear();
+    st.push_back(0);
+    while (!st.empty()) {
+        const Node& n = b.nodes[st.back()];
+        st.pop_back();
+        if (!box_hit_wide(n.mn, n.mx, r, wpad)) continue;
+        for (int i = n.begin; n.kids.empty() && i < n.end; ++i) {
+            double t;
+            if (tri_hit(b.tris[b.order[i]], r, t) && t < tmax) return true;
+        }
+        for (int c : n.kids) st.push_back(c);
+    }
+    return false;
+}
 }  // namespace
 extern "C" {
 
 // One pose: spp paths per pixel of 1 + bounces segments; rgb per pixel,
 // primary-segment id / pos / dist per sample at ((j-row0)*W + i)*spp + s.
+// shadow != 0: a bounce vertex (k >= 1) adds its colour only if the light
+// sees it (occluded() above); the primary vertex is the camera ray's own
+// closest hit, seen from the light at the camera by definition, and casts none.
+// shadow_counts (may be NULL): [occlusion rays cast, of which occluded].
 // Returns the number of samples whose primary ray hit, or -1.
 long long orc_render_paths(const orc_bvh* h, const double cam_pos[3], const double cam_dir[3], int W, int H,
-                           int row0, int nrows, int frame, int spp, int bounces, int threads, int32_t* hit_id,
-                           double* hit_pos, double* hit_dist, uint8_t* rgb) {
+                           int row0, int nrows, int frame, int spp, int bounces, int shadow, int threads,
+                           int32_t* hit_id, double* hit_pos, double* hit_dist, uint8_t* rgb,
+                           long long* shadow_counts) {
     if (W <= 0 || H <= 0 || row0 < 0 || nrows < 0 || row0 + nrows > H || spp < 1 || bounces < 0) {
         g_err = "bad path geometry";
         return -1;
     }
+    // occlusion box margin: 2^-30 of the scene's coordinate range
+    const Node& root = h->b.nodes[0];
+    const double cmax = std::max({std::fabs(root.mn.x), std::fabs(root.mn.y), std::fabs(root.mn.z),
+                                  std::fabs(root.mx.x), std::fabs(root.mx.y), std::fabs(root.mx.z),
+                                  std::fabs(cam_pos[0]), std::fabs(cam_pos[1]), std::fabs(cam_pos[2])});
+    const double wpad = std::ldexp(cmax + 1.0, -30);
+    long long s_cast = 0, s_occ = 0;
     const double fov = 90.0 * (std::numbers::pi / 180.0);
     const double th = std::tan(fov * 0.5);
     const double aspect = static_cast<double>(W) / H;
@@ -1043,7 +1090,7 @@ long long orc_render_paths(const orc_bvh* h, const double cam_pos[3], const doub
     long long hits = 0;
 #ifdef _OPENMP
     if (threads < 1) threads = 1;
-#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : hits)
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : hits, s_cast, s_occ)
 #endif
     for (int i = 0; i < W; ++i) {
         std::vector<int> st;
@@ -1075,11 +1122,19 @@ long long orc_render_paths(const orc_bvh* h, const double cam_pos[3], const doub
                     }
                     if (id < 0) break;
                     const V3 nrm = h->b.tris[id].normal;
-                    double c[3];
-                    shade(true, pos, nrm, cp, c);
-                    L[0] = L[0] + w * c[0];
-                    L[1] = L[1] + w * c[1];
-                    L[2] = L[2] + w * c[2];
+                    bool lit = true;
+                    if (shadow && b > 0) {
+                        s_cast++;
+                        lit = !occluded(h->b, cp, pos, wpad, st);
+                        s_occ += !lit;
+                    }
+                    if (lit) {
+                        double c[3];
+                        shade(true, pos, nrm, cp, c);
+                        L[0] = L[0] + w * c[0];
+                        L[1] = L[1] + w * c[1];
+                        L[2] = L[2] + w * c[2];
+                    }
                     w = w * 0.5;
                     if (b == bounces) break;
                     V3 N = nrm;  // the unit normal shade() uses (normalised once more)
@@ -1095,6 +1150,10 @@ long long orc_render_paths(const orc_bvh* h, const double cam_pos[3], const doub
             if (rgb)
                 for (int k = 0; k < 3; k++) rgb[o * 3 + k] = to_byte(spp == 1 ? acc[k] : acc[k] / (double)spp);
         }
+    }
+    if (shadow_counts) {
+        shadow_counts[0] = s_cast;
+        shadow_counts[1] = s_occ;
     }
     return hits;
 }

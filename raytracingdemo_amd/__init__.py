@@ -294,16 +294,20 @@ class Scene:
 
     def render_paths_device(self, device: int, pos, d, W: int, H: int, row0: int, row_stride: int, nrows: int,
                             frame: int = 0, spp: int = 16, bounces: int = 4, hit_id=0, dist=0, hit_pos=0, rgb=0,
-                            hit_count=0, stream=0, timing: bool = False, count: bool = False):
+                            hit_count=0, stream=0, timing: bool = False, count: bool = False,
+                            shadow: bool = False):
         """Diffuse path tracing of one pose into device pointers (include/rt.h
         rt_render_paths_device): rgb per pixel, primary-segment outputs per sample;
-        count: add the ray segments traced to frame_stats()["rays"]."""
+        count: add the ray segments traced to frame_stats()["rays"]; shadow: an
+        occlusion ray toward the head-light from every bounce vertex
+        (RT_FLAG_SHADOW)."""
         o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
         cam = _camera(pos, d, W, H)
         N.check(N.lib().rt_render_paths_device(self._h, int(device), C.byref(cam), int(frame), int(spp), int(bounces),
                                                int(row0), int(row_stride), int(nrows), C.byref(o),
                                                C.c_void_p(stream or None),
-                                               (N.RT_FLAG_TIMING if timing else 0) | (N.RT_FLAG_COUNT if count else 0)))
+                                               (N.RT_FLAG_TIMING if timing else 0) | (N.RT_FLAG_COUNT if count else 0) |
+                                               (N.RT_FLAG_SHADOW if shadow else 0)))
 
     def frame_stats(self, device: int = 0, reset: bool = True) -> dict:
         s = N.rt_frame_stats_t()

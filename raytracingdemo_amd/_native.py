@@ -27,6 +27,7 @@ RT_MODE_EXACT = 0
 RT_MODE_FP64 = 1
 RT_FLAG_COUNT = 1
 RT_FLAG_TIMING = 2
+RT_FLAG_SHADOW = 4
 RT_MISS = 0xFFFFFFFF
 
 # Every symbol include/rt.h declares (checked by tests/test_abi.py).
@@ -83,7 +84,8 @@ class rt_frame_stats_t(C.Structure):
                 ("wave_tiles", C.c_uint64), ("wave_tris", C.c_uint64), ("redo_rays", C.c_uint64), ("redo_chain", C.c_uint64),
                 ("spilled_rays", C.c_uint64), ("dropped_rays", C.c_uint64), ("empty_node_steps", C.c_uint64),
                 ("wave_tri_tests", C.c_uint64), ("wave_winners", C.c_uint64),
-                ("reserved", C.c_uint64 * 7), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
+                ("shadow_rays", C.c_uint64), ("shadow_occluded", C.c_uint64),
+                ("reserved", C.c_uint64 * 5), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
 
 
 class rt_build_times_t(C.Structure):

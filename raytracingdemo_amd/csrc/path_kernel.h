@@ -273,6 +273,61 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
     over_out = over;
 }
 
+// Head-light occlusion of a bounce vertex p (the oracle's occluded(),
+// oracle/rt_oracle.cpp): the ray from the light at the camera C
+// toward p, o = C, d = e / |e| (e = p - C, Vector3::normalize's divisions),
+// is occluded iff some triangle passes the reference's Moller-Trumbore test
+// (triangle.hpp:40-62) with t < |e| (1 - 2^-20) — over all triangles, so any
+// tree that finds every candidate gives the same answer.  The fp32 walk of the
+// walk tree (slabs widened by the pad, interval clipped to the fp32 bound of
+// tmax) keeps every triangle the fp64 test could pass; tri_classify's certain
+// class with an upper bound below 0.999 tmax is an occluder outright, any
+// other survivor whose lower bound is within the interval gets the fp64 test.
+// The first occluder ends the walk (any hit, no order needed).
+constexpr double kShadowScale = 1.0 - 0x1p-20;
+template <int W, int S, bool QN>
+__device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFrameCam& cam, double px, double py,
+                                              double pz, LaneStack<S>& st) {
+    const double ex = px - cam.pos[0], ey = py - cam.pos[1], ez = pz - cam.pos[2];
+    const double len = __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+    if (!(len > 0.0)) return false;
+    Ray64 r;
+    r.ox = cam.pos[0];
+    r.oy = cam.pos[1];
+    r.oz = cam.pos[2];
+    r.dx = ex / len;
+    r.dy = ey / len;
+    r.dz = ez / len;
+    r.ix = r.iy = r.iz = 0.0;
+    const double tmax = len * kShadowScale;
+    const Ray32 q = make_ray32<true>(r, ray_pad(sc, r));
+    const float tcert = (float)(tmax * 0.999);
+    LaneCounts lc;
+    LaneWalk<W, S, 1, false, QN> w;
+    w.begin(sc, q, 0.f, st);
+    w.tcull = round_up_f(tmax);
+    while (w.cur != RT_INVALID_REF) {
+        if (!(w.cur & RT_LEAF_BIT)) {
+            w.visit_node(sc, st, lc);
+            continue;
+        }
+        const uint32_t first = w.cur & RT_LEAF_FIRST_MASK;
+        const uint32_t cnt = ((w.cur >> 27) & 15u) + 1u;
+        for (uint32_t k = first; k < first + cnt; k++) {
+            const float4* R = reinterpret_cast<const float4*>(sc.tri32 + 12 * (size_t)k);
+            float tl, tu;
+            const int cls = tri_classify(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, w.tcull, tl, tu);
+            if (cls == 2 && tu < tcert) return true;
+            if (cls != 0) {
+                double t;
+                if (mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, r, t) && t < tmax) return true;
+            }
+        }
+        w.pop_next(st);
+    }
+    return false;
+}
+
 // Primary segments through wave_walk (PRIM, PACK on 8-wide trees whose stack
 // bound fits 128 entries): RT_PATHS_PRIMARY=0 walks them per lane.
 #ifndef RT_PATHS_PRIM
@@ -309,7 +364,10 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
 // pixels, one sample path per lane (lane = pixel * spp + sample; the pixels a
 // tw x th block), and the pixel's radiance is summed across its lanes in
 // sample order — the same additions as the per-lane sample loop.
-template <int W, int S, bool COUNT = false, bool PACK = false, bool PRIM = false>
+// SHADOW: a bounce vertex adds its colour only if the light sees it
+// (lane_occluded, one occlusion ray per vertex k >= 1; the primary vertex is
+// the camera ray's own closest hit, which the light at the camera sees).
+template <int W, int S, bool COUNT = false, bool PACK = false, bool PRIM = false, bool SHADOW = false>
 __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, uint32_t frame,
                                                int bounces) {
     static_assert(!PRIM || (PACK && W == 8 && RT_PATHS_DEFER), "wave-walked primaries: packed 8-wide deferred paths");
@@ -349,6 +407,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
             r = (tile / tiles_x) * 8 + (lane >> 3);
         }
         uint32_t hits = 0, segs = 0;  // segs: ray segments traced (RT_FLAG_COUNT)
+        uint32_t sh_cast = 0, sh_occ = 0;  // SHADOW: occlusion rays cast / occluded
         LaneCounts tot;               // COUNT: the lane's fetch counts over its paths
         // PRIM: the primary segment of every lane of the wave (one sample per
         // lane) walked together, before the lanes go their own ways
@@ -425,11 +484,21 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                         hits += win.tri >= 0;
                     }
                     if (win.tri < 0) break;
-                    double c[3];
-                    shade_at(cam, hb.px, hb.py, hb.pz, sh.nx, sh.ny, sh.nz, c);
-                    L[0] = L[0] + w * c[0];
-                    L[1] = L[1] + w * c[1];
-                    L[2] = L[2] + w * c[2];
+                    bool lit = true;
+                    if constexpr (SHADOW) {
+                        if (b > 0) {
+                            lit = !lane_occluded<W, S, W == 8 && RT_QNODES>(sc, cam, hb.px, hb.py, hb.pz, st);
+                            sh_cast++;
+                            sh_occ += !lit;
+                        }
+                    }
+                    if (lit) {
+                        double c[3];
+                        shade_at(cam, hb.px, hb.py, hb.pz, sh.nx, sh.ny, sh.nz, c);
+                        L[0] = L[0] + w * c[0];
+                        L[1] = L[1] + w * c[1];
+                        L[2] = L[2] + w * c[2];
+                    }
                     w = w * 0.5;
                     if (b == bounces) break;
                     double nx, ny, nz;
@@ -462,6 +531,10 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         }
         wave_add<13>(fp.hit_count, hits);
         if (fp.counters) wave_add<20>(fp.counters, segs);
+        if (SHADOW && fp.counters) {
+            wave_add<20>(fp.counters + 24, sh_cast);
+            wave_add<20>(fp.counters + 25, sh_occ);
+        }
         if (COUNT && fp.counters) {
             wave_add<24>(fp.counters + 1, tot.nodes);
             wave_add<24>(fp.counters + 6, tot.pre);

@@ -1210,8 +1210,19 @@ bool paths_primary_wave(const RtDevScene& sc) {
 
 // Diffuse path tracing of one pose (path_kernel.h): spp paths per pixel of
 // 1 + bounces segments each, on a zeroed work queue; leaves it dirty.
+// shadow: occlusion rays toward the head-light at the bounce vertices.
+template <int W, bool COUNT = false, bool PACK = false, bool PRIM = false>
+void launch_k_paths(dim3 grid, dim3 blk, hipStream_t s, const RtDevScene& sc, const RtFrameParams& fp,
+                    const RtLaunchAux& aux, uint32_t frame, int bounces, bool shadow) {
+    if (shadow)
+        hipLaunchKernelGGL((k_paths<W, kPathStack, COUNT, PACK, PRIM, true>), grid, blk, 0, s, sc, fp, aux, frame,
+                           bounces);
+    else
+        hipLaunchKernelGGL((k_paths<W, kPathStack, COUNT, PACK, PRIM, false>), grid, blk, 0, s, sc, fp, aux, frame,
+                           bounces);
+}
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
-                        int bounces, hipStream_t s, const hipEvent_t* ev) {
+                        int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev) {
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
     if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.tile_ctr || !aux.spill || aux.grid <= 0 ||
         aux.spill_cap + kPathStack < sc.stack_bound)
@@ -1221,27 +1232,25 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     const dim3 grid((unsigned)aux.grid), blk(256);
     if (ev) (void)hipEventRecord(ev[0], s);
     switch (sc.width) {
-        case 2: hipLaunchKernelGGL((k_paths<2, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
-        case 4: hipLaunchKernelGGL((k_paths<4, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 2: launch_k_paths<2>(grid, blk, s, sc, fp, aux, frame, bounces, shadow); break;
+        case 4: launch_k_paths<4>(grid, blk, s, sc, fp, aux, frame, bounces, shadow); break;
         case 8:
             // (fp.pack: a wave holds every sample of 64 / spp pixels)
             if (fp.pack && paths_primary_wave(sc)) {  // primary segments by the wave walk (path_kernel.h)
                 if (fp.counters)
-                    hipLaunchKernelGGL((k_paths<8, kPathStack, true, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
-                                       bounces);
+                    launch_k_paths<8, true, true, true>(grid, blk, s, sc, fp, aux, frame, bounces, shadow);
                 else
-                    hipLaunchKernelGGL((k_paths<8, kPathStack, false, true, true>), grid, blk, 0, s, sc, fp, aux, frame,
-                                       bounces);
+                    launch_k_paths<8, false, true, true>(grid, blk, s, sc, fp, aux, frame, bounces, shadow);
             } else if (fp.counters && fp.pack)  // the counting pass: fetch counts too
-                hipLaunchKernelGGL((k_paths<8, kPathStack, true, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                launch_k_paths<8, true, true>(grid, blk, s, sc, fp, aux, frame, bounces, shadow);
             else if (fp.counters)
-                hipLaunchKernelGGL((k_paths<8, kPathStack, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                launch_k_paths<8, true>(grid, blk, s, sc, fp, aux, frame, bounces, shadow);
             else if (fp.pack)
-                hipLaunchKernelGGL((k_paths<8, kPathStack, false, true>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                launch_k_paths<8, false, true>(grid, blk, s, sc, fp, aux, frame, bounces, shadow);
             else
-                hipLaunchKernelGGL((k_paths<8, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces);
+                launch_k_paths<8>(grid, blk, s, sc, fp, aux, frame, bounces, shadow);
             break;
-        case 16: hipLaunchKernelGGL((k_paths<16, kPathStack>), grid, blk, 0, s, sc, fp, aux, frame, bounces); break;
+        case 16: launch_k_paths<16>(grid, blk, s, sc, fp, aux, frame, bounces, shadow); break;
         default: return hipErrorInvalidValue;
     }
     if (ev) (void)hipEventRecord(ev[1], s);

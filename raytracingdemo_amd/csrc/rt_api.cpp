@@ -28,7 +28,7 @@ hipError_t launch_trace(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 int exact_blocks_per_cu(int width, uint32_t stack_bound);
 int packet_blocks_per_cu(int width);
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
-                        int bounces, hipStream_t s, const hipEvent_t* ev);
+                        int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev);
 hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
                            uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
@@ -76,7 +76,7 @@ size_t align_up(size_t x) {
 }
 
 // d_counters: RT_FLAG_COUNT counters (rt_frame_stats)
-constexpr size_t kCounterWords = 24;  // 18-23: RT_PROFILE builds (packet_kernel.h)
+constexpr size_t kCounterWords = 32;  // 18-23: RT_PROFILE builds (packet_kernel.h); 24-25: occlusion rays
 #if defined(RT_PROFILE) && RT_PROFILE
 constexpr bool RT_PROFILE_BUILD = true;  // every timed launch writes the counters
 #else
@@ -1000,12 +1000,22 @@ int rt_scene_build_times(const rt_scene* s, rt_build_times_t* out) {
 
 int rt_scene_upload(rt_scene* s, const int* devices, int n_devices) {
     if (!s || (n_devices > 0 && !devices)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (n_devices < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative device count");
+    // the list is rank order of the RCCL communicator a multi-device render
+    // builds (ncclCommInitAll): every ordinal once, checked before any device
+    // or RCCL call
+    for (int q = 0; q < n_devices; q++) {
+        if (devices[q] < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative device ordinal");
+        for (int p = 0; p < q; p++)
+            if (devices[p] == devices[q]) return fail(RT_ERR_INVALID_ARGUMENT, "device ordinal listed twice");
+    }
     std::lock_guard<std::mutex> lk(s->mu);
     try {
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device");
+        for (int q = 0; q < n_devices; q++)
+            if (devices[q] >= count) return fail(RT_ERR_INVALID_ARGUMENT, "device ordinal out of range");
         for (int q = 0; q < n_devices; q++) {
-            if (devices[q] < 0 || devices[q] >= count) return fail(RT_ERR_NO_DEVICE, "bad device ordinal");
             bool have = false;
             for (auto& r : s->reps) have |= r->device == devices[q];
             if (!have) upload_one(s, devices[q]);
@@ -1095,7 +1105,12 @@ int rt_render_shard_device_job(rt_scene* s, int device, const rt_camera* cams, i
         (!job->gathered || !job->frames_out || job->shards < 1 || job->height < 1 || job->width < 1 ||
          job->elem_bytes < 1 || job->frame_rows < 0 ||
          (job->frame_rows > 0 && job->frame_rows < rt_shard_rows(job->height, job->shards, 0)) ||
-         (uint64_t)job->frames * (uint64_t)job->height >= (1ull << 32)))
+         (uint64_t)job->frames * (uint64_t)job->height >= (1ull << 32) ||
+         // every shard's section must lie inside its block (the tallest
+         // shard's rows: frame_rows, or rt_shard_rows of shard 0)
+         job->section_offset + (uint64_t)job->frames *
+                 (uint64_t)(job->frame_rows > 0 ? job->frame_rows : rt_shard_rows(job->height, job->shards, 0)) *
+                 (uint64_t)job->width * (uint64_t)job->elem_bytes > job->block_bytes))
         return fail(RT_ERR_INVALID_ARGUMENT, "bad de-interleave job");
     if (!s || !out || (nframes > 0 && !cams)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     if (nframes < 0) return fail(RT_ERR_INVALID_ARGUMENT, "negative frame count");
@@ -1181,6 +1196,7 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
         }
         hipError_t e;
         if (paths_wavefront()) {
+            if (flags & RT_FLAG_SHADOW) return fail(RT_ERR_INVALID_ARGUMENT, "RT_PATHS_WF=1 has no occlusion rays");
             const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows;
             ensure_cand(*r, P);  // candidate lists, stride P
             const PathWs ws = ensure_pw(*r, P);
@@ -1190,7 +1206,8 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             q.fresh = false;  // the work queue is left dirty: the next packet launch clears it
         } else {
             Slot& q = take_slot(*r, st, (flags & RT_FLAG_COUNT) != 0);
-            e = rt::launch_paths(r->dev, fp, aux_of(*r, q), (uint32_t)frame, bounces, st, tev);
+            e = rt::launch_paths(r->dev, fp, aux_of(*r, q), (uint32_t)frame, bounces, (flags & RT_FLAG_SHADOW) != 0,
+                                 st, tev);
             q.fresh = false;
         }
         HIP_TRY(e);
@@ -1335,6 +1352,8 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->empty_node_steps = c[15];
         out->wave_tri_tests = c[16];
         out->wave_winners = c[17];
+        out->shadow_rays = c[24];
+        out->shadow_occluded = c[25];
         out->timed_launches = r.tev_used;
         out->trace_ms = 0.0;
         for (size_t k = 0; k < r.tev_used; k++) {

@@ -128,7 +128,9 @@ def test_shard_render_job_is_validated_before_any_device_work():
     buf = np.zeros(4096, dtype=np.uint8)
     good = dict(gathered=buf.ctypes.data, block_bytes=1024, section_offset=0, shards=2, frames=1, height=16,
                 width=16, elem_bytes=3, frame_rows=8, frames_out=buf.ctypes.data)
-    for bad in (dict(shards=0), dict(gathered=None), dict(frames_out=None), dict(frame_rows=4), dict(elem_bytes=0)):
+    for bad in (dict(shards=0), dict(gathered=None), dict(frames_out=None), dict(frame_rows=4), dict(elem_bytes=0),
+                dict(block_bytes=8 * 16 * 3 - 1), dict(section_offset=1024 - 8 * 16 * 3 + 1),
+                dict(frame_rows=0, block_bytes=8 * 16 * 3 - 1)):
         j = N.rt_deinterleave_job(**{**good, **bad})
         st = L.rt_render_shard_device_job(s.handle, 0, cams, 1, 1, N.RT_MODE_EXACT, 0, 2, C.byref(o), C.byref(j),
                                           None, 0)
@@ -137,6 +139,25 @@ def test_shard_render_job_is_validated_before_any_device_work():
     j = N.rt_deinterleave_job(**good)
     st = L.rt_render_shard_device_job(s.handle, 0, cams, 1, 1, N.RT_MODE_EXACT, 0, 2, C.byref(o), C.byref(j), None, 0)
     assert st != N.RT_OK and b"not uploaded" in L.rt_last_error()
+
+
+def test_upload_rejects_repeated_or_negative_device_ordinals():
+    """rt_scene_upload's device list is the rank order of the RCCL communicator
+    a multi-device render creates (ncclCommInitAll): a
+    negative or repeated ordinal is RT_ERR_INVALID_ARGUMENT before any device
+    or RCCL call (so here too, without a GPU); an ordinal past the device
+    count is RT_ERR_INVALID_ARGUMENT on a GPU box, RT_ERR_NO_DEVICE here."""
+    N, L = _lib()
+    import raytracingdemo_amd as rt
+    from conftest import golden_scene
+    s = rt.Scene(golden_scene("teapot.obj"), "bsah", 8)
+    for devs, msg in (([0, 0], b"listed twice"), ([1, 0, 1], b"listed twice"), ([-1], b"negative")):
+        arr = (C.c_int * len(devs))(*devs)
+        assert L.rt_scene_upload(s.handle, arr, len(devs)) == N.RT_ERR_INVALID_ARGUMENT, devs
+        assert msg in L.rt_last_error(), devs
+    assert L.rt_scene_upload(s.handle, None, -1) == N.RT_ERR_INVALID_ARGUMENT
+    arr = (C.c_int * 1)(4096)
+    assert L.rt_scene_upload(s.handle, arr, 1) in (N.RT_ERR_INVALID_ARGUMENT, N.RT_ERR_NO_DEVICE)
 
 
 @pytest.mark.parametrize("G,F,H,W,eb", [(1, 2, 5, 3, 4), (2, 3, 7, 5, 3), (3, 2, 1080, 16, 8), (8, 1, 1081, 9, 24),

@@ -359,7 +359,7 @@ def test_config_c3_shape_standin_bunny_1080p(oracle):
         assert int(cnt[f]) == o["hits"] > 0, f
 
 
-def _paths(s, pos, d, Wp, Hp, frame, spp, bounces, row0, stride, nrows):
+def _paths(s, pos, d, Wp, Hp, frame, spp, bounces, row0, stride, nrows, shadow=False):
     npx = nrows * Wp
     t_id = torch.empty(npx * spp, dtype=torch.int32, device="cuda:0")
     t_dist = torch.empty(npx * spp, dtype=torch.float64, device="cuda:0")
@@ -367,12 +367,17 @@ def _paths(s, pos, d, Wp, Hp, frame, spp, bounces, row0, stride, nrows):
     t_cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
     s.render_paths_device(0, pos, d, Wp, Hp, row0, stride, nrows, frame=frame, spp=spp, bounces=bounces,
                           hit_id=t_id.data_ptr(), dist=t_dist.data_ptr(), rgb=t_rgb.data_ptr(),
-                          hit_count=t_cnt.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+                          hit_count=t_cnt.data_ptr(), stream=torch.cuda.current_stream().cuda_stream,
+                          shadow=shadow, count=shadow)
     torch.cuda.synchronize()
     g_id = t_id.cpu().numpy().view(np.uint32).reshape(npx, spp)
-    return {"id": np.where(g_id == rt.RT_MISS, -1, g_id.astype(np.int64)),
-            "dist": t_dist.cpu().numpy().reshape(npx, spp), "rgb": t_rgb.cpu().numpy().reshape(npx, 3),
-            "hits": int(t_cnt.item())}
+    out = {"id": np.where(g_id == rt.RT_MISS, -1, g_id.astype(np.int64)),
+           "dist": t_dist.cpu().numpy().reshape(npx, spp), "rgb": t_rgb.cpu().numpy().reshape(npx, 3),
+           "hits": int(t_cnt.item())}
+    if shadow:
+        st = s.frame_stats(0, reset=True)
+        out["shadow_cast"], out["shadow_occluded"] = st["shadow_rays"], st["shadow_occluded"]
+    return out
 
 
 def _same_paths(g, o, what):
@@ -382,9 +387,13 @@ def _same_paths(g, o, what):
     bad = np.flatnonzero((g["rgb"] != o["rgb"]).any(1))
     assert bad.size == 0, (what, bad[:10])
     assert g["hits"] == o["hits"] > 0, what
+    for k in ("shadow_cast", "shadow_occluded"):
+        if k in g:
+            assert g[k] == o[k], (what, k)
 
 
-def test_config_c5_exact_combination_matches_oracle(oracle):
+@pytest.mark.parametrize("shadow", [False, True])
+def test_config_c5_exact_combination_matches_oracle(oracle, shadow):
     """Config c5 exactly as `bench.py --paths` times it: sponza proxy, walk
     tree built on the device, 3840x2160 camera, 16 spp (the packed path: a
     wave holds every sample of 2x2 pixels), 1 + 4 segments, pose k of the
@@ -392,6 +401,9 @@ def test_config_c5_exact_combination_matches_oracle(oracle):
     bottom; ~1.1 M segments each) and one strided shard (4 rows 540 apart, the
     row_stride the per-rank call takes) against orc_render_paths: every
     sample's primary id and distance, every pixel's colour and the hit count.
+    shadow: with the occlusion rays toward the head-light from every bounce
+    vertex (RT_FLAG_SHADOW, as `bench.py --paths` times it), also the numbers
+    of occlusion rays cast and occluded.
     Reference: StackBVH::traverse per segment (src/stack_bvh.hpp:611-644),
     the vertex colour of shadeScreen (src/main.cpp:356-377)."""
     from raytracingdemo_amd.scenes import sponza_proxy_triangles
@@ -403,15 +415,16 @@ def test_config_c5_exact_combination_matches_oracle(oracle):
     for frame in (0, 1):
         pos, d = path.circular_path(frame)
         for row0 in (0, Hp // 2 - 2, Hp - 4):
-            g = _paths(s, pos, d, Wp, Hp, frame, S, B, row0, 1, 4)
-            o = ob.render_paths(pos, d, Wp, Hp, frame, S, B, row0=row0, nrows=4)
+            g = _paths(s, pos, d, Wp, Hp, frame, S, B, row0, 1, 4, shadow)
+            o = ob.render_paths(pos, d, Wp, Hp, frame, S, B, row0=row0, nrows=4, shadow=shadow)
             _same_paths(g, o, (frame, row0))
     # a strided shard (rows 3, 543, 1083, 1623: row0 = rank, stride = world)
     pos, d = path.circular_path(2)
-    g = _paths(s, pos, d, Wp, Hp, 2, S, B, 3, 540, 4)
-    parts = [ob.render_paths(pos, d, Wp, Hp, 2, S, B, row0=r, nrows=1) for r in (3, 543, 1083, 1623)]
+    g = _paths(s, pos, d, Wp, Hp, 2, S, B, 3, 540, 4, shadow)
+    parts = [ob.render_paths(pos, d, Wp, Hp, 2, S, B, row0=r, nrows=1, shadow=shadow) for r in (3, 543, 1083, 1623)]
     o = {k: np.concatenate([p[k] for p in parts]) for k in ("id", "dist", "rgb")}
-    o["hits"] = sum(p["hits"] for p in parts)
+    for k in ("hits", "shadow_cast", "shadow_occluded"):
+        o[k] = sum(p[k] for p in parts)
     _same_paths(g, o, "strided shard")
 
 

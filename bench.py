@@ -193,7 +193,55 @@ def scene_difficulty(label, algo, k):
     return d.get(key)
 
 
-def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
+def rank_problems(table, backend, pg_size, world, gpus, rehearse):
+    """What is wrong with an N-rank run, from every rank's [rank, local rank,
+    device ordinal, PCI bus] row (rank order) and the process group's backend
+    and size; [] when it is what --gpus asks for."""
+    ordinals = [r[2] for r in table]
+    problems = []
+    if pg_size != gpus or world != gpus or len(table) != gpus:
+        problems.append(f"process group size {pg_size} / WORLD_SIZE {world} / {len(table)} rows != --gpus {gpus}")
+    if [r[0] for r in table] != list(range(len(table))):
+        problems.append(f"ranks {[r[0] for r in table]}")
+    if not rehearse:
+        if backend != "nccl":
+            problems.append(f"backend {backend}, not nccl (RCCL)")
+        if len(set(ordinals)) != len(table) or len(set((r[3], r[2]) for r in table)) != len(table):
+            problems.append(f"device ordinals {ordinals} (bus {[r[3] for r in table]}) not one per rank")
+    return problems
+
+
+def rank_facts(a, world, rank, local, dev, coll, rehearse):
+    """Self-check of an N-rank run, before any timing: the
+    process group's size and backend, every rank's device ordinal and PCI bus
+    as the ranks themselves report them (all_gather over the same communicator
+    that carries the frames).  Any disagreement with --gpus ends the run with
+    exit status 1 on every rank (rehearsals: every rank on device 0 over gloo,
+    by design)."""
+    import torch
+    import torch.distributed as dist
+    backend = str(dist.get_backend())
+    pg_size = dist.get_world_size()
+    props = torch.cuda.get_device_properties(dev)
+    bus = int(getattr(props, "pci_bus_id", -1))
+    me = torch.tensor([rank, local, torch.cuda.current_device(), bus], dtype=torch.int64, device=dev)
+    allv = [coll(torch.empty_like(me)) for _ in range(world)]
+    dist.all_gather(allv, coll(me))
+    table = [[int(x) for x in v.tolist()] for v in allv]
+    problems = rank_problems(table, backend, pg_size, world, a.gpus, rehearse)
+    facts = {"world_size": world, "process_group_size": pg_size, "backend": backend,
+             "rccl": backend == "nccl", "device_ordinals": [r[2] for r in table], "pci_bus": [r[3] for r in table],
+             "verified": not problems}
+    if problems:
+        if rank == 0:
+            print(json.dumps({"error": "multi-rank self-check failed", "problems": problems, "ranks": facts}),
+                  flush=True)
+        dist.destroy_process_group()
+        raise SystemExit(1)
+    return facts
+
+
+def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ranks=None):
     """Config c5: diffuse path tracing of primary + secondary rays (rt_render_paths_device).
     A step is one pose of the orbit (step k: frame k % 36), every rank tracing its
     interleaved rows, then one RCCL gather of the colours to rank 0, which
@@ -288,6 +336,14 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
         except (OSError, ValueError, KeyError):
             pass
         achieved = alg_pose / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        valu = None
+        try:
+            pv = json.load(open(os.path.join(ROOT, "profiles", "pmc_valu_paths.json")))
+            if pv.get("workload_key") == key:
+                valu = {"busy": pv["valu_busy"], "issue": issue_roofline(pv),
+                        "wave_cycles_split": pv.get("wave_cycles_split"), "source": "profiles/pmc_valu_paths.json"}
+        except (OSError, ValueError, KeyError):
+            pass
         line = {
             "metric": f"Mrays/sec (primary + {B} diffuse bounces, {S}spp) on Sponza {W}x{H}",
             "value": round(nominal / elapsed / 1e6, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
@@ -300,6 +356,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
                                    + (", one head-light occlusion ray per bounce vertex" if shadow else ""),
                        "width": W, "height": H, "spp": S, "bounces": B, "frames_per_step": F,
                        "parallelism": f"image rows interleaved x{world}" + (" + RCCL gather" if world > 1 else ""),
+                       **({"ranks": {**ranks, "gather_bytes_per_step": world * rows * W * 3 * F}} if ranks else {}),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "segments_traced_per_s_M": round(segs_per_pose * a.steps * F / elapsed / 1e6, 2),
             "segments_per_sample": round(segs_per_pose / (W * H * S), 3),
@@ -318,7 +375,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse):
                          "bytes": "per-lane node steps x 96 (quantised) + wave node steps x 256 and wave triangle "
                                   "records x 48 (primary segments walked by the wave) + pre-filter x 48 + fp64 tests "
                                   "x 72 + chain checks x 52 + segments x 56 + 3 per pixel",
-                         "wave_nodes_per_pose": round(cs["wave_nodes"] / F), "wave_tris_per_pose": round(cs["wave_tris"] / F)},
+                         "wave_nodes_per_pose": round(cs["wave_nodes"] / F), "wave_tris_per_pose": round(cs["wave_tris"] / F),
+                         "valu": valu},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -396,6 +454,7 @@ def main():
                 opts = None
             dist.init_process_group("nccl", device_id=dev, pg_options=opts)
     coll = (lambda t: t.cpu()) if rehearse else (lambda t: t)  # collective-side tensors
+    ranks = rank_facts(a, world, rank, local, dev, coll, rehearse) if world > 1 else None
 
     if a.scene == "armadillo":
         sc = armadillo_scene()
@@ -436,7 +495,7 @@ def main():
         build_ms["walk_tree_host_ms"] = round(hb["walk_tree_ms"], 1)
         build_ms["scene_create_host_walk_ms"] = round(hb["total_ms"], 1)
     if a.paths:
-        return run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse)
+        return run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ranks)
     st = scene.stats()
     W, H, F = a.width, a.height, a.frames
     center = rt.scene_center(tris)
@@ -729,7 +788,7 @@ def main():
         try:
             pv = json.load(open(os.path.join(ROOT, "profiles", "pmc_valu.json")))
             if pv.get("workload_key") == key:
-                valu = {"busy": pv["valu_busy"], "insts_per_launch": pv["valu_insts_per_launch"],
+                valu = {"busy": pv["valu_busy"], "issue": issue_roofline(pv), "insts_per_launch": pv["valu_insts_per_launch"],
                         "salu_insts_per_launch": pv["salu_insts_per_launch"],
                         # SURVEY §8(d) asks for VALU ops per ray: every lane of a
                         # wave64 instruction is one ray's op (a tile's 64 rays share
@@ -767,6 +826,12 @@ def main():
                        "parallelism": f"8-row image bands interleaved x{world}" +
                                       (" + RCCL gather of rgb (overlapped)" if world > 1 else ""),
                        **({"gather_verified": verified} if world > 1 else {}),
+                       # rank 0's de-interleave of the gathered frames: done by the
+                       # traversal kernel of a render (rt_render_shard_device_job) or
+                       # by its own kernel, over the timed steps
+                       **({"side_jobs": {"fused": ks["side_jobs_fused"], "kernel": ks["side_jobs_kernel"]}}
+                          if ks["side_jobs_fused"] + ks["side_jobs_kernel"] else {}),
+                       **({"ranks": {**ranks, "gather_bytes_per_step": world * pay_bytes}} if ranks else {}),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -816,6 +881,23 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def issue_roofline(pv):
+    """The instruction-issue bound beside the HBM one (the walk is cache-resident
+    and issue/latency-bound): the share of the SIMDs' issue
+    cycles the kernel's VALU (2 cycles per wave64 instruction on a SIMD-32)
+    and SALU (1 cycle) instructions take, from the committed SQ passes
+    (tools/pmc_valu.py): (2 VALU + SALU) / (1024 SIMDs x active cycles)."""
+    cyc = pv.get("cycles_per_xcd")
+    valu, salu = pv.get("valu_insts_per_launch"), pv.get("salu_insts_per_launch")
+    if not (cyc and valu and salu):
+        return None
+    return {"frac": round((2.0 * valu + salu) / (1024.0 * cyc), 4), "valu": round(2.0 * valu / (1024.0 * cyc), 4),
+            "salu": round(salu / (1024.0 * cyc), 4), "unit": "issue cycles / SIMD cycles",
+            "formula": "(2 x SQ_INSTS_VALU + SQ_INSTS_SALU) / (1024 x GRBM_GUI_ACTIVE / 8)",
+            # the two ports apart: VALU per SIMD, SALU on the CU's one scalar unit
+            "valu_port": round(2.0 * valu / (1024.0 * cyc), 4), "salu_port_per_cu": round(salu / (256.0 * cyc), 4)}
 
 
 def packed_spp(spp):

@@ -150,7 +150,9 @@ typedef struct {
     uint64_t wave_winners;   /*   winners' shading records, once per wave  */
     uint64_t shadow_rays;    /* paths with RT_FLAG_SHADOW: occlusion rays cast  */
     uint64_t shadow_occluded;/*   of which occluded                            */
-    uint64_t reserved[5];
+    uint64_t side_jobs_fused;  /* rt_deinterleave_job: done by the traversal kernel */
+    uint64_t side_jobs_kernel; /*   done by a de-interleave kernel after the render */
+    uint64_t reserved[3];
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */

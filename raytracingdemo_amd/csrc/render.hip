@@ -675,6 +675,10 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
     const int tid = threadIdx.x;
     if (tid == 0) {
         n_sh = *(volatile uint32_t*)(aux.tile_ctr + RT_REDO_COUNT);
+        // the launch's redo count to the host (it sizes the slot's list and
+        // the fix-up grid of the next launches by it; a vector store)
+        if (blockIdx.x == 0 && aux.redo_seen)
+            __hip_atomic_store(aux.redo_seen, n_sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence();
         if (atomicAdd(aux.tile_ctr + RT_FIXUP_DONE, 1u) == gridDim.x - 1) {
             aux.tile_ctr[RT_REDO_COUNT] = 0;
@@ -715,7 +719,11 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
         const int p = (int)(ob / npix);
         const uint32_t o = ob - (uint32_t)p * npix;
         const int i = (int)(o % (uint32_t)fp.W), r = (int)(o / (uint32_t)fp.W);
-        trace_pixel<W, S, COUNT>(sc, fp, p, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
+        // (a retry re-traces pixels the walk counted already: no fetch counts)
+        if (COUNT && !retry)
+            trace_pixel<W, S, true>(sc, fp, p, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
+        else
+            trace_pixel<W, S, false>(sc, fp, p, i, r, st, (v & kRedoPass1) ? 1 : 0, true);
     }
 }
 
@@ -913,7 +921,9 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     // rest of the pipeline is timed as frame minus traversal by the caller)
     if (ev) (void)hipEventRecord(ev[0], s);
     if (use_packet(sc.stack_bound)) {
-        int fg = kFixupGrid;
+        // (aux.fgrid: the host saw this slot's redo list overflow, so a
+        // retry of the whole launch is likely: the full grid)
+        int fg = aux.fgrid > 0 ? aux.fgrid : kFixupGrid;
         if (const char* e = getenv("RT_FIXUP_GRID")) fg = atoi(e) > 0 ? atoi(e) : fg;  // tuning hook, read per call
         const dim3 fgrid((unsigned)(aux.grid < fg ? aux.grid : fg));
         if (!split_resolve(fp.spp)) {

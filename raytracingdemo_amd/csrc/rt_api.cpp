@@ -32,6 +32,7 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
                            uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
+bool packet_takes_job(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count);
 bool packet_split(int spp, bool pack);
 uint32_t params_bytes();
 int exact_lds_stack();
@@ -101,6 +102,7 @@ struct Slot {
     uint64_t* d_spill = nullptr;
     uint32_t* d_redo = nullptr;  // packet pipeline -> fix-up kernel pixel list
     uint64_t redo_cap = 0;
+    uint32_t* h_seen = nullptr;  // host-mapped: the redo count k_fixup saw in the slot's last launch
     uint64_t* d_pool = nullptr;  // candidate overflow pool (pool_chunks x RT_POOL_CHUNK entries)
     hipStream_t last = nullptr;  // the stream of the slot's last launch
     bool used = false;
@@ -135,6 +137,8 @@ struct Replica {
     std::vector<std::array<hipEvent_t, 2>> tev;
     size_t tev_used = 0;
     hipEvent_t ev_out = nullptr;
+    // side de-interleave jobs run by the traversal kernel itself / as their own kernel
+    uint64_t jobs_fused = 0, jobs_kernel = 0;
 };
 
 }  // namespace
@@ -240,6 +244,7 @@ void free_replica(Replica& r) {
         if (q.d_tiles) hipFree(q.d_tiles);
         if (q.d_spill) hipFree(q.d_spill);
         if (q.d_redo) hipFree(q.d_redo);
+        if (q.h_seen) hipHostFree(q.h_seen);
         if (q.d_pool) hipFree(q.d_pool);
         if (q.ev) hipEventDestroy(q.ev);
     }
@@ -259,6 +264,19 @@ Replica& replica_for(rt_scene* s, int device) {
     for (auto& r : s->reps)
         if (r->device == device) return *r;
     throw rt::Error{RT_ERR_NO_DEVICE, "scene not uploaded to device " + std::to_string(device)};
+}
+
+// The launch state of one slot (work-queue block, stack spill, candidate
+// pool, redo-count word; the redo list is sized per launch by ensure_redo).
+void alloc_slot(Replica& r, Slot& q) {
+    if (q.d_tiles) return;
+    HIP_TRY(hipMalloc(&q.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(q.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&q.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&q.d_pool, (size_t)r.pool_chunks * RT_POOL_CHUNK * sizeof(uint64_t)));
+    HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&q.h_seen), sizeof(uint32_t), hipHostMallocMapped));
+    *q.h_seen = 0;
 }
 
 void upload_one(rt_scene* s, int device) {
@@ -347,13 +365,7 @@ void upload_one(rt_scene* s, int device) {
         const long v = std::atol(e);
         if (v >= 1 && v <= (long)kPoolChunks) r.pool_chunks = (uint32_t)v;
     }
-    for (Slot& q : r.slot) {
-        HIP_TRY(hipMalloc(&q.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
-        HIP_TRY(hipMemset(q.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc(&q.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
-        HIP_TRY(hipMalloc(&q.d_pool, (size_t)r.pool_chunks * RT_POOL_CHUNK * sizeof(uint64_t)));
-        HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
-    }
+    alloc_slot(r, r.slot[0]);  // (the second slot on the first launch from another stream: take_slot)
     s->reps.push_back(std::move(rp));
 }
 
@@ -371,9 +383,13 @@ void quiesce(Replica& r) {
 
 // Redo list: a fixed pool of entries, not one per pose pixel (on the sponza
 // proxy ~0 pixels are redone; a launch whose redo count passes the pool is
-// retried whole by k_fixup).  RT_REDO_CAP (read per call; a test hook) lowers
-// the entries a launch may use.
+// retried whole by k_fixup).  k_fixup reports each launch's count to a
+// host-mapped word of the slot; a slot that overflowed gets a longer list
+// (twice the count, up to kRedoGrow entries) and, while its launches still
+// overflow, the full fix-up grid for the retry.  RT_REDO_CAP (read per call;
+// a test hook) lowers the entries a launch may use.
 constexpr uint64_t kRedoEntries = 1u << 20;  // 4 MiB
+constexpr uint64_t kRedoGrow = 1u << 26;     // 256 MiB
 uint64_t redo_limit() {
     const char* e = std::getenv("RT_REDO_CAP");
     const long long v = e ? std::atoll(e) : 0;
@@ -382,8 +398,8 @@ uint64_t redo_limit() {
 
 // Redo list of a slot for a launch of `pixels` pose pixels (grown, never
 // shrunk; at most kRedoEntries).
-void ensure_redo(Slot& q, uint64_t pixels) {
-    pixels = std::min<uint64_t>(std::max<uint64_t>(pixels, 1), kRedoEntries);
+void ensure_redo(Slot& q, uint64_t pixels, uint64_t most = kRedoEntries) {
+    pixels = std::min<uint64_t>(std::max<uint64_t>(pixels, 1), most);
     if (q.redo_cap >= pixels) return;
     quiesce_slot(q);
     if (q.d_redo) HIP_TRY(hipFree(q.d_redo));
@@ -525,6 +541,13 @@ int batch_frames() {
 // (HBM candidate lists, the wavefront workspace, the counting pass's
 // counters), so it follows the launches of every slot.
 Slot& take_slot(Replica& r, hipStream_t st, bool shared) {
+    // one caller stream: slot 0 only (launches on one stream are ordered
+    // anyway); the second slot is allocated when a launch comes from another
+    // stream than slot 0's last one
+    if (!r.slot[1].d_tiles) {
+        if (!r.slot[0].used || r.slot[0].last == st) r.next_slot = 0;
+        else alloc_slot(r, r.slot[1]);
+    }
     Slot& q = r.slot[r.next_slot];
     r.next_slot = (r.next_slot + 1) % kSlots;
     auto follow = [&](Slot& o) {
@@ -603,8 +626,20 @@ uint32_t literal_stack_bound(const rt_scene* s) {
 void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
             const hipEvent_t* tev, const rt_deinterleave_job* job) {
     bool fresh_after = false;
+    // a slot whose last launch overflowed its redo list (the count k_fixup
+    // reported, possibly from a launch still running: a sizing hint only)
+    const uint32_t seen = __atomic_load_n(q.h_seen, __ATOMIC_RELAXED);
+    const uint64_t lpix = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)(fp.nframes / std::max(fp.spp, 1));
+    if (seen > q.redo_cap && q.redo_cap < std::min(lpix, kRedoGrow))
+        ensure_redo(q, std::min<uint64_t>(2ull * seen, lpix), kRedoGrow);
     RtLaunchAux a = aux_of(r, q);
+    a.redo_seen = q.h_seen;
+    if (seen > a.redo_cap) a.fgrid = r.grid;
     set_job(a, job);
+    if (a.job_src) {
+        const bool empty = fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0;
+        (!empty && rt::packet_takes_job(r.dev, fp, mode, count) ? r.jobs_fused : r.jobs_kernel)++;
+    }
     const hipError_t e = rt::launch_trace(r.dev, fp, a, mode, count, st, s->literal_stack, tev, q.fresh, &fresh_after);
     q.fresh = e == hipSuccess && fresh_after;
     HIP_TRY(e);
@@ -1354,6 +1389,9 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->wave_winners = c[17];
         out->shadow_rays = c[24];
         out->shadow_occluded = c[25];
+        out->side_jobs_fused = r.jobs_fused;
+        out->side_jobs_kernel = r.jobs_kernel;
+        if (reset) r.jobs_fused = r.jobs_kernel = 0;
         out->timed_launches = r.tev_used;
         out->trace_ms = 0.0;
         for (size_t k = 0; k < r.tev_used; k++) {

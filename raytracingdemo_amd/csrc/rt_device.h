@@ -173,6 +173,9 @@ struct RtLaunchAux {
     int32_t grid;         // persistent blocks (CUs x resident blocks per CU)
     RT_G uint32_t* redo;       // packet kernel -> k_fixup: pixel index | start-pass bit
     uint64_t redo_cap;    // entries (a fixed pool: past it k_fixup retries the whole launch)
+    uint32_t* redo_seen;  // host-mapped word: k_fixup reports the launch's redo count there (or null);
+                          // the host grows the slot's list for its next launches from it
+    int32_t fgrid;        // k_fixup blocks (0: the default kFixupGrid)
     RT_G uint64_t* pool;       // candidate overflow pool: pool_chunks x RT_POOL_CHUNK entries
     uint32_t pool_chunks;
     int32_t pgrid;             // workgroups of the packet kernel (64 * kPacketWaves threads each)

@@ -44,12 +44,15 @@ def source_rows(H: int, world: int, rows: int, band: int = BAND) -> list[int]:
 
 
 _IDX: dict = {}
+_FLAT_MAX = 8  # index tensors kept per cache (one per shape and device; _FLAT's hold F*H int64)
 
 
 def _index(H: int, world: int, rows: int, device, band: int):
     import torch
     key = (H, world, rows, str(device), band)
     if key not in _IDX:
+        while len(_IDX) >= _FLAT_MAX:
+            _IDX.pop(next(iter(_IDX)))
         _IDX[key] = torch.tensor(source_rows(H, world, rows, band), dtype=torch.long, device=device)
     return _IDX[key]
 
@@ -80,6 +83,8 @@ def _flat_index(H: int, world: int, F: int, rows: int, device, band: int):
         src = _index(H, world, rows, device, band)
         g, r = src // rows, src % rows
         f = torch.arange(F, dtype=torch.long, device=device)[:, None]
+        while len(_FLAT) >= _FLAT_MAX:  # bounded: a sweep over sizes keeps only the latest shapes
+            _FLAT.pop(next(iter(_FLAT)))
         _FLAT[key] = ((g[None, :] * F + f) * rows + r[None, :]).reshape(-1)
     return _FLAT[key]
 

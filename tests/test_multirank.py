@@ -141,3 +141,47 @@ def test_python_shards_match_the_library_layout():
             assert [len(rr) for rr in rows] == [rt.shard_height(H, world, r) for r in range(world)]
             assert max(len(rr) for rr in rows) <= rows_per_rank(H, world)
             assert all(rr == sorted(rr) for rr in rows)
+
+def _facts_worker(rank: int, world: int, port: int, ordinals, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        me = torch.tensor([rank, rank, ordinals[rank], 0x40 + ordinals[rank]], dtype=torch.int64)
+        allv = [torch.empty_like(me) for _ in range(world)]
+        dist.all_gather(allv, me)
+        table = [[int(x) for x in v.tolist()] for v in allv]
+        for gpus, backend in ((world, "nccl"), (world + 1, "nccl"), (world, "gloo")):
+            q.put((rank, gpus, backend, bench.rank_problems(table, backend, dist.get_world_size(), world, gpus,
+                                                            False)))
+    except Exception as e:
+        q.put((rank, None, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ordinals,ok", [([0, 1], True), ([0, 0], False), ([3, 1, 2], True), ([1, 2, 1], False)])
+def test_bench_rank_self_check(ordinals, ok):
+    """bench.py's N-rank self-check (rank_problems on the rows all_gather
+    collects from every rank, gloo here): one device ordinal per rank, the
+    process group's size equal to --gpus and the nccl (RCCL) backend pass;
+    a repeated ordinal, a --gpus that disagrees or another backend fail."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    world = len(ordinals)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_facts_worker, args=(r, world, port, ordinals, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(3 * world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, gpus, backend, problems in res:
+        assert gpus is not None, problems
+        if gpus == world and backend == "nccl":
+            assert (problems == []) == ok, (ordinals, problems)
+        else:
+            assert problems, (gpus, backend)

@@ -9,7 +9,16 @@ A wave64 VALU instruction occupies a SIMD-32 for 2 cycles (MI355X_MICROARCH.md,
 "Wave scheduling"); GRBM_GUI_ACTIVE is summed over the 8 XCDs.  The non-
 counting dispatch of one 36-frame launch is used.
 
-Usage: tools/pmc_valu.py KEY_FILE OUT_JSON SQ_CSV [SQ_CSV ...]
+Also the issue roofline of the kernel: the share of the
+SIMDs' issue cycles its VALU and SALU instructions take,
+
+  issue = (SQ_INSTS_VALU x 2 + SQ_INSTS_SALU x 1) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+
+(a wave64 VALU instruction holds its SIMD-32 for 2 cycles, a SALU
+instruction issues in 1), with the VALU and SALU shares beside it.
+
+Usage: tools/pmc_valu.py [--kernel NAME] KEY_FILE OUT_JSON SQ_CSV [SQ_CSV ...]
+  NAME: k_trace_packet (default) or k_paths
 """
 import collections
 import csv
@@ -20,33 +29,42 @@ import sys
 
 
 def counting(name):
-    """k_trace_packet<W, SP, K, COUNT, FUSED>: the COUNT instantiation is the
-    counting pass, not the timed kernel."""
-    m = re.search(r"k_trace_packet<\d+, \d+, \d+, (true|false)", name)
+    """k_trace_packet<W, SP, K, COUNT, FUSED> / k_paths<W, S, COUNT, ...>: the
+    COUNT instantiation is the counting pass, not the timed kernel."""
+    m = re.search(r"k_trace_packet<\d+, \d+, \d+, (true|false)", name) or \
+        re.search(r"k_paths<\d+, \d+, (true|false)", name)
     return bool(m and m.group(1) == "true")
 
 
 def main():
-    key_file, out = sys.argv[1:3]
+    args = sys.argv[1:]
+    kernel = "k_trace_packet"
+    if args and args[0] == "--kernel":
+        kernel = args[1]
+        args = args[2:]
+    key_file, out = args[:2]
     tot = collections.defaultdict(float)
     disp = collections.defaultdict(set)
-    for path in sys.argv[3:]:
+    for path in args[2:]:
         for r in csv.DictReader(open(path)):
             n = r["Kernel_Name"]
-            if "k_trace_packet" not in n or counting(n):
+            if kernel + "<" not in n or counting(n):
                 continue
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
             disp[r["Counter_Name"]].add((path, r["Dispatch_Id"]))
     per = {c: tot[c] / max(len(disp[c]), 1) for c in tot}  # per dispatch
     cycles = per["GRBM_GUI_ACTIVE"] / 8.0
     valu = per["SQ_INSTS_VALU"]
+    salu = per.get("SQ_INSTS_SALU")
     res = {
         "workload_key": open(key_file).read().strip(),
-        "kernel": "k_trace_packet",
+        "kernel": kernel,
         "valu_insts_per_launch": valu,
-        "salu_insts_per_launch": per.get("SQ_INSTS_SALU"),
+        "salu_insts_per_launch": salu,
         "cycles_per_xcd": cycles,
         "valu_busy": round(valu * 2.0 / (1024.0 * cycles), 4),
+        **({"issue": round((valu * 2.0 + salu) / (1024.0 * cycles), 4),
+            "salu_share": round(salu / (1024.0 * cycles), 4)} if salu else {}),
         "wave_cycles_split": {k: round(per[k] / per["SQ_WAVE_CYCLES"], 4)
                               for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
                                         "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_ANY") if k in per},

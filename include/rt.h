@@ -34,6 +34,24 @@
  * HIP work.  Counting passes (RT_FLAG_COUNT) and the modes that use the
  * replica-wide candidate lists are ordered after every earlier launch.
  * rt_scene_destroy must not race with other calls on the same scene.
+ *
+ * Deviations from the boundary SURVEY.md §8(b) sketched (deliberate):
+ *  - rt_render_frame_cpu is absent.  The library has no CPU render path of
+ *    any kind, so nothing can fall back to one; the CPU baseline is the
+ *    reference's own traversal compiled -O3 from its headers (oracle/_ref,
+ *    test and bench infrastructure only).
+ *  - Samples per pixel and the seed are not rt_camera fields.  spp travels as
+ *    an argument of the entry points that take samples
+ *    (rt_render_batch_spp_device, rt_render_shard_device,
+ *    rt_render_batch_multi, rt_render_paths_device); stratified samples need
+ *    no seed, and the path tracer's hash seed is the `frame` argument.
+ *    rt_camera keeps the reference's Camera fields (camera.hpp:20-38) plus
+ *    the image size.
+ *  - SURVEY's mode PARITY_FP64 | FAST_FP32 maps to RT_MODE_FP64 (fp64
+ *    traversal of the reference tree throughout) | RT_MODE_EXACT (fp32
+ *    conservative traversal with the fp64 reference tests at the leaves).
+ *    Both return the reference's results bit for bit; FAST_FP32 in the survey
+ *    allowed a tolerance this library does not need.
  */
 #ifndef RT_MI355X_H
 #define RT_MI355X_H
@@ -60,7 +78,8 @@ extern "C" {
 #define RT_ALGO_SAH 1
 #define RT_ALGO_BSAH 2
 
-/* traversal modes: both are exact (identical results); they differ in speed */
+/* traversal modes: both are exact (identical results); they differ in speed
+ * (SURVEY.md §8(b)'s FAST_FP32 / PARITY_FP64) */
 #define RT_MODE_EXACT 0 /* fp32 conservative traversal + fp64 reference leaf tests */
 #define RT_MODE_FP64 1  /* fp64 traversal throughout (simple, slower)          */
 
@@ -337,7 +356,12 @@ int rt_render_batch_spp_device(rt_scene *s, int device, const rt_camera *cams, i
  * Per pixel (i, j) and sample s: hash-seeded sub-pixel offset (frame, pixel,
  * sample), 1 + bounces segments, cosine-weighted bounces, radiance
  * sum_k 0.5^k * shadeScreen colour of vertex k (light at the camera); the
- * pixel colour is the mean over samples cast as saveScreen does.  Outputs:
+ * pixel colour is the mean over samples cast as saveScreen does.
+ * RT_FLAG_SHADOW: vertex k >= 1 adds its colour only if no triangle passes the
+ * reference's Moller-Trumbore test on the segment from the light (the camera
+ * position C) to the vertex p, at t < |p - C| (1 - 2^-20) along the unit
+ * direction (p - C) / |p - C| — one occlusion ray per bounce vertex; the
+ * primary vertex is the camera ray's own hit and casts none.  Outputs:
  * rgb per pixel; hit_id / dist / pos of the primary segment per sample at
  * (row * width + i) * spp + s; hit_count += samples whose primary ray hit.
  * Row shard as rt_render_rows_device; asynchronous on `stream`.  flags:

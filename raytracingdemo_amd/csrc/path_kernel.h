@@ -288,19 +288,29 @@ constexpr double kShadowScale = 1.0 - 0x1p-20;
 template <int W, int S, bool QN>
 __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFrameCam& cam, double px, double py,
                                               double pz, LaneStack<S>& st) {
-    const double ex = px - cam.pos[0], ey = py - cam.pos[1], ez = pz - cam.pos[2];
-    const double len = __builtin_sqrt(ex * ex + ey * ey + ez * ez);
-    if (!(len > 0.0)) return false;
-    Ray64 r;
-    r.ox = cam.pos[0];
-    r.oy = cam.pos[1];
-    r.oz = cam.pos[2];
-    r.dx = ex / len;
-    r.dy = ey / len;
-    r.dz = ez / len;
-    r.ix = r.iy = r.iz = 0.0;
+    // the fp64 ray, built again for the rare fp64 test rather than held
+    // (12 VGPRs) through the walk
+    auto ray_of = [&](double& len) {
+        const double ex = px - cam.pos[0], ey = py - cam.pos[1], ez = pz - cam.pos[2];
+        len = __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+        Ray64 r;
+        r.ox = cam.pos[0];
+        r.oy = cam.pos[1];
+        r.oz = cam.pos[2];
+        r.dx = ex / len;
+        r.dy = ey / len;
+        r.dz = ez / len;
+        r.ix = r.iy = r.iz = 0.0;
+        return r;
+    };
+    double len;
+    Ray32 q;
+    {
+        const Ray64 r = ray_of(len);
+        if (!(len > 0.0)) return false;
+        q = make_ray32<true>(r, ray_pad(sc, r));
+    }
     const double tmax = len * kShadowScale;
-    const Ray32 q = make_ray32<true>(r, ray_pad(sc, r));
     const float tcert = (float)(tmax * 0.999);
     LaneCounts lc;
     LaneWalk<W, S, 1, false, QN> w;
@@ -319,8 +329,8 @@ __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFram
             const int cls = tri_classify(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, w.tcull, tl, tu);
             if (cls == 2 && tu < tcert) return true;
             if (cls != 0) {
-                double t;
-                if (mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, r, t) && t < tmax) return true;
+                double t, l2;
+                if (mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, ray_of(l2), t) && t < tmax) return true;
             }
         }
         w.pop_next(st);

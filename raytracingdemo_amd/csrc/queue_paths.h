@@ -1,0 +1,437 @@
+// Queued diffuse path tracing (config c5; SURVEY.md §8(f) item 3: a
+// wavefront path tracer with compacted bounce queues and occlusion rays).
+// Included by render.hip after path_kernel.h.  The path model is
+// path_kernel.h's, bit for bit: every fp64 expression is the
+// megakernel's in the same order, so the outputs equal k_paths' and the
+// oracle's (orc_render_paths).
+//
+// A pose is traced segment by segment over ALL its paths (W x rows x spp of
+// them, up to 132.7 M at config c5: the state of every path of the pose lives
+// in HBM, 80 B per queued ray, sized for MI355X's 288 GB):
+//   k_q_primary   persistent waves over packed tiles (every sample of 64 / spp
+//                 pixels, or 8 x 8 pixels of one sample): the wave-cooperative
+//                 walk of the 64 primary rays (path_kernel.h wave_walk), the
+//                 exact resolve per lane, the per-sample outputs, the primary
+//                 vertex's colour, and the first bounce ray appended to queue
+//                 0 — compacted: one atomic per wave, paths that missed drop out;
+//   k_q_segment   segment b = 1 .. bounces: persistent waves pull 64 queued
+//                 rays at a time; per lane the fp32 walk of the quantised
+//                 nodes (lane_walk), the exact fp64 resolve, the occlusion ray
+//                 toward the head-light (SHADOW, lane_occluded), the vertex
+//                 colour added to the path's radiance, and the next bounce ray
+//                 appended to the other queue (compacted again).  A lane whose
+//                 candidate list overflowed, or whose winner the reference
+//                 tree cannot see, goes on the segment's fall-back list;
+//   k_q_fallback  those rays through the exact per-lane traversal (trace_core)
+//                 and the same epilogue (kept out of k_q_segment, whose
+//                 registers it would raise for ~1e-4 of the rays);
+//   k_q_accum     per pixel the paths' final radiance summed in sample order,
+//                 the colour cast as saveScreen.
+// The path state a ray carries (its radiance so far) travels in its queue
+// entry; a path that ends (miss, or its last segment) leaves its radiance in
+// Lfin.  Kernel ordering on the stream replaces every device-wide barrier; the
+// control words (queue counts, pull cursors, fall-back counts: one per segment,
+// each on its own 64-B line) are zeroed once per pose by the host.
+#pragma once
+
+#ifndef RT_Q_WPE
+#define RT_Q_WPE 5  // waves per SIMD of k_q_segment (register cap 96; the compiler ignores 6 with 24 KB of LDS per block)
+#endif
+#ifndef RT_Q_K
+#define RT_Q_K 4  // LDS candidates per lane in k_q_segment
+#endif
+#ifndef RT_Q_STACK
+#define RT_Q_STACK 8  // LDS stack ring entries per lane in k_q_segment
+#endif
+
+// Control words (u32, RT_QC_STRIDE apart): per segment b = 0 .. bounces,
+//   emit(b)  rays segment b appended to queue b & 1 (segment b + 1's input)
+//   pull(b)  pull cursor of segment b's kernel (primary: tile cursor)
+//   fb(b)    fall-back entries segment b listed
+#define RT_QC_STRIDE 16
+__device__ __forceinline__ RT_G uint32_t* qc_emit(const PathQs& q, int b) { return q.ctl + (3 * b) * RT_QC_STRIDE; }
+__device__ __forceinline__ RT_G uint32_t* qc_pull(const PathQs& q, int b) { return q.ctl + (3 * b + 1) * RT_QC_STRIDE; }
+__device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) { return q.ctl + (3 * b + 2) * RT_QC_STRIDE; }
+
+// Queue entry e of queue k: 10 doubles {o, d, L, path | pad}.
+constexpr int kQDoubles = 10;
+__device__ __forceinline__ RT_G double* q_entry(const PathQs& q, int k, uint32_t e) {
+    return q.q[k] + (size_t)kQDoubles * e;
+}
+__device__ __forceinline__ void q_load(const PathQs& q, int k, uint32_t e, Ray64& r, double L[3], uint32_t& path) {
+    const RT_G double* p = q_entry(q, k, e);
+    r.ox = p[0];
+    r.oy = p[1];
+    r.oz = p[2];
+    r.dx = p[3];
+    r.dy = p[4];
+    r.dz = p[5];
+    r.ix = r.iy = r.iz = 0.0;
+    L[0] = p[6];
+    L[1] = p[7];
+    L[2] = p[8];
+    path = (uint32_t)__double_as_longlong(p[9]);
+}
+
+// Appends each emitting lane's bounce ray (origin, direction, path) to queue
+// k with one atomic per wave (the compaction: lanes whose paths ended append
+// nothing) and returns the lane's entry; the radiance is written after the
+// occlusion test (q_light).  Every lane of the wave calls it.
+__device__ __forceinline__ uint32_t q_append(const PathQs& q, int k, RT_G uint32_t* cnt, bool emit, const Ray64& nr,
+                                             uint32_t path) {
+    const uint64_t em = __ballot(emit);
+    if (em == 0) return 0;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __builtin_ctzll(em);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__builtin_popcountll(em));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    const uint32_t slot = base + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1ull));
+    if (emit) {
+        RT_G double* p = q_entry(q, k, slot);
+        p[0] = nr.ox;
+        p[1] = nr.oy;
+        p[2] = nr.oz;
+        p[3] = nr.dx;
+        p[4] = nr.dy;
+        p[5] = nr.dz;
+        p[9] = __longlong_as_double((long long)path);
+    }
+    return slot;
+}
+
+// Sample index of a path -> its pixel's image coordinates and the hash seed.
+__device__ __forceinline__ uint32_t q_seed(const RtFrameParams& fp, uint32_t frame, uint32_t path) {
+    const uint32_t spp = (uint32_t)fp.spp;
+    const uint32_t pix = path / spp, s = path - pix * spp;
+    const int i = (int)(pix % (uint32_t)fp.W), r = (int)(pix / (uint32_t)fp.W);
+    const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
+    return path_seed(frame, (uint32_t)j * (uint32_t)fp.W + (uint32_t)i, s);
+}
+
+// A segment's vertex, first half (k_paths' loop body after the trace): the
+// hit point and, with bounces left, the next bounce ray (emit).  ray: the
+// segment's ray (o, d); win: its exact closest hit (tri >= 0).
+__device__ __forceinline__ void q_bounce(const RtDevScene& sc, const RtFrameParams& fp, uint32_t frame, int b,
+                                         int bounces, const Ray64& ray, const Win& win, uint32_t path, double& px,
+                                         double& py, double& pz, bool& emit, Ray64& nr) {
+    (void)hit_dist(ray, win.t, px, py, pz);
+    emit = b < bounces;
+    if (!emit) return;
+    const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)win.tri;
+    const uint32_t seed = q_seed(fp, frame, path);
+    bounce_dir(T[RT_T64_NORMAL], T[RT_T64_NORMAL + 1], T[RT_T64_NORMAL + 2], ray.dx, ray.dy, ray.dz,
+               path_u(seed, 2u + 2u * (uint32_t)b), path_u(seed, 3u + 2u * (uint32_t)b), nr.dx, nr.dy, nr.dz);
+    nr.ox = px;
+    nr.oy = py;
+    nr.oz = pz;
+}
+
+// Second half: the vertex adds 0.5^b of its shadeScreen colour to the path's
+// radiance L if the light sees it (SHADOW, b > 0: lane_occluded; vertex 0
+// always), and the radiance goes to the bounce ray's entry (emit: queue kout,
+// entry slot) or, when the path ends here, to Lfin.  tri < 0: a miss, the
+// path ends with L as it is.  L is read from the segment's own queue entry
+// (primary: zero), so nothing of the path is held in registers across the
+// walks.
+template <int W, int S, bool SHADOW>
+__device__ __forceinline__ void q_light(const RtDevScene& sc, const PathQs& qs, const RtFrameCam& cam, int b,
+                                        const RT_G double* Lin, int32_t tri, double px, double py, double pz,
+                                        bool emit, int kout, uint32_t slot, uint32_t path, LaneStack<S>& st,
+                                        uint32_t& sh_cast, uint32_t& sh_occ) {
+    bool lit = tri >= 0;
+    if (SHADOW && lit && b > 0) {
+        lit = !lane_occluded<W, S, W == 8 && RT_QNODES>(sc, cam, px, py, pz, st);
+        sh_cast++;
+        sh_occ += !lit;
+    }
+    double L[3] = {0.0, 0.0, 0.0};
+    if (Lin) {
+        L[0] = Lin[0];
+        L[1] = Lin[1];
+        L[2] = Lin[2];
+    }
+    if (lit) {
+        const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)tri;
+        const double w = __builtin_ldexp(1.0, -b);  // 0.5^b: k_paths' repeated halving, exactly
+        double c[3];
+        shade_at(cam, px, py, pz, T[RT_T64_NORMAL], T[RT_T64_NORMAL + 1], T[RT_T64_NORMAL + 2], c);
+        L[0] = L[0] + w * c[0];
+        L[1] = L[1] + w * c[1];
+        L[2] = L[2] + w * c[2];
+    }
+    RT_G double* f = emit ? q_entry(qs, kout, slot) + 6 : qs.Lfin + 3 * (size_t)path;
+    f[0] = L[0];
+    f[1] = L[1];
+    f[2] = L[2];
+}
+
+// Primary segments.  PACK (64 % spp == 0): a unit is every sample of 64 / spp
+// pixels (lane = pixel * spp + sample); else a unit is 8 x 8 pixels of one
+// sample (unit = sample * tiles + tile).  PRIM: the wave-cooperative walk
+// (8-wide trees whose stack bound fits 128 entries), else per lane.
+template <int W, int S, bool COUNT, bool PACK, bool PRIM>
+__global__ void __launch_bounds__(256) RT_PATHS_ATTR k_q_primary(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
+                                                                 PathQs qs, uint32_t frame, int bounces) {
+    static_assert(!PRIM || (W == 8 && RT_PATHS_DEFER), "wave-walked primaries: 8-wide deferred paths");
+    __shared__ uint2 lds[S][256];
+    __shared__ uint2 pcand[RT_PATHS_K][256];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int spp = fp.spp;
+    int tw = 8, th = 8;
+    if constexpr (PACK) {
+        const int P = 64 / spp;
+        tw = 1;
+        while (tw * tw < P) tw <<= 1;
+        th = P / tw;
+    }
+    const int tiles_x = (fp.W + tw - 1) / tw;
+    const int tiles = tiles_x * ((fp.nrows + th - 1) / th);
+    const int units = PACK ? tiles : tiles * spp;
+    LaneStack<S> st;
+    st.attach(lds, aux, tid);
+    const RtFrameCam cam = frame_cam(fp, 0);
+    for (;;) {
+        int unit = 0;
+        if (lane == 0) unit = (int)atomicAdd(qc_pull(qs, 0), 1u);
+        unit = __shfl(unit, 0);
+        if (unit >= units) break;
+        int i, r, s;
+        if constexpr (PACK) {
+            const int pl = lane / spp;
+            s = lane & (spp - 1);
+            i = (unit % tiles_x) * tw + pl % tw;
+            r = (unit / tiles_x) * th + pl / tw;
+        } else {
+            s = unit / tiles;
+            const int t = unit - s * tiles;
+            i = (t % tiles_x) * 8 + (lane & 7);
+            r = (t / tiles_x) * 8 + (lane >> 3);
+        }
+        const bool valid = i < fp.W && r < fp.nrows;
+        const int iv = valid ? i : 0, rv = valid ? r : 0;
+        const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, rv);
+        const uint32_t seed = path_seed(frame, (uint32_t)j * (uint32_t)fp.W + (uint32_t)iv, (uint32_t)s);
+        RtFrameCam c1 = cam;
+        c1.ox = path_u(seed, 0);
+        c1.oy = path_u(seed, 1);
+        const Ray64 ray = gen_ray<false>(fp, c1, iv, j);
+        auto ray_of = [&]() { return with_inv(ray); };
+        LaneCounts lc;
+        Win win;
+        if constexpr (PRIM) {
+            const float pd = ray_pad(sc, ray);
+            const Ray32 q0 = make_ray32<true>(ray, pd);
+            const float tsl = round_up_f(0x1p-40 * ((double)q0.co + 1.0));
+            uint32_t* wstack = reinterpret_cast<uint32_t*>(&lds[0][tid & ~63]);  // 128 u32 of this wave's row
+            float tcull;
+            int nc;
+            bool over;
+            wave_walk<W, RT_PATHS_K, COUNT>(sc, fp, q0, pd, tsl, valid, wstack, pcand, tid, lc, tcull, nc, over);
+            if (valid) {
+                if (over) {
+                    win = trace_core<W, S, COUNT>(sc, ray_of, pd, st, 0, lc);
+                } else if (resolve_cands<COUNT>(sc, ray_of(), [&](int c) { return pcand[c][tid]; }, nc, tcull, win,
+                                                lc) != 0) {
+                    win = trace_core<W, S, COUNT>(sc, ray_of, pd, st, 1, lc);
+                }
+            }
+        } else if (valid) {
+            win = trace_deferred<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES>(sc, ray_of, ray_pad(sc, ray), st,
+                                                                              pcand, lc);
+        }
+        bool emit = false;
+        Ray64 nr;
+        double px = 0.0, py = 0.0, pz = 0.0;
+        const uint32_t path = ((uint32_t)rv * (uint32_t)fp.W + (uint32_t)iv) * (uint32_t)spp + (uint32_t)s;
+        uint32_t hit = 0, sc0 = 0, so0 = 0;
+        if (valid) {
+            if (win.tri >= 0) q_bounce(sc, fp, frame, 0, bounces, ray, win, path, px, py, pz, emit, nr);
+            Best hb;
+            hb.dist = win.dist;
+            hb.rank = win.rank;
+            hb.tri = win.tri;
+            hb.px = px;
+            hb.py = py;
+            hb.pz = pz;
+            store_sample(fp, path, hb, shade_of(sc, win.tri));
+            hit = win.tri >= 0;
+        }
+        const uint32_t slot = q_append(qs, 0, qc_emit(qs, 0), emit, nr, path);
+        if (valid) q_light<W, S, false>(sc, qs, cam, 0, nullptr, win.tri, px, py, pz, emit, 0, slot, path, st, sc0, so0);
+        wave_add<13>(fp.hit_count, hit);
+        if (fp.counters) wave_add<1>(fp.counters, valid ? 1u : 0u);
+        if (COUNT && fp.counters) {
+            wave_add<24>(fp.counters + 1, lc.nodes);
+            wave_add<24>(fp.counters + 6, lc.pre);
+            wave_add<24>(fp.counters + 2, lc.tris);
+            wave_add<24>(fp.counters + 3, lc.chain);
+        }
+    }
+}
+
+// Segment b (1 .. bounces) over queue (b - 1) & 1.  Fall-back entries: the
+// queue slot | 0x80000000 when the walk's list overflowed (trace_core from
+// pass 0), the slot alone when the winner was invisible (from pass 1).
+#if RT_Q_WPE > 0
+#define RT_Q_ATTR __attribute__((amdgpu_waves_per_eu(RT_Q_WPE)))
+#else
+#define RT_Q_ATTR
+#endif
+constexpr uint32_t kQFromPass0 = 0x80000000u;
+template <int W, int S, int K, bool COUNT, bool SHADOW>
+__global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
+                                                             PathQs qs, uint32_t frame, int b, int bounces) {
+    __shared__ uint2 lds[S][256];
+    __shared__ uint2 cand[K][256];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int qin = (b - 1) & 1, qout = b & 1;
+    const uint32_t n = *qc_emit(qs, b - 1);
+    LaneStack<S> st;
+    st.attach(lds, aux, tid);
+    const RtFrameCam cam = frame_cam(fp, 0);
+    uint32_t segs = 0, sh_cast = 0, sh_occ = 0;
+    LaneCounts tot;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(qc_pull(qs, b), 64u);
+        base = (uint32_t)__shfl((int)base, 0);
+        if (base >= n) break;
+        const uint32_t e = base + (uint32_t)lane;
+        const bool act = e < n;
+        bool emit = false, fall = false;
+        Ray64 nr;
+        Win win;
+        win.tri = -1;
+        double px = 0.0, py = 0.0, pz = 0.0;
+        uint32_t path = 0;
+        if (act) {
+            float tcull;
+            int nc;
+            bool over;
+            {
+                // only the fp32 view of the ray lives through the walk
+                Ray64 ray;
+                double L[3];
+                q_load(qs, qin, e, ray, L, path);
+                const float pd = ray_pad(sc, ray);
+                const Ray32 q = make_ray32<true>(ray, pd);
+                const float tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
+                LaneCounts lc;
+                lane_walk<W, S, K, COUNT, W == 8 && RT_QNODES>(sc, q, tsl, st, cand, lc, tcull, nc, over);
+                if (COUNT) {
+                    tot.nodes += lc.nodes;
+                    tot.pre += lc.pre;
+                }
+            }
+            Ray64 ray;
+            double L[3];
+            q_load(qs, qin, e, ray, L, path);  // (the entry again: L1 / L2)
+            uint32_t fe = e | kQFromPass0;
+            fall = over;
+            if (!over) {
+                fe = e;
+                LaneCounts lc;
+                fall = resolve_cands<COUNT>(sc, with_inv(ray), [&](int c) { return cand[c][tid]; }, nc, tcull, win,
+                                            lc) != 0;
+                if (COUNT) {
+                    tot.tris += lc.tris;
+                    tot.chain += lc.chain;
+                }
+            }
+            segs++;
+            if (fall) {
+                qs.fb[qin * (size_t)qs.cap + atomicAdd(qc_fb(qs, b), 1u)] = fe;
+            } else if (win.tri >= 0) {
+                q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
+            }
+        }
+        const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        if (act && !fall)
+            q_light<W, S, SHADOW>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path,
+                                  st, sh_cast, sh_occ);
+    }
+    if (fp.counters) {
+        wave_add<24>(fp.counters, segs);
+        if (SHADOW) {
+            wave_add<24>(fp.counters + 24, sh_cast);
+            wave_add<24>(fp.counters + 25, sh_occ);
+        }
+        if (COUNT) {
+            wave_add<28>(fp.counters + 1, tot.nodes);
+            wave_add<28>(fp.counters + 6, tot.pre);
+            wave_add<28>(fp.counters + 2, tot.tris);
+            wave_add<28>(fp.counters + 3, tot.chain);
+        }
+    }
+}
+
+// Segment b's fall-back list: trace_core, then the same vertex epilogue.
+// Grid-stride with the same trip count for every lane of a wave (the append
+// ballots).
+template <int W, int S, bool COUNT, bool SHADOW>
+__global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs,
+                                                    uint32_t frame, int b, int bounces) {
+    __shared__ uint2 lds[S][256];
+    const int tid = threadIdx.x;
+    const int qin = (b - 1) & 1, qout = b & 1;
+    const uint32_t n = *qc_fb(qs, b);
+    LaneStack<S> st;
+    st.attach(lds, aux, tid);
+    const RtFrameCam cam = frame_cam(fp, 0);
+    const uint32_t stride = gridDim.x * 256u;
+    const uint32_t iters = (n + stride - 1) / stride;
+    uint32_t sh_cast = 0, sh_occ = 0;
+    LaneCounts tot;
+    for (uint32_t it = 0; it < iters; it++) {
+        const uint32_t k = it * stride + blockIdx.x * 256u + (uint32_t)tid;
+        bool emit = false;
+        Ray64 nr;
+        Win win;
+        win.tri = -1;
+        double px = 0.0, py = 0.0, pz = 0.0;
+        uint32_t path = 0, e = 0;
+        if (k < n) {
+            const uint32_t fe = qs.fb[qin * (size_t)qs.cap + k];
+            e = fe & ~kQFromPass0;
+            Ray64 ray;
+            double L[3];
+            q_load(qs, qin, e, ray, L, path);
+            auto ray_of = [&]() { return with_inv(ray); };
+            win = trace_core<W, S, COUNT>(sc, ray_of, ray_pad(sc, ray), st, (fe & kQFromPass0) ? 0 : 1, tot);
+            if (win.tri >= 0) q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
+        }
+        const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        if (k < n)
+            q_light<W, S, SHADOW>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path,
+                                  st, sh_cast, sh_occ);
+    }
+    if (fp.counters) {
+        if (SHADOW) {
+            wave_add<24>(fp.counters + 24, sh_cast);
+            wave_add<24>(fp.counters + 25, sh_occ);
+        }
+        if (COUNT) {
+            wave_add<28>(fp.counters + 1, tot.nodes);
+            wave_add<28>(fp.counters + 2, tot.tris);
+            wave_add<28>(fp.counters + 3, tot.chain);
+        }
+    }
+}
+
+// Pixel colours: the paths' final radiance summed in sample order from 0.0
+// (k_paths' acc), then saveScreen's cast of the mean.
+__global__ void __launch_bounds__(256) k_q_accum(RtFrameParams fp, PathQs qs) {
+    const uint32_t pix = blockIdx.x * 256u + threadIdx.x;
+    if (pix >= (uint32_t)fp.W * (uint32_t)fp.nrows) return;
+    double acc[3] = {0.0, 0.0, 0.0};
+    const RT_G double* f = qs.Lfin + 3 * (size_t)pix * (size_t)fp.spp;
+    for (int s = 0; s < fp.spp; s++) {
+        acc[0] = acc[0] + f[3 * s];
+        acc[1] = acc[1] + f[3 * s + 1];
+        acc[2] = acc[2] + f[3 * s + 2];
+    }
+    store_rgb(fp, pix, acc);
+}

@@ -654,6 +654,7 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
 #include "packet_kernel.h"
 #include "path_kernel.h"
 #include "wavefront_paths.h"
+#include "queue_paths.h"
 
 // Finishes the pixels the packet pipeline handed over (redo list, count in
 // tile_ctr[RT_REDO_COUNT]) with the per-lane exact kernel: from pass 0 after a
@@ -1016,8 +1017,13 @@ int blocks_per_cu_w(uint32_t stack_bound) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_trace_exact<W, kLdsStack, false, 3>, 256, 0) != hipSuccess)
         n = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, k_paths<W, kPathStack>, 256, 0) != hipSuccess) m = 1;
+    int q = 0;  // (the queued segment kernel's persistent grid shares the spill columns)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, k_q_segment<W, RT_Q_STACK, RT_Q_K, false, true>, 256, 0) !=
+        hipSuccess)
+        q = 1;
     (void)stack_bound;
-    return n > m ? n : m;
+    n = n > m ? n : m;
+    return n > q ? n : q;
 }
 template <int W>
 int packet_blocks_per_cu_w() {
@@ -1060,8 +1066,9 @@ int packet_blocks_per_cu(int width) {
 
 // the smallest LDS ring of the per-lane kernels (spill sizing)
 int exact_lds_stack() {
-    const int a = kLdsStack < kPathStack ? kLdsStack : kPathStack;
-    return a < RT_PW_STACK ? a : RT_PW_STACK;
+    int a = kLdsStack < kPathStack ? kLdsStack : kPathStack;
+    a = a < RT_PW_STACK ? a : RT_PW_STACK;
+    return a < RT_Q_STACK ? a : RT_Q_STACK;
 }
 int packet_candidates() { return RT_CAND_LDS; }  // HBM list entries per pixel (spp > 1, wavefront paths)
 bool packet_split(int spp, bool pack) { return needs_cand(spp, pack); }
@@ -1304,6 +1311,88 @@ hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const 
         }
         hipLaunchKernelGGL(k_pw_accum, agrid, blk, 0, s, fp, ws, smp);
     }
+    if (ev) (void)hipEventRecord(ev[1], s);
+    return hipGetLastError();
+}
+
+// Queued path tracing of one pose (queue_paths.h): the primary segments of
+// every path, then per bounce segment the compacted queue and its fall-back
+// list, then the pixel sums.  The control words are zeroed here.
+template <int W>
+void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
+                       uint32_t frame, int bounces, bool shadow, bool count, hipStream_t s) {
+    const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
+    for (int b = 1; b <= bounces; b++) {
+        if constexpr (W == 8) {
+            if (count && shadow) {
+                hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, true, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+                hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, true, true>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+                continue;
+            }
+            if (count) {
+                hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, true, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+                hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, true, false>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+                continue;
+            }
+        }
+        if (shadow) {
+            hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, false, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+            hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, false, true>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+        } else {
+            hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+            hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, false, false>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+        }
+    }
+}
+
+hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
+                          uint32_t frame, int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev) {
+    if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
+    const uint64_t paths = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.spp;
+    if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.spill || aux.grid <= 0 || !qs.ctl ||
+        paths > qs.cap || aux.spill_cap + RT_Q_STACK < sc.stack_bound || aux.spill_cap + kPathStack < sc.stack_bound ||
+        aux.spill_cap + kLdsStack < sc.stack_bound)
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(qs.ctl, 0, RT_QC_WORDS(bounces) * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const bool count = fp.counters != nullptr;
+    const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
+    if (ev) (void)hipEventRecord(ev[0], s);
+    switch (sc.width) {
+        case 2:
+            hipLaunchKernelGGL((k_q_primary<2, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+            launch_q_segments<2>(sc, fp, aux, qs, frame, bounces, shadow, false, s);
+            break;
+        case 4:
+            hipLaunchKernelGGL((k_q_primary<4, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+            launch_q_segments<4>(sc, fp, aux, qs, frame, bounces, shadow, false, s);
+            break;
+        case 8:
+            if (fp.pack && paths_primary_wave(sc)) {
+                if (count)
+                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, true, true, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+                else
+                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, true, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+            } else if (paths_primary_wave(sc)) {
+                if (count)
+                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, true, false, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+                else
+                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, false, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+            } else if (fp.pack) {
+                hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, true, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+            } else {
+                hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+            }
+            launch_q_segments<8>(sc, fp, aux, qs, frame, bounces, shadow, count, s);
+            break;
+        case 16:
+            hipLaunchKernelGGL((k_q_primary<16, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+            launch_q_segments<16>(sc, fp, aux, qs, frame, bounces, shadow, false, s);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(k_q_accum, agrid, blk, 0, s, fp, qs);
     if (ev) (void)hipEventRecord(ev[1], s);
     return hipGetLastError();
 }

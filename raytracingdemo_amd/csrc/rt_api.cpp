@@ -31,6 +31,8 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
                         int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev);
 hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
                            uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev);
+hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
+                          uint32_t frame, int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
 bool packet_takes_job(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count);
 bool packet_split(int spp, bool pack);
@@ -132,6 +134,8 @@ struct Replica {
     uint64_t cand_cap = 0;       // pixels
     void* d_pw = nullptr;        // wavefront path tracer workspace (PathWs), pw_cap paths
     uint64_t pw_cap = 0;
+    void* d_pq = nullptr;        // queued path tracer workspace (PathQs), pq_cap paths
+    uint64_t pq_cap = 0;
     // RT_FLAG_TIMING: events around the traversal kernel per timed launch,
     // read and recycled by rt_frame_stats
     std::vector<std::array<hipEvent_t, 2>> tev;
@@ -250,6 +254,7 @@ void free_replica(Replica& r) {
     }
     if (r.d_cand) hipFree(r.d_cand);
     if (r.d_pw) hipFree(r.d_pw);
+    if (r.d_pq) hipFree(r.d_pq);
     for (auto& a : r.tev)
         for (hipEvent_t e : a) hipEventDestroy(e);
     if (r.ev_out) hipEventDestroy(r.ev_out);
@@ -445,12 +450,42 @@ PathWs ensure_pw(Replica& r, uint64_t P) {
     return ws;
 }
 
-// Paths through the megakernel (default, path_kernel.h k_paths) or the
-// wavefront pipeline (RT_PATHS_WF=1, wavefront_paths.h; bit-identical, but
-// 1.94 vs 2.81 G nominal rays/s on config c5: DESIGN.md §11).
-bool paths_wavefront() {
-    const char* e = std::getenv("RT_PATHS_WF");  // read per call: tests switch it in-process
-    return e && std::atoi(e) != 0;
+// Queued path-tracer workspace for P paths (grown, never shrunk): two
+// segment queues (80 B per entry), the final radiance (24 B per path), two
+// fall-back lists (4 B per path each) and the control words.
+constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4;
+PathQs ensure_pq(Replica& r, uint64_t P) {
+    if (r.pq_cap < P) {
+        quiesce(r);  // earlier launches may still use it
+        if (r.d_pq) HIP_TRY(hipFree(r.d_pq));
+        r.d_pq = nullptr;
+        r.pq_cap = 0;
+        HIP_TRY(hipMalloc(&r.d_pq, P * kPqBytesPerPath + RT_QC_WORDS(64) * sizeof(uint32_t) + 256));
+        r.pq_cap = P;
+    }
+    uint8_t* base = static_cast<uint8_t*>(r.d_pq);
+    const uint64_t c = r.pq_cap;
+    PathQs qs{};
+    qs.q[0] = reinterpret_cast<double*>(base);
+    qs.q[1] = reinterpret_cast<double*>(base + c * 80);
+    qs.Lfin = reinterpret_cast<double*>(base + c * 160);
+    qs.fb = reinterpret_cast<uint32_t*>(base + c * 184);
+    qs.ctl = reinterpret_cast<uint32_t*>(base + align_up<char>(c * 192));
+    qs.cap = (uint32_t)c;
+    return qs;
+}
+
+// Path pipeline (RT_PATHS, read per call: tests switch it in-process):
+// "queue" — the queued tracer (queue_paths.h: compacted segment queues, lean
+// per-segment kernels); "mega" — the megakernel (path_kernel.h k_paths);
+// RT_PATHS_WF=1 — the round-2 wavefront tracer (wavefront_paths.h).
+enum class PathPipe { mega, queue, wf };
+PathPipe path_pipe() {
+    const char* w = std::getenv("RT_PATHS_WF");
+    if (w && std::atoi(w) != 0) return PathPipe::wf;
+    const char* e = std::getenv("RT_PATHS");
+    if (e && e[0] == 'q') return PathPipe::queue;
+    return PathPipe::mega;
 }
 
 void check_camera(const rt_scene* s, const rt_camera* c) {
@@ -1230,7 +1265,14 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             tev = r->tev[r->tev_used++].data();
         }
         hipError_t e;
-        if (paths_wavefront()) {
+        const PathPipe pipe = path_pipe();
+        if (pipe == PathPipe::queue) {
+            const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows * (uint64_t)spp;
+            const PathQs qs = ensure_pq(*r, P);
+            Slot& q = take_slot(*r, st, true);  // (the replica-wide workspace: after every slot's launches)
+            e = rt::launch_paths_q(r->dev, fp, aux_of(*r, q), qs, (uint32_t)frame, bounces,
+                                   (flags & RT_FLAG_SHADOW) != 0, st, tev);
+        } else if (pipe == PathPipe::wf) {
             if (flags & RT_FLAG_SHADOW) return fail(RT_ERR_INVALID_ARGUMENT, "RT_PATHS_WF=1 has no occlusion rays");
             const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows;
             ensure_cand(*r, P);  // candidate lists, stride P

@@ -247,6 +247,17 @@ struct RtFrameParams {
     RtPose pose[RT_MAX_BATCH];    // pose f / spp of sample frame f (104 B each: 36 fit the LDS copy)
 };
 
+// Workspace of the queued path tracer (queue_paths.h), per replica: every
+// path of a pose at once.
+struct PathQs {
+    RT_G double* q[2];     // segment queues, 10 doubles per entry {o, d, L, path}
+    RT_G double* Lfin;     // 3 per path (pixel * spp + sample): radiance when the path ended
+    RT_G uint32_t* fb;     // fall-back lists, [2][cap]: queue slots for the exact per-lane traversal
+    RT_G uint32_t* ctl;    // control words (queue_paths.h qc_*), zeroed per pose
+    uint32_t cap;          // paths (entries per queue)
+};
+#define RT_QC_WORDS(bounces) (3 * ((bounces) + 1) * 16)
+
 // Workspace of the wavefront path tracer (wavefront_paths.h), per replica.
 struct PathWs {
     RT_G double* qray[2];  // segment queues: 8 doubles per entry {o, d, path id (low word of [6]), -}

@@ -567,6 +567,35 @@ def test_paths_shadow_sponza_proxy_band(oracle):
     assert np.array_equal(sh["rgb"], full["rgb"].reshape(H, W, 3)[rows].reshape(-1, 3))
 
 
+@pytest.mark.parametrize("model,spp,bounces,shadow", [("stanford-bunny.obj", 16, 4, True), ("suzanne.obj", 3, 3, True),
+                                                      ("teapot.obj", 4, 2, False), ("stanford-bunny.obj", 1, 0, False)])
+def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, shadow, monkeypatch):
+    """The queued pipeline (RT_PATHS=queue, queue_paths.h: the primary segments
+    by the wave walk, then per bounce one compacted queue of every path's rays,
+    a fall-back list for the exact per-lane traversal, and the pixel sums)
+    renders the same bits as the megakernel and the oracle: packed (spp 16, 4)
+    and one-sample (spp 3, 1) primary tiles, occlusion rays, a strided shard,
+    and the counts of segments and occlusion rays."""
+    tris = golden_scene(model)
+    s = scene(model, "bsah", 8)
+    pos, d = rt.CameraPath(rt.scene_center(tris), 36).circular_path(13)
+    W, H = 61, 37
+    monkeypatch.setenv("RT_PATHS", "mega")
+    mega = _paths_render(s, pos, d, W, H, 13, spp, bounces, shadow=shadow, stats=True)
+    mega_sh = _paths_render(s, pos, d, W, H, 13, spp, bounces, row0=2, stride=3, shadow=shadow)
+    monkeypatch.setenv("RT_PATHS", "queue")
+    q = _paths_render(s, pos, d, W, H, 13, spp, bounces, shadow=shadow, stats=True)
+    q_sh = _paths_render(s, pos, d, W, H, 13, spp, bounces, row0=2, stride=3, shadow=shadow)
+    for k in ("id", "dist", "rgb", "hits"):
+        assert np.array_equal(q[k], mega[k]), k
+        assert np.array_equal(q_sh[k], mega_sh[k]), k
+    for k in ("rays", "shadow_rays", "shadow_occluded"):
+        assert q["stats"][k] == mega["stats"][k], k
+    o = oracle.bvh(tris, "bsah", 8).render_paths(pos, d, W, H, 13, spp, bounces, shadow=shadow)
+    assert np.array_equal(q["rgb"], o["rgb"])
+    assert q["rgb"].max() > 0
+
+
 @pytest.mark.parametrize("model,spp,bounces", [("stanford-bunny.obj", 3, 4), ("teapot.obj", 2, 1)])
 def test_paths_wavefront_matches_megakernel_and_oracle(oracle, model, spp, bounces, monkeypatch):
     """The wavefront pipeline (RT_PATHS_WF=1: walk / shade / accumulate

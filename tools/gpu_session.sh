@@ -89,6 +89,18 @@ for s in $STEPS; do
                done
                python tools/pmc_summary.py gpurun_out/sq/sq*_counter_collection.csv > gpurun_out/sq_summary.txt
                python tools/pmc_valu.py gpurun_out/pmc_key.txt gpurun_out/pmc_valu.json gpurun_out/sq/sq*_counter_collection.csv ;;
+        sqpaths) # the SQ passes of `sq` over one pose of config c5 (bench.py --paths, occlusion rays on)
+               for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
+                           "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD" \
+                           "SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SCRATCH_READ SQ_INSTS_SCRATCH_WRITE" \
+                           "TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
+                   pn=$((${pn:-0}+1))
+                   run sqp$pn 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sqp -o sqp$pn \
+                       -- python bench.py --paths --steps 1 --warmup 0 --no-cpu --key-out gpurun_out/pmcp_key.txt || exit 1
+               done
+               python tools/pmc_summary.py gpurun_out/sqp/sqp*_counter_collection.csv --match k_paths > gpurun_out/sqp_summary.txt
+               python tools/pmc_valu.py --kernel k_paths gpurun_out/pmcp_key.txt gpurun_out/pmc_valu_paths.json \
+                   gpurun_out/sqp/sqp*_counter_collection.csv ;;
         ab)    # A/B over environment settings: AB_ENVS="A=1 B=2;A=3;..." (one bench per entry)
                i=0; IFS=';' read -ra cfgs <<< "${AB_ENVS:-}"
                for c in "${cfgs[@]}"; do i=$((i+1))

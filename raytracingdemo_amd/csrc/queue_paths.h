@@ -49,9 +49,11 @@
 //   pull(b)  pull cursor of segment b's kernel (primary: tile cursor)
 //   fb(b)    fall-back entries segment b listed
 #define RT_QC_STRIDE 16
-__device__ __forceinline__ RT_G uint32_t* qc_emit(const PathQs& q, int b) { return q.ctl + (3 * b) * RT_QC_STRIDE; }
-__device__ __forceinline__ RT_G uint32_t* qc_pull(const PathQs& q, int b) { return q.ctl + (3 * b + 1) * RT_QC_STRIDE; }
-__device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) { return q.ctl + (3 * b + 2) * RT_QC_STRIDE; }
+//   sh(b)    occlusion records segment b appended (queued shadows)
+__device__ __forceinline__ RT_G uint32_t* qc_emit(const PathQs& q, int b) { return q.ctl + (4 * b) * RT_QC_STRIDE; }
+__device__ __forceinline__ RT_G uint32_t* qc_pull(const PathQs& q, int b) { return q.ctl + (4 * b + 1) * RT_QC_STRIDE; }
+__device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) { return q.ctl + (4 * b + 2) * RT_QC_STRIDE; }
+__device__ __forceinline__ RT_G uint32_t* qc_sh(const PathQs& q, int b) { return q.ctl + (4 * b + 3) * RT_QC_STRIDE; }
 
 // Queue entry e of queue k: 10 doubles {o, d, L, path | pad}.
 constexpr int kQDoubles = 10;
@@ -134,16 +136,26 @@ __device__ __forceinline__ void q_bounce(const RtDevScene& sc, const RtFramePara
 // path ends with L as it is.  L is read from the segment's own queue entry
 // (primary: zero), so nothing of the path is held in registers across the
 // walks.
-template <int W, int S, bool SHADOW>
+// SH: 0 no occlusion rays, 1 the occlusion ray walked here (per lane), 2
+// queued: the radiance without this vertex goes to its destination now and
+// the occlusion record is returned in `queue` (q_shadow_append; the binned
+// occlusion pass adds the colour if the light sees the vertex).
+template <int W, int S, int SH>
 __device__ __forceinline__ void q_light(const RtDevScene& sc, const PathQs& qs, const RtFrameCam& cam, int b,
                                         const RT_G double* Lin, int32_t tri, double px, double py, double pz,
                                         bool emit, int kout, uint32_t slot, uint32_t path, LaneStack<S>& st,
-                                        uint32_t& sh_cast, uint32_t& sh_occ) {
+                                        uint32_t& sh_cast, uint32_t& sh_occ, bool& queue, uint32_t& dst) {
     bool lit = tri >= 0;
-    if (SHADOW && lit && b > 0) {
+    queue = false;
+    dst = emit ? (0x80000000u | ((uint32_t)kout << 30) | slot) : path;
+    if (SH == 1 && lit && b > 0) {
         lit = !lane_occluded<W, S, W == 8 && RT_QNODES>(sc, cam, px, py, pz, st);
         sh_cast++;
         sh_occ += !lit;
+    }
+    if (SH == 2 && lit && b > 0) {
+        queue = true;
+        lit = false;
     }
     double L[3] = {0.0, 0.0, 0.0};
     if (Lin) {
@@ -164,6 +176,336 @@ __device__ __forceinline__ void q_light(const RtDevScene& sc, const PathQs& qs, 
     f[0] = L[0];
     f[1] = L[1];
     f[2] = L[2];
+}
+
+// Radiance destination of a queued occlusion record: a queue entry's L
+// (bit 31, queue in bit 30, entry below) or the path's Lfin.
+__device__ __forceinline__ RT_G double* q_dst(const PathQs& qs, uint32_t dst) {
+    if (dst & 0x80000000u) return q_entry(qs, (dst >> 30) & 1u, dst & 0x3FFFFFFFu) + 6;
+    return qs.Lfin + 3 * (size_t)dst;
+}
+
+// Appends the lanes' occlusion records {p, tri, dst} to srec[0] (one atomic
+// per wave); every lane of the wave calls it.
+__device__ __forceinline__ void q_shadow_append(const PathQs& qs, int b, bool queue, double px, double py, double pz,
+                                                int32_t tri, uint32_t dst) {
+    const uint64_t em = __ballot(queue);
+    if (em == 0) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __builtin_ctzll(em);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(qc_sh(qs, b), (uint32_t)__builtin_popcountll(em));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    if (!queue) return;
+    RT_G double* r = qs.srec[0] + 4 * (size_t)(base + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1ull)));
+    r[0] = px;
+    r[1] = py;
+    r[2] = pz;
+    r[3] = __longlong_as_double((long long)(((uint64_t)dst << 32) | (uint32_t)tri));
+}
+
+// Bin of an occlusion ray: the cube-map tile (RT_SH_G x RT_SH_G per face) of
+// its direction from the light.  Only the order of the occlusion pass depends
+// on it, never a result.
+__device__ __forceinline__ uint32_t sh_bin(const RtFrameCam& cam, double px, double py, double pz) {
+    const float dx = (float)(px - cam.pos[0]), dy = (float)(py - cam.pos[1]), dz = (float)(pz - cam.pos[2]);
+    const float ax = __builtin_fabsf(dx), ay = __builtin_fabsf(dy), az = __builtin_fabsf(dz);
+    uint32_t face;
+    float u, v, m;
+    if (ax >= ay && ax >= az) {
+        face = dx < 0.f ? 1u : 0u;
+        m = ax; u = dy; v = dz;
+    } else if (ay >= az) {
+        face = dy < 0.f ? 3u : 2u;
+        m = ay; u = dx; v = dz;
+    } else {
+        face = dz < 0.f ? 5u : 4u;
+        m = az; u = dx; v = dy;
+    }
+    const float s = m > 0.f ? 0.5f * (float)RT_SH_G / m : 0.f;
+    int iu = (int)((u + m) * s), iv = (int)((v + m) * s);
+    iu = iu < 0 ? 0 : iu >= RT_SH_G ? RT_SH_G - 1 : iu;
+    iv = iv < 0 ? 0 : iv >= RT_SH_G ? RT_SH_G - 1 : iv;
+    return (face * RT_SH_G + (uint32_t)iv) * RT_SH_G + (uint32_t)iu;
+}
+
+// Binning of segment b's occlusion records (a counting sort by sh_bin; the
+// order inside a bin is whatever the LDS atomics give): block k of
+// RT_SH_BLOCKS takes records [k n / NB, (k+1) n / NB).
+__device__ __forceinline__ void sh_range(uint32_t n, uint32_t k, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)((uint64_t)n * k / RT_SH_BLOCKS);
+    hi = (uint32_t)((uint64_t)n * (k + 1) / RT_SH_BLOCKS);
+}
+__global__ void __launch_bounds__(1024) k_sh_hist(RtFrameParams fp, PathQs qs, int b) {
+    __shared__ uint32_t h[RT_SH_BINS];
+    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) h[i] = 0;
+    __syncthreads();
+    const RtFrameCam cam = frame_cam(fp, 0);
+    uint32_t lo, hi;
+    sh_range(*qc_sh(qs, b), blockIdx.x, lo, hi);
+    for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
+        const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
+        atomicAdd(&h[sh_bin(cam, r[0], r[1], r[2])], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x] = h[i];
+}
+// Exclusive scan of bhist in place, bin-major (one block: each thread scans a
+// contiguous run, then the runs' totals are scanned in LDS).
+__global__ void __launch_bounds__(1024) k_sh_scan(PathQs qs) {
+    constexpr uint32_t N = RT_SH_BINS * RT_SH_BLOCKS, R = N / 1024;
+    static_assert(N % 1024 == 0 && R % 4 == 0, "scan runs of whole uint4s");
+    __shared__ uint32_t part[1024];
+    RT_G uint4* run = reinterpret_cast<RT_G uint4*>(qs.bhist + (size_t)threadIdx.x * R);
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < R / 4; k++) {
+        const uint4 v = run[k];
+        sum += v.x + v.y + v.z + v.w;
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the run totals
+        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t acc = part[threadIdx.x] - sum;
+    for (uint32_t k = 0; k < R / 4; k++) {
+        uint4 v = run[k];
+        const uint32_t a = acc, b2 = a + v.x, c = b2 + v.y, d = c + v.z;
+        acc = d + v.w;
+        v.x = a;
+        v.y = b2;
+        v.z = c;
+        v.w = d;
+        run[k] = v;
+    }
+}
+__global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs, int b) {
+    __shared__ uint32_t cur[RT_SH_BINS];
+    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) cur[i] = qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x];
+    __syncthreads();
+    const RtFrameCam cam = frame_cam(fp, 0);
+    uint32_t lo, hi;
+    sh_range(*qc_sh(qs, b), blockIdx.x, lo, hi);
+    for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
+        const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
+        const double x = r[0], y = r[1], z = r[2], w = r[3];
+        RT_G double* o = qs.srec[1] + 4 * (size_t)atomicAdd(&cur[sh_bin(cam, x, y, z)], 1u);
+        o[0] = x;
+        o[1] = y;
+        o[2] = z;
+        o[3] = w;
+    }
+}
+
+// The wave-cooperative any-hit walk of 64 occlusion rays that share the light
+// as origin (one bin's worth of directions): wave_walk's loop with the
+// scalar child records and `ballot`, each lane's interval [0, tmax]; a lane
+// stops (its interval emptied) at its first occluder: tri_classify's certain
+// class with an upper bound below 0.999 tmax, or the fp64 test of any other
+// survivor (lane_occluded's rule, same answer).  The walk ends when every
+// lane has stopped or the stack is empty.  Returns the lane's occlusion.
+template <int W>
+__device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameCam& cam, double px, double py,
+                                            double pz, bool valid, uint32_t* __restrict__ wstack) {
+    auto ray_of = [&](double& len) {
+        const double ex = px - cam.pos[0], ey = py - cam.pos[1], ez = pz - cam.pos[2];
+        len = __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+        Ray64 r;
+        r.ox = cam.pos[0];
+        r.oy = cam.pos[1];
+        r.oz = cam.pos[2];
+        r.dx = ex / len;
+        r.dy = ey / len;
+        r.dz = ez / len;
+        r.ix = r.iy = r.iz = 0.0;
+        return r;
+    };
+    double len = 0.0;
+    Ray32 q;
+    float pd;
+    {
+        const Ray64 r = ray_of(len);
+        valid = valid && len > 0.0;
+        pd = ray_pad(sc, r);
+        q = make_ray32<true>(r, pd);
+    }
+    const double tmax = len * kShadowScale;
+    const float tcert = (float)(tmax * 0.999);
+    float tcull = valid ? round_up_f(tmax) : -1.f;
+    bool occ = false;
+    const uint32_t lsg = (q.ix < 0.f ? 1u : 0u) | (q.iy < 0.f ? 2u : 0u) | (q.iz < 0.f ? 4u : 0u);
+    const uint32_t dsg = uni(lsg);
+    const int oct = __ballot(valid && lsg != dsg) == 0 ? (int)dsg : 8;
+    const f2 nox{-(q.ox + pd) * q.ix, -(q.ox - pd) * q.ix};
+    const f2 noy{-(q.oy + pd) * q.iy, -(q.oy - pd) * q.iy};
+    const f2 noz{-(q.oz + pd) * q.iz, -(q.oz - pd) * q.iz};
+    uint32_t cur = sc.root_ref;
+    if (!(cur & RT_LEAF_BIT)) cur |= sc.root_meta << 24;
+    {
+        float bb[1][6];
+        for (int a = 0; a < 6; a++) bb[0][a] = sc.root_box[a];
+        uint64_t h[1];
+        child_hits<1, -1>(bb, q, nox, noy, noz, tcull, h);
+        if (h[0] == 0) cur = RT_INVALID_REF;
+    }
+    int sp = 0;
+    const RT_G uint8_t* const nodes = sc.nodes;
+    const RT_G float* const tri32 = sc.tri32;
+    auto walk = [&]<int OCT>() __attribute__((always_inline)) {
+        if (cur == RT_INVALID_REF) return;
+        for (;;) {
+            if (!(cur & RT_LEAF_BIT)) {
+                float bx[W][6];
+                uint32_t rs[W];
+                const uint32_t meta = cur >> 24;
+                uint64_t hm[W];
+                {
+                    const cchild_p nb = (cchild_p)(nodes + (size_t)(cur & 0x00FFFFFFu) * (32 * W));
+                    ChildRec ch[W];
+#pragma unroll
+                    for (int c = 0; c < W; c++) ch[c] = load_child(nb + c);
+#pragma unroll
+                    for (int c = 0; c < W; c++) {
+                        bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;
+                        bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
+                    }
+#pragma unroll
+                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref | (ch[c].pad << 24);
+                    child_hits<W, OCT>(bx, q, nox, noy, noz, tcull, hm);
+                }
+                const uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);
+                if (mask != 0) {
+                    const bool rev = (dsg >> (meta & 3u)) & 1u;
+                    const int near_c = rev ? 31 - __builtin_clz(mask) : __builtin_ctz(mask);
+                    const uint32_t pm = mask & ~(1u << near_c);
+                    if (pm != 0) {
+                        const uint32_t refv = lanes_of<W>(rs);
+                        const uint32_t lid = mbcnt_lo(~0u);
+                        const uint32_t below = mbcnt_lo(pm);
+                        const uint32_t mine = (pm >> (lid & 31u)) & 1u;
+                        const uint32_t above = (uint32_t)__builtin_popcount(pm) - below - mine;
+                        const int slot = (int)(rev ? below : above);
+                        if (mine & (lid < (uint32_t)W)) wstack[sp + slot] = refv;
+                        sp += __builtin_popcount(pm);
+                    }
+                    uint32_t nr = rs[0];
+#pragma unroll
+                    for (int c = 1; c < W; c++) nr = near_c == c ? rs[c] : nr;
+                    cur = nr;
+                    continue;
+                }
+            } else {
+                const uint32_t first = cur & RT_LEAF_FIRST_MASK;
+                const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
+                const uint32_t end = first + cnt;
+                for (uint32_t k0 = first; k0 < end; k0 += kLeafChunk) {
+                    const cfloat_p R = (cfloat_p)(tri32 + 12 * (size_t)k0);
+                    float4 TA[kLeafChunk], TB[kLeafChunk], TC[kLeafChunk];
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        TA[t] = load_f4(R + 12 * t);
+                        TB[t] = load_f4(R + 12 * t + 4);
+                        TC[t] = load_f4(R + 12 * t + 8);
+                    }
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) pin_s(TA[t], TB[t], TC[t]);
+#pragma unroll
+                    for (int t = 0; t < kLeafChunk; t++) {
+                        const uint32_t k = k0 + t;
+                        if (k >= end) break;
+                        float tl, tu;
+                        const int cls = tcull >= 0.f ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy,
+                                                                    q.dz, q.co, tcull, tl, tu)
+                                                     : 0;
+                        if (__ballot(cls != 0) == 0) continue;
+                        if (cls == 0) continue;
+                        bool hit = cls == 2 && tu < tcert;
+                        if (!hit) {
+                            double t, l2;
+                            hit = mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, ray_of(l2), t) && t < tmax;
+                        }
+                        if (hit) {
+                            occ = true;
+                            tcull = -1.f;  // this lane enters no box from now on
+                        }
+                    }
+                }
+                if (__ballot(tcull >= 0.f) == 0) break;  // every ray is occluded (or was never valid)
+            }
+            if (sp == 0) break;
+            sp--;
+            cur = uni(wstack[sp]);
+        }
+    };
+    switch (oct) {
+        case 0: walk.template operator()<0>(); break;
+        case 1: walk.template operator()<1>(); break;
+        case 2: walk.template operator()<2>(); break;
+        case 3: walk.template operator()<3>(); break;
+        case 4: walk.template operator()<4>(); break;
+        case 5: walk.template operator()<5>(); break;
+        case 6: walk.template operator()<6>(); break;
+        case 7: walk.template operator()<7>(); break;
+        default: walk.template operator()<-1>(); break;
+    }
+    return occ;
+}
+
+// Segment b's binned occlusion records, 64 per wave through wave_anyhit; a
+// vertex the light sees adds 0.5^b of its colour to its destination's
+// radiance (the segment kernel wrote the radiance before this vertex there).
+#ifndef RT_SH_WPE
+#define RT_SH_WPE 6  // waves per SIMD of k_sh_walk
+#endif
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_WPE))) k_sh_walk(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
+    __shared__ uint32_t wst[4][128];  // one 128-entry node stack per wave
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t n = *qc_sh(qs, b);
+    const RtFrameCam cam = frame_cam(fp, 0);
+    uint32_t* wstack = wst[tid >> 6];
+    uint32_t occl = 0, cast = 0;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 1, 64u);  // (the pull line's second word)
+        base = (uint32_t)__shfl((int)base, 0);
+        if (base >= n) break;
+        const uint32_t e = base + (uint32_t)lane;
+        const bool act = e < n;
+        double px = 0.0, py = 0.0, pz = 0.0;
+        uint64_t td = 0;
+        if (act) {
+            const RT_G double* r = qs.srec[1] + 4 * (size_t)e;
+            px = r[0];
+            py = r[1];
+            pz = r[2];
+            td = (uint64_t)__double_as_longlong(r[3]);
+        }
+        const bool occ = wave_anyhit<W>(sc, cam, px, py, pz, act, wstack);
+        if (act) {
+            cast++;
+            occl += occ;
+        }
+        if (act && !occ) {
+            const uint32_t tri = (uint32_t)td, dst = (uint32_t)(td >> 32);
+            const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)tri;
+            const double w = __builtin_ldexp(1.0, -b);
+            double c[3];
+            shade_at(cam, px, py, pz, T[RT_T64_NORMAL], T[RT_T64_NORMAL + 1], T[RT_T64_NORMAL + 2], c);
+            RT_G double* L = q_dst(qs, dst);
+            L[0] = L[0] + w * c[0];
+            L[1] = L[1] + w * c[1];
+            L[2] = L[2] + w * c[2];
+        }
+    }
+    if (fp.counters) {
+        wave_add<24>(fp.counters + 24, cast);
+        wave_add<24>(fp.counters + 25, occl);
+    }
 }
 
 // Primary segments.  PACK (64 % spp == 0): a unit is every sample of 64 / spp
@@ -259,7 +601,11 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_q_primary(RtDevScene sc, 
             hit = win.tri >= 0;
         }
         const uint32_t slot = q_append(qs, 0, qc_emit(qs, 0), emit, nr, path);
-        if (valid) q_light<W, S, false>(sc, qs, cam, 0, nullptr, win.tri, px, py, pz, emit, 0, slot, path, st, sc0, so0);
+        if (valid) {
+            bool qd;
+            uint32_t dst;
+            q_light<W, S, 0>(sc, qs, cam, 0, nullptr, win.tri, px, py, pz, emit, 0, slot, path, st, sc0, so0, qd, dst);
+        }
         wave_add<13>(fp.hit_count, hit);
         if (fp.counters) wave_add<1>(fp.counters, valid ? 1u : 0u);
         if (COUNT && fp.counters) {
@@ -280,7 +626,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_q_primary(RtDevScene sc, 
 #define RT_Q_ATTR
 #endif
 constexpr uint32_t kQFromPass0 = 0x80000000u;
-template <int W, int S, int K, bool COUNT, bool SHADOW>
+template <int W, int S, int K, bool COUNT, int SH>
 __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                              PathQs qs, uint32_t frame, int b, int bounces) {
     __shared__ uint2 lds[S][256];
@@ -349,13 +695,16 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
             }
         }
         const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        bool qd = false;
+        uint32_t dst = 0;
         if (act && !fall)
-            q_light<W, S, SHADOW>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path,
-                                  st, sh_cast, sh_occ);
+            q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
+                              sh_cast, sh_occ, qd, dst);
+        if constexpr (SH == 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         wave_add<24>(fp.counters, segs);
-        if (SHADOW) {
+        if (SH == 1) {
             wave_add<24>(fp.counters + 24, sh_cast);
             wave_add<24>(fp.counters + 25, sh_occ);
         }
@@ -371,7 +720,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
 // Segment b's fall-back list: trace_core, then the same vertex epilogue.
 // Grid-stride with the same trip count for every lane of a wave (the append
 // ballots).
-template <int W, int S, bool COUNT, bool SHADOW>
+template <int W, int S, bool COUNT, int SH>
 __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs,
                                                     uint32_t frame, int b, int bounces) {
     __shared__ uint2 lds[S][256];
@@ -404,12 +753,15 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
             if (win.tri >= 0) q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
         }
         const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        bool qd = false;
+        uint32_t dst = 0;
         if (k < n)
-            q_light<W, S, SHADOW>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path,
-                                  st, sh_cast, sh_occ);
+            q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
+                              sh_cast, sh_occ, qd, dst);
+        if constexpr (SH == 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
-        if (SHADOW) {
+        if (SH == 1) {
             wave_add<24>(fp.counters + 24, sh_cast);
             wave_add<24>(fp.counters + 25, sh_occ);
         }

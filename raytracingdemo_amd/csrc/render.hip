@@ -1318,31 +1318,45 @@ hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const 
 // Queued path tracing of one pose (queue_paths.h): the primary segments of
 // every path, then per bounce segment the compacted queue and its fall-back
 // list, then the pixel sums.  The control words are zeroed here.
+template <int W, bool COUNT, int SH>
+void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
+                      uint32_t frame, int b, int bounces, hipStream_t s) {
+    const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
+    hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
+                       bounces);
+    hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, COUNT, SH>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+    if constexpr (SH == 2) {
+        // the segment's occlusion records: binned by direction from the light,
+        // then walked 64 at a time by the wave-cooperative any-hit walk
+        hipLaunchKernelGGL(k_sh_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b);
+        hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
+        hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b);
+        hipLaunchKernelGGL((k_sh_walk<W>), dim3((unsigned)aux.pgrid), blk, 0, s, sc, fp, aux, qs, b);
+    }
+}
+// sh: 0 no occlusion rays, 1 per lane in the segment kernel, 2 queued and binned
 template <int W>
 void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
-                       uint32_t frame, int bounces, bool shadow, bool count, hipStream_t s) {
-    const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
+                       uint32_t frame, int bounces, int sh, bool count, hipStream_t s) {
     for (int b = 1; b <= bounces; b++) {
-        if constexpr (W == 8) {
-            if (count && shadow) {
-                hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, true, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
-                hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, true, true>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
-                continue;
-            }
-            if (count) {
-                hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, true, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
-                hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, true, false>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
-                continue;
-            }
-        }
-        if (shadow) {
-            hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, false, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
-            hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, false, true>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+        if (W == 8 && count) {
+            if (sh == 2) launch_q_segment<W, true, 2>(sc, fp, aux, qs, frame, b, bounces, s);
+            else if (sh == 1) launch_q_segment<W, true, 1>(sc, fp, aux, qs, frame, b, bounces, s);
+            else launch_q_segment<W, true, 0>(sc, fp, aux, qs, frame, b, bounces, s);
         } else {
-            hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
-            hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, false, false>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+            if (sh == 2) launch_q_segment<W, false, 2>(sc, fp, aux, qs, frame, b, bounces, s);
+            else if (sh == 1) launch_q_segment<W, false, 1>(sc, fp, aux, qs, frame, b, bounces, s);
+            else launch_q_segment<W, false, 0>(sc, fp, aux, qs, frame, b, bounces, s);
         }
     }
+}
+
+// Occlusion rays of the queued pipeline: queued and binned (default), or
+// RT_SHADOW_RAYS=lane: walked per lane inside the segment kernel (read per call).
+int queued_shadow_mode(bool shadow) {
+    if (!shadow) return 0;
+    const char* e = getenv("RT_SHADOW_RAYS");
+    return e && e[0] == 'l' ? 1 : 2;
 }
 
 hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
@@ -1356,16 +1370,18 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     hipError_t e = hipMemsetAsync(qs.ctl, 0, RT_QC_WORDS(bounces) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const bool count = fp.counters != nullptr;
+    const int sh = queued_shadow_mode(shadow);
+    if (sh == 2 && (!qs.srec[0] || !qs.srec[1] || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
     if (ev) (void)hipEventRecord(ev[0], s);
     switch (sc.width) {
         case 2:
             hipLaunchKernelGGL((k_q_primary<2, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
-            launch_q_segments<2>(sc, fp, aux, qs, frame, bounces, shadow, false, s);
+            launch_q_segments<2>(sc, fp, aux, qs, frame, bounces, sh, false, s);
             break;
         case 4:
             hipLaunchKernelGGL((k_q_primary<4, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
-            launch_q_segments<4>(sc, fp, aux, qs, frame, bounces, shadow, false, s);
+            launch_q_segments<4>(sc, fp, aux, qs, frame, bounces, sh, false, s);
             break;
         case 8:
             if (fp.pack && paths_primary_wave(sc)) {
@@ -1383,11 +1399,11 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
             } else {
                 hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
             }
-            launch_q_segments<8>(sc, fp, aux, qs, frame, bounces, shadow, count, s);
+            launch_q_segments<8>(sc, fp, aux, qs, frame, bounces, sh, count, s);
             break;
         case 16:
             hipLaunchKernelGGL((k_q_primary<16, kPathStack, false, false, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
-            launch_q_segments<16>(sc, fp, aux, qs, frame, bounces, shadow, false, s);
+            launch_q_segments<16>(sc, fp, aux, qs, frame, bounces, sh, false, s);
             break;
         default:
             return hipErrorInvalidValue;

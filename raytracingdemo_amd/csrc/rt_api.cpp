@@ -453,14 +453,15 @@ PathWs ensure_pw(Replica& r, uint64_t P) {
 // Queued path-tracer workspace for P paths (grown, never shrunk): two
 // segment queues (80 B per entry), the final radiance (24 B per path), two
 // fall-back lists (4 B per path each) and the control words.
-constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4;
+constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4 + 2 * 32;  // (+ the occlusion records, 32 B twice)
 PathQs ensure_pq(Replica& r, uint64_t P) {
     if (r.pq_cap < P) {
         quiesce(r);  // earlier launches may still use it
         if (r.d_pq) HIP_TRY(hipFree(r.d_pq));
         r.d_pq = nullptr;
         r.pq_cap = 0;
-        HIP_TRY(hipMalloc(&r.d_pq, P * kPqBytesPerPath + RT_QC_WORDS(64) * sizeof(uint32_t) + 256));
+        HIP_TRY(hipMalloc(&r.d_pq, P * kPqBytesPerPath + RT_QC_WORDS(64) * sizeof(uint32_t) +
+                                       (uint64_t)RT_SH_BINS * RT_SH_BLOCKS * sizeof(uint32_t) + 1024));
         r.pq_cap = P;
     }
     uint8_t* base = static_cast<uint8_t*>(r.d_pq);
@@ -470,7 +471,12 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
     qs.q[1] = reinterpret_cast<double*>(base + c * 80);
     qs.Lfin = reinterpret_cast<double*>(base + c * 160);
     qs.fb = reinterpret_cast<uint32_t*>(base + c * 184);
-    qs.ctl = reinterpret_cast<uint32_t*>(base + align_up<char>(c * 192));
+    qs.srec[0] = reinterpret_cast<double*>(base + align_up<char>(c * 192));
+    qs.srec[1] = reinterpret_cast<double*>(base + align_up<char>(c * 192) + c * 32);
+    const uint64_t o_ctl = align_up<char>(align_up<char>(c * 192) + c * 64);
+    qs.ctl = reinterpret_cast<uint32_t*>(base + o_ctl);
+    qs.bhist = reinterpret_cast<uint32_t*>(base + align_up<char>(o_ctl + RT_QC_WORDS(64) * sizeof(uint32_t)));
+    qs.sh_blocks = RT_SH_BLOCKS;
     qs.cap = (uint32_t)c;
     return qs;
 }

@@ -255,8 +255,20 @@ struct PathQs {
     RT_G uint32_t* fb;     // fall-back lists, [2][cap]: queue slots for the exact per-lane traversal
     RT_G uint32_t* ctl;    // control words (queue_paths.h qc_*), zeroed per pose
     uint32_t cap;          // paths (entries per queue)
+    // occlusion-ray queue (queued shadows): records {p (3 doubles), tri | dst}
+    // as the segment kernel appends them ([0]) and binned by their direction
+    // from the light ([1]); per-block bin counts of the binning passes
+    RT_G double* srec[2];
+    RT_G uint32_t* bhist;  // [bins][sh_blocks]
+    uint32_t sh_blocks;
 };
-#define RT_QC_WORDS(bounces) (3 * ((bounces) + 1) * 16)
+#define RT_QC_WORDS(bounces) (4 * ((bounces) + 1) * 16)
+// occlusion-ray bins: a cube map around the light, RT_SH_G x RT_SH_G tiles per face
+#ifndef RT_SH_G
+#define RT_SH_G 32
+#endif
+#define RT_SH_BINS (6 * RT_SH_G * RT_SH_G)
+#define RT_SH_BLOCKS 256
 
 // Workspace of the wavefront path tracer (wavefront_paths.h), per replica.
 struct PathWs {

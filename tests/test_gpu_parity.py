@@ -567,15 +567,21 @@ def test_paths_shadow_sponza_proxy_band(oracle):
     assert np.array_equal(sh["rgb"], full["rgb"].reshape(H, W, 3)[rows].reshape(-1, 3))
 
 
-@pytest.mark.parametrize("model,spp,bounces,shadow", [("stanford-bunny.obj", 16, 4, True), ("suzanne.obj", 3, 3, True),
-                                                      ("teapot.obj", 4, 2, False), ("stanford-bunny.obj", 1, 0, False)])
+@pytest.mark.parametrize("model,spp,bounces,shadow", [("stanford-bunny.obj", 16, 4, "queue"),
+                                                      ("suzanne.obj", 3, 3, "queue"), ("suzanne.obj", 3, 3, "lane"),
+                                                      ("teapot.obj", 4, 2, None), ("stanford-bunny.obj", 1, 0, None)])
 def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, shadow, monkeypatch):
     """The queued pipeline (RT_PATHS=queue, queue_paths.h: the primary segments
     by the wave walk, then per bounce one compacted queue of every path's rays,
     a fall-back list for the exact per-lane traversal, and the pixel sums)
     renders the same bits as the megakernel and the oracle: packed (spp 16, 4)
-    and one-sample (spp 3, 1) primary tiles, occlusion rays, a strided shard,
+    and one-sample (spp 3, 1) primary tiles, occlusion rays (queued, binned by
+    direction from the light and walked by the wave-cooperative any-hit walk;
+    or RT_SHADOW_RAYS=lane: per lane in the segment kernel), a strided shard,
     and the counts of segments and occlusion rays."""
+    if shadow:
+        monkeypatch.setenv("RT_SHADOW_RAYS", shadow)
+    shadow = shadow is not None
     tris = golden_scene(model)
     s = scene(model, "bsah", 8)
     pos, d = rt.CameraPath(rt.scene_center(tris), 36).circular_path(13)

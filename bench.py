@@ -81,6 +81,9 @@ def parse():
     p.add_argument("--paths", action="store_true",
                    help="config c5: diffuse path tracing (secondary rays), 16 spp x (1 + 4 bounces) by default")
     p.add_argument("--bounces", type=int, default=4, help="paths: secondary bounces per sample")
+    p.add_argument("--pipeline", default=os.environ.get("RT_PATHS", "queue"), choices=["queue", "mega"],
+                   help="paths: the queued tracer (compacted per-segment queues, binned occlusion rays) or the "
+                        "megakernel (sets RT_PATHS for the library)")
     p.add_argument("--no-shadow", action="store_true",
                    help="paths: no occlusion rays toward the head-light at the bounce vertices (RT_FLAG_SHADOW)")
     p.add_argument("--scene", default="sponza", choices=["sponza", "armadillo"],
@@ -255,6 +258,10 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
 
     W, H, S, B, F = a.width, a.height, a.spp, a.bounces, a.frames
     shadow = not a.no_shadow
+    os.environ["RT_PATHS"] = a.pipeline  # (read by the library per call)
+    queued = a.pipeline == "queue"
+    shadow_mode = ("queued, binned by direction from the light, wave-walked" if queued and
+                   os.environ.get("RT_SHADOW_RAYS", "")[:1] != "l" else "per lane") if shadow else None
     path = rt.CameraPath(rt.scene_center(tris), 36)
     rows = rows_per_rank(H, world, band=1)  # the paths kernel takes single interleaved rows
     my_rows = len(shard_rows(rank, world, H, band=1))
@@ -287,8 +294,23 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
     # winner's 56-B record; 3 B of colour per pixel
     # (primary segments walked by the wave, path_kernel.h wave_walk: 256-B
     # nodes and 48-B triangle records once per wave)
-    alg_pose = (cs["node_fetches"] * 96 + cs["wave_nodes"] * 256 + cs["wave_tris"] * 48 + cs["tri_prefilter"] * 48
+    alg_walk = (cs["node_fetches"] * 96 + cs["wave_nodes"] * 256 + cs["wave_tris"] * 48 + cs["tri_prefilter"] * 48
                 + cs["tri_tests"] * 72 + cs["chain_checks"] * 52 + cs["rays"] * 56) / F + my_rows * W * 3
+    alg_pose, alg_parts = alg_walk, {"walks_and_resolve": round(alg_walk)}
+    if queued:
+        # the queued pipeline's own traffic (queue_paths.h): every bounce ray's
+        # 80-B queue entry written once and read once, every path's final
+        # radiance written and read (24 B each way); every occlusion record
+        # (32 B) written, read by the two binning passes, written binned and
+        # read by the walk, the lit ones' radiance read and written (48 B); the
+        # occlusion walk's wave node steps (256 B) and triangle records (48 B)
+        samples = my_rows * W * S
+        bounce_rays = (cs["rays"] / F) - samples
+        q_bytes = bounce_rays * 160 + samples * 48
+        sh_bytes = (cs["shadow_rays"] * 160 + (cs["shadow_rays"] - cs["shadow_occluded"]) * 48 +
+                    cs["shadow_wave_nodes"] * 256 + cs["shadow_wave_tris"] * 48) / F
+        alg_pose += q_bytes + sh_bytes
+        alg_parts.update({"queues": round(q_bytes), "occlusion": round(sh_bytes)})
     # W warm-up steps, then render-only steps until SETTLE_S of GPU work (main())
     for w in range(a.warmup):
         step(w, timing=True)
@@ -324,7 +346,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         cpu = None
         if world == 1 and not a.no_cpu:
             cpu = paths_cpu_baseline(tris, a, path, W, H, S, B, shadow)
-        key = f"{label}|{W}x{H}|{a.algo}-{a.k}|paths|spp{S}|b{B}|n{world}" + ("|shadow" if shadow else "")
+        key = (f"{label}|{W}x{H}|{a.algo}-{a.k}|paths|spp{S}|b{B}|n{world}" + ("|shadow" if shadow else "")
+               + f"|{a.pipeline}")
         if a.key_out:
             with open(a.key_out, "w") as fh:
                 fh.write(key + "\n")
@@ -360,21 +383,31 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "segments_traced_per_s_M": round(segs_per_pose * a.steps * F / elapsed / 1e6, 2),
             "segments_per_sample": round(segs_per_pose / (W * H * S), 3),
-            "shadow": {"on": shadow, "rays_per_pose": round(cs["shadow_rays"] / F),
+            "pipeline": ("queued: wave-walked primaries, compacted per-segment bounce queues, per-lane bounce walks"
+                         if queued else "megakernel (k_paths)"),
+            "shadow": {"on": shadow, "mode": shadow_mode, "rays_per_pose": round(cs["shadow_rays"] / F),
                        "occluded_per_pose": round(cs["shadow_occluded"] / F),
                        "rays_per_sample": round(cs["shadow_rays"] / F / (W * my_rows * S), 3),
                        "note": "one occlusion ray toward the head-light per bounce vertex (RT_FLAG_SHADOW); not "
                                "counted in value's nominal W*H*spp*(1+bounces)"},
             "kernel_ms_avg": round(ks["trace_ms"] / max(ks["timed_launches"], 1), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_paths",
-                         "alg_bytes_per_launch": round(alg_pose),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": ("queued pipeline (k_q_primary, k_q_segment, k_q_fallback, k_sh_*, k_q_accum; "
+                                    "HIP events around the pose)" if queued else "k_paths"),
+                         "alg_bytes_per_launch": round(alg_pose), "alg_bytes_parts": alg_parts,
                          "per_segment": {k: round(cs[c] / max(cs["rays"], 1), 3) for k, c in
                                          (("node_fetches", "node_fetches"), ("tri_prefilter", "tri_prefilter"),
                                           ("tri_tests_fp64", "tri_tests"), ("chain_checks", "chain_checks"))},
                          "bytes": "per-lane node steps x 96 (quantised) + wave node steps x 256 and wave triangle "
                                   "records x 48 (primary segments walked by the wave) + pre-filter x 48 + fp64 tests "
-                                  "x 72 + chain checks x 52 + segments x 56 + 3 per pixel",
+                                  "x 72 + chain checks x 52 + segments x 56 + 3 per pixel; queued: + 160 per bounce "
+                                  "ray and 48 per sample (queues, final radiance) + per occlusion ray 160 (records "
+                                  "through the binning) + 48 per lit one + its wave walk's node steps x 256 and "
+                                  "triangle records x 48",
+                         "convention": "a record once per fetching wave instruction: the wave walks' (primary, "
+                                       "occlusion) nodes and triangles once per wave, the per-lane bounce walks' "
+                                       "per lane (each lane's node is its own fetch)",
                          "wave_nodes_per_pose": round(cs["wave_nodes"] / F), "wave_tris_per_pose": round(cs["wave_tris"] / F),
                          "valu": valu},
             "cpu_baseline": cpu,

@@ -171,7 +171,9 @@ typedef struct {
     uint64_t shadow_occluded;/*   of which occluded                            */
     uint64_t side_jobs_fused;  /* rt_deinterleave_job: done by the traversal kernel */
     uint64_t side_jobs_kernel; /*   done by a de-interleave kernel after the render */
-    uint64_t reserved[3];
+    uint64_t shadow_wave_nodes;/* queued occlusion rays: wave node steps of the any-hit walk */
+    uint64_t shadow_wave_tris; /*   and triangle records it fetched, once per wave      */
+    uint64_t reserved[1];
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */

@@ -307,9 +307,10 @@ __global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs
 // class with an upper bound below 0.999 tmax, or the fp64 test of any other
 // survivor (lane_occluded's rule, same answer).  The walk ends when every
 // lane has stopped or the stack is empty.  Returns the lane's occlusion.
-template <int W>
+template <int W, bool COUNT>
 __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameCam& cam, double px, double py,
-                                            double pz, bool valid, uint32_t* __restrict__ wstack) {
+                                            double pz, bool valid, uint32_t* __restrict__ wstack, uint32_t& w_nodes,
+                                            uint32_t& w_tris) {
     auto ray_of = [&](double& len) {
         const double ex = px - cam.pos[0], ey = py - cam.pos[1], ez = pz - cam.pos[2];
         len = __builtin_sqrt(ex * ex + ey * ey + ez * ez);
@@ -358,6 +359,7 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
         if (cur == RT_INVALID_REF) return;
         for (;;) {
             if (!(cur & RT_LEAF_BIT)) {
+                if (COUNT) w_nodes++;
                 float bx[W][6];
                 uint32_t rs[W];
                 const uint32_t meta = cur >> 24;
@@ -401,6 +403,7 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
                 const uint32_t first = cur & RT_LEAF_FIRST_MASK;
                 const uint32_t cnt = ((cur >> 27) & 15u) + 1u;
                 const uint32_t end = first + cnt;
+                if (COUNT) w_tris += cnt;
                 for (uint32_t k0 = first; k0 < end; k0 += kLeafChunk) {
                     const cfloat_p R = (cfloat_p)(tri32 + 12 * (size_t)k0);
                     float4 TA[kLeafChunk], TB[kLeafChunk], TC[kLeafChunk];
@@ -460,7 +463,7 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
 #ifndef RT_SH_WPE
 #define RT_SH_WPE 6  // waves per SIMD of k_sh_walk
 #endif
-template <int W>
+template <int W, bool COUNT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_WPE))) k_sh_walk(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
     __shared__ uint32_t wst[4][128];  // one 128-entry node stack per wave
     const int tid = threadIdx.x;
@@ -468,7 +471,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_
     const uint32_t n = *qc_sh(qs, b);
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t* wstack = wst[tid >> 6];
-    uint32_t occl = 0, cast = 0;
+    uint32_t occl = 0, cast = 0, w_nodes = 0, w_tris = 0;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 1, 64u);  // (the pull line's second word)
@@ -485,7 +488,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_
             pz = r[2];
             td = (uint64_t)__double_as_longlong(r[3]);
         }
-        const bool occ = wave_anyhit<W>(sc, cam, px, py, pz, act, wstack);
+        const bool occ = wave_anyhit<W, COUNT>(sc, cam, px, py, pz, act, wstack, w_nodes, w_tris);
         if (act) {
             cast++;
             occl += occ;
@@ -505,6 +508,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_
     if (fp.counters) {
         wave_add<24>(fp.counters + 24, cast);
         wave_add<24>(fp.counters + 25, occl);
+        if (COUNT && lane == 0) {  // (wave-uniform: the walk's node steps and triangle records, once per wave)
+            atomicAdd(&fp.counters[26], (unsigned long long)w_nodes);
+            atomicAdd(&fp.counters[27], (unsigned long long)w_tris);
+        }
     }
 }
 

@@ -1331,7 +1331,7 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
         hipLaunchKernelGGL(k_sh_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b);
         hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
         hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b);
-        hipLaunchKernelGGL((k_sh_walk<W>), dim3((unsigned)aux.pgrid), blk, 0, s, sc, fp, aux, qs, b);
+        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), dim3((unsigned)aux.pgrid), blk, 0, s, sc, fp, aux, qs, b);
     }
 }
 // sh: 0 no occlusion rays, 1 per lane in the segment kernel, 2 queued and binned
@@ -1353,10 +1353,12 @@ void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLa
 
 // Occlusion rays of the queued pipeline: queued and binned (default), or
 // RT_SHADOW_RAYS=lane: walked per lane inside the segment kernel (read per call).
-int queued_shadow_mode(bool shadow) {
+// (The any-hit walk's wave stack holds kPacketStack entries: deeper trees
+// walk their occlusion rays per lane.)
+int queued_shadow_mode(const RtDevScene& sc, bool shadow) {
     if (!shadow) return 0;
     const char* e = getenv("RT_SHADOW_RAYS");
-    return e && e[0] == 'l' ? 1 : 2;
+    return (e && e[0] == 'l') || sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
 }
 
 hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
@@ -1370,7 +1372,7 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     hipError_t e = hipMemsetAsync(qs.ctl, 0, RT_QC_WORDS(bounces) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const bool count = fp.counters != nullptr;
-    const int sh = queued_shadow_mode(shadow);
+    const int sh = queued_shadow_mode(sc, shadow);
     if (sh == 2 && (!qs.srec[0] || !qs.srec[1] || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
     if (ev) (void)hipEventRecord(ev[0], s);

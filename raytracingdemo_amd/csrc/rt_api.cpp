@@ -1437,6 +1437,8 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->wave_winners = c[17];
         out->shadow_rays = c[24];
         out->shadow_occluded = c[25];
+        out->shadow_wave_nodes = c[26];
+        out->shadow_wave_tris = c[27];
         out->side_jobs_fused = r.jobs_fused;
         out->side_jobs_kernel = r.jobs_kernel;
         if (reset) r.jobs_fused = r.jobs_kernel = 0;

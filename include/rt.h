@@ -361,7 +361,7 @@ int rt_render_batch_spp_device(rt_scene *s, int device, const rt_camera *cams, i
  * pixel colour is the mean over samples cast as saveScreen does.
  * RT_FLAG_SHADOW: vertex k >= 1 adds its colour only if no triangle passes the
  * reference's Moller-Trumbore test on the segment from the light (the camera
- * position C) to the vertex p, at t < |p - C| (1 - 2^-20) along the unit
+ * position C) to the vertex p, at t < |p - C| (1 - 2^-12) along the unit
  * direction (p - C) / |p - C| — one occlusion ray per bounce vertex; the
  * primary vertex is the camera ray's own hit and casts none.  Outputs:
  * rgb per pixel; hit_id / dist / pos of the primary segment per sample at

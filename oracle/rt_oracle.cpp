@@ -1025,12 +1025,12 @@ V3 bounce_dir(V3 n, const V3& din, double u1, double u2) {
 // o = C, d = e / |e| with e = p - C (Vector3::normalize's division,
 // vector3.hpp:91-95), length len = |e|.  Occluded iff some triangle of the
 // scene passes the reference's Moller-Trumbore test (triangle.hpp:40-62,
-// EPS 1e-8) with t < len * (1 - 2^-20) — any triangle, whatever the tree: the
-// test is tree-independent (no ancestor-box semantics), and the 2^-20 margin
+// EPS 1e-8) with t < len * (1 - 2^-12) — any triangle, whatever the tree: the
+// test is tree-independent (no ancestor-box semantics), and the 2^-12 margin
 // keeps p's own triangle (t = len up to rounding) and its neighbours through p
 // out.  The traversal only prunes: boxes widened by wpad (far above any fp64
 // rounding of a passing test), interval unclipped.  len = 0: lit.
-constexpr double kShadowScale = 1.0 - 0x1p-20;
+constexpr double kShadowScale = 1.0 - 0x1p-12;
 inline bool box_hit_wide(const V3& mn, const V3& mx, const Ray& r, double w) {
     return box_hit(V3{mn.x - w, mn.y - w, mn.z - w}, V3{mx.x + w, mx.y + w, mx.z + w}, r);
 }

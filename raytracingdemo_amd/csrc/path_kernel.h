@@ -277,14 +277,16 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
 // oracle/rt_oracle.cpp): the ray from the light at the camera C
 // toward p, o = C, d = e / |e| (e = p - C, Vector3::normalize's divisions),
 // is occluded iff some triangle passes the reference's Moller-Trumbore test
-// (triangle.hpp:40-62) with t < |e| (1 - 2^-20) — over all triangles, so any
+// (triangle.hpp:40-62) with t < |e| (1 - 2^-12) — over all triangles, so any
 // tree that finds every candidate gives the same answer.  The fp32 walk of the
 // walk tree (slabs widened by the pad, interval clipped to the fp32 bound of
 // tmax) keeps every triangle the fp64 test could pass; tri_classify's certain
 // class with an upper bound below 0.999 tmax is an occluder outright, any
 // other survivor whose lower bound is within the interval gets the fp64 test.
-// The first occluder ends the walk (any hit, no order needed).
-constexpr double kShadowScale = 1.0 - 0x1p-20;
+// The first occluder ends the walk (any hit, no order needed).  The margin
+// 2^-12 is far wider than the fp32 filter's error budget, so p's own triangle
+// (t = |e| up to rounding) is rejected in fp32 and costs no fp64 test.
+constexpr double kShadowScale = 1.0 - 0x1p-12;
 template <int W, int S, bool QN>
 __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFrameCam& cam, double px, double py,
                                               double pz, LaneStack<S>& st) {

@@ -515,12 +515,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_
     }
 }
 
+// Fall-back entries: the queue slot (segment 0: the path) | kQFromPass0 when
+// the walk's list overflowed (trace_core from pass 0), alone when the winner
+// was invisible (from pass 1).
+constexpr uint32_t kQFromPass0 = 0x80000000u;
+
 // Primary segments.  PACK (64 % spp == 0): a unit is every sample of 64 / spp
 // pixels (lane = pixel * spp + sample); else a unit is 8 x 8 pixels of one
 // sample (unit = sample * tiles + tile).  PRIM: the wave-cooperative walk
 // (8-wide trees whose stack bound fits 128 entries), else per lane.
+// (PRIM: the per-lane stack is not used; S = 1 leaves the LDS to the wave
+// stacks (row 0) and the candidate lists, 10 KB per block)
+#ifndef RT_QP_WPE
+#define RT_QP_WPE 6  // waves per SIMD of k_q_primary (wave-walked)
+#endif
 template <int W, int S, bool COUNT, bool PACK, bool PRIM>
-__global__ void __launch_bounds__(256) RT_PATHS_ATTR k_q_primary(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ? RT_QP_WPE : RT_PATHS_WPE))) k_q_primary(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                                  PathQs qs, uint32_t frame, int bounces) {
     static_assert(!PRIM || (W == 8 && RT_PATHS_DEFER), "wave-walked primaries: 8-wide deferred paths");
     __shared__ uint2 lds[S][256];
@@ -566,36 +576,48 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_q_primary(RtDevScene sc, 
         c1.ox = path_u(seed, 0);
         c1.oy = path_u(seed, 1);
         const Ray64 ray = gen_ray<false>(fp, c1, iv, j);
-        auto ray_of = [&]() { return with_inv(ray); };
         LaneCounts lc;
         Win win;
-        if constexpr (PRIM) {
+        // the primary ray's walk: wave-cooperative (PRIM) or per lane; a lane
+        // whose list overflowed or whose winner the reference cannot see goes
+        // to k_q_fallback (segment 0) with its ray
+        float tcull;
+        int nc;
+        bool over;
+        {
             const float pd = ray_pad(sc, ray);
             const Ray32 q0 = make_ray32<true>(ray, pd);
             const float tsl = round_up_f(0x1p-40 * ((double)q0.co + 1.0));
-            uint32_t* wstack = reinterpret_cast<uint32_t*>(&lds[0][tid & ~63]);  // 128 u32 of this wave's row
-            float tcull;
-            int nc;
-            bool over;
-            wave_walk<W, RT_PATHS_K, COUNT>(sc, fp, q0, pd, tsl, valid, wstack, pcand, tid, lc, tcull, nc, over);
-            if (valid) {
-                if (over) {
-                    win = trace_core<W, S, COUNT>(sc, ray_of, pd, st, 0, lc);
-                } else if (resolve_cands<COUNT>(sc, ray_of(), [&](int c) { return pcand[c][tid]; }, nc, tcull, win,
-                                                lc) != 0) {
-                    win = trace_core<W, S, COUNT>(sc, ray_of, pd, st, 1, lc);
-                }
+            if constexpr (PRIM) {
+                uint32_t* wstack = reinterpret_cast<uint32_t*>(&lds[0][tid & ~63]);  // 128 u32 of this wave's row
+                wave_walk<W, RT_PATHS_K, COUNT>(sc, fp, q0, pd, tsl, valid, wstack, pcand, tid, lc, tcull, nc, over);
+            } else if (valid) {
+                lane_walk<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES>(sc, q0, tsl, st, pcand, lc, tcull, nc, over);
             }
-        } else if (valid) {
-            win = trace_deferred<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES>(sc, ray_of, ray_pad(sc, ray), st,
-                                                                              pcand, lc);
+        }
+        bool fall = false;
+        if (valid) {
+            fall = over;
+            if (!over)
+                fall = resolve_cands<COUNT>(sc, with_inv(ray), [&](int c) { return pcand[c][tid]; }, nc, tcull, win,
+                                            lc) != 0;
+        }
+        const uint32_t path = ((uint32_t)rv * (uint32_t)fp.W + (uint32_t)iv) * (uint32_t)spp + (uint32_t)s;
+        if (fall) {  // the ray to the fall-back list: q[1] (free until segment 1) holds it
+            RT_G double* p = q_entry(qs, 1, atomicAdd(qc_fb(qs, 0), 1u));
+            p[0] = ray.ox;
+            p[1] = ray.oy;
+            p[2] = ray.oz;
+            p[3] = ray.dx;
+            p[4] = ray.dy;
+            p[5] = ray.dz;
+            p[9] = __longlong_as_double((long long)(path | (over ? kQFromPass0 : 0u)));
         }
         bool emit = false;
         Ray64 nr;
         double px = 0.0, py = 0.0, pz = 0.0;
-        const uint32_t path = ((uint32_t)rv * (uint32_t)fp.W + (uint32_t)iv) * (uint32_t)spp + (uint32_t)s;
         uint32_t hit = 0, sc0 = 0, so0 = 0;
-        if (valid) {
+        if (valid && !fall) {
             if (win.tri >= 0) q_bounce(sc, fp, frame, 0, bounces, ray, win, path, px, py, pz, emit, nr);
             Best hb;
             hb.dist = win.dist;
@@ -608,7 +630,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_q_primary(RtDevScene sc, 
             hit = win.tri >= 0;
         }
         const uint32_t slot = q_append(qs, 0, qc_emit(qs, 0), emit, nr, path);
-        if (valid) {
+        if (valid && !fall) {
             bool qd;
             uint32_t dst;
             q_light<W, S, 0>(sc, qs, cam, 0, nullptr, win.tri, px, py, pz, emit, 0, slot, path, st, sc0, so0, qd, dst);
@@ -632,7 +654,6 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_q_primary(RtDevScene sc, 
 #else
 #define RT_Q_ATTR
 #endif
-constexpr uint32_t kQFromPass0 = 0x80000000u;
 template <int W, int S, int K, bool COUNT, int SH>
 __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                              PathQs qs, uint32_t frame, int b, int bounces) {
@@ -732,7 +753,9 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
                                                     uint32_t frame, int b, int bounces) {
     __shared__ uint2 lds[S][256];
     const int tid = threadIdx.x;
-    const int qin = (b - 1) & 1, qout = b & 1;
+    // segment 0: the primary rays k_q_primary left in q[1]; segment b > 0:
+    // the listed entries of queue (b - 1) & 1
+    const int qin = b == 0 ? 1 : (b - 1) & 1, qout = b & 1;
     const uint32_t n = *qc_fb(qs, b);
     LaneStack<S> st;
     st.attach(lds, aux, tid);
@@ -748,23 +771,44 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
         Win win;
         win.tri = -1;
         double px = 0.0, py = 0.0, pz = 0.0;
-        uint32_t path = 0, e = 0;
+        uint32_t path = 0, e = 0, hit = 0;
         if (k < n) {
-            const uint32_t fe = qs.fb[qin * (size_t)qs.cap + k];
-            e = fe & ~kQFromPass0;
             Ray64 ray;
             double L[3];
-            q_load(qs, qin, e, ray, L, path);
+            bool pass0;
+            if (b == 0) {
+                e = k;
+                q_load(qs, qin, e, ray, L, path);
+                pass0 = (path & kQFromPass0) != 0;
+                path &= ~kQFromPass0;
+            } else {
+                const uint32_t fe = qs.fb[qin * (size_t)qs.cap + k];
+                e = fe & ~kQFromPass0;
+                pass0 = (fe & kQFromPass0) != 0;
+                q_load(qs, qin, e, ray, L, path);
+            }
             auto ray_of = [&]() { return with_inv(ray); };
-            win = trace_core<W, S, COUNT>(sc, ray_of, ray_pad(sc, ray), st, (fe & kQFromPass0) ? 0 : 1, tot);
+            win = trace_core<W, S, COUNT>(sc, ray_of, ray_pad(sc, ray), st, pass0 ? 0 : 1, tot);
             if (win.tri >= 0) q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
+            if (b == 0) {  // the primary segment's per-sample outputs
+                Best hb;
+                hb.dist = win.dist;
+                hb.rank = win.rank;
+                hb.tri = win.tri;
+                hb.px = px;
+                hb.py = py;
+                hb.pz = pz;
+                store_sample(fp, path, hb, shade_of(sc, win.tri));
+                hit = win.tri >= 0;
+            }
         }
         const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        if (b == 0) wave_add<1>(fp.hit_count, hit);
         bool qd = false;
         uint32_t dst = 0;
         if (k < n)
-            q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
-                              sh_cast, sh_occ, qd, dst);
+            q_light<W, S, SH>(sc, qs, cam, b, b == 0 ? nullptr : q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit,
+                              qout, slot, path, st, sh_cast, sh_occ, qd, dst);
         if constexpr (SH == 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {

@@ -1338,6 +1338,13 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
 template <int W>
 void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                        uint32_t frame, int bounces, int sh, bool count, hipStream_t s) {
+    // the primary segments' fall-back rays (segment 0; no occlusion rays there)
+    if (W == 8 && count)
+        hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, true, 0>), dim3(64), dim3(256), 0, s, sc, fp, aux, qs, frame, 0,
+                           bounces);
+    else
+        hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, false, 0>), dim3(64), dim3(256), 0, s, sc, fp, aux, qs, frame, 0,
+                           bounces);
     for (int b = 1; b <= bounces; b++) {
         if (W == 8 && count) {
             if (sh == 2) launch_q_segment<W, true, 2>(sc, fp, aux, qs, frame, b, bounces, s);
@@ -1375,6 +1382,9 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     const int sh = queued_shadow_mode(sc, shadow);
     if (sh == 2 && (!qs.srec[0] || !qs.srec[1] || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
+    // the wave-walked primary kernel uses no per-lane stack (no spill
+    // columns): the packet kernel's grid, 7 workgroups per CU
+    const dim3 pgrid((unsigned)(aux.pgrid > aux.grid ? aux.pgrid : aux.grid));
     if (ev) (void)hipEventRecord(ev[0], s);
     switch (sc.width) {
         case 2:
@@ -1388,14 +1398,14 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
         case 8:
             if (fp.pack && paths_primary_wave(sc)) {
                 if (count)
-                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, true, true, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+                    hipLaunchKernelGGL((k_q_primary<8, 1, true, true, true>), pgrid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
                 else
-                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, true, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+                    hipLaunchKernelGGL((k_q_primary<8, 1, false, true, true>), pgrid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
             } else if (paths_primary_wave(sc)) {
                 if (count)
-                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, true, false, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+                    hipLaunchKernelGGL((k_q_primary<8, 1, true, false, true>), pgrid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
                 else
-                    hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, false, true>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
+                    hipLaunchKernelGGL((k_q_primary<8, 1, false, false, true>), pgrid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
             } else if (fp.pack) {
                 hipLaunchKernelGGL((k_q_primary<8, kPathStack, false, true, false>), grid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
             } else {

@@ -153,7 +153,7 @@ __device__ __forceinline__ void q_light(const RtDevScene& sc, const PathQs& qs, 
         sh_cast++;
         sh_occ += !lit;
     }
-    if (SH == 2 && lit && b > 0) {
+    if (SH >= 2 && lit && b > 0) {
         queue = true;
         lit = false;
     }
@@ -204,10 +204,18 @@ __device__ __forceinline__ void q_shadow_append(const PathQs& qs, int b, bool qu
     r[3] = __longlong_as_double((long long)(((uint64_t)dst << 32) | (uint32_t)tri));
 }
 
-// Bin of an occlusion ray: the cube-map tile (RT_SH_G x RT_SH_G per face) of
-// its direction from the light.  Only the order of the occlusion pass depends
-// on it, never a result.
-__device__ __forceinline__ uint32_t sh_bin(const RtFrameCam& cam, double px, double py, double pz) {
+// Sort key of an occlusion ray: the cube-map cell of its direction from the
+// light — face (3 bits) over the Morton code of the cell (u, v) on the face
+// (RT_SH_CELLS^2 cells, 0.18 degrees).  Only the order of the occlusion pass
+// depends on it, never a result.
+__device__ __forceinline__ uint32_t morton9(uint32_t x) {  // 9 bits spread to the even bits
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+__device__ __forceinline__ uint32_t sh_key(const RtFrameCam& cam, double px, double py, double pz) {
     const float dx = (float)(px - cam.pos[0]), dy = (float)(py - cam.pos[1]), dz = (float)(pz - cam.pos[2]);
     const float ax = __builtin_fabsf(dx), ay = __builtin_fabsf(dy), az = __builtin_fabsf(dz);
     uint32_t face;
@@ -222,21 +230,25 @@ __device__ __forceinline__ uint32_t sh_bin(const RtFrameCam& cam, double px, dou
         face = dz < 0.f ? 5u : 4u;
         m = az; u = dx; v = dy;
     }
-    const float s = m > 0.f ? 0.5f * (float)RT_SH_G / m : 0.f;
+    const float s = m > 0.f ? 0.5f * (float)RT_SH_CELLS / m : 0.f;
     int iu = (int)((u + m) * s), iv = (int)((v + m) * s);
-    iu = iu < 0 ? 0 : iu >= RT_SH_G ? RT_SH_G - 1 : iu;
-    iv = iv < 0 ? 0 : iv >= RT_SH_G ? RT_SH_G - 1 : iv;
-    return (face * RT_SH_G + (uint32_t)iv) * RT_SH_G + (uint32_t)iu;
+    iu = iu < 0 ? 0 : iu >= RT_SH_CELLS ? RT_SH_CELLS - 1 : iu;
+    iv = iv < 0 ? 0 : iv >= RT_SH_CELLS ? RT_SH_CELLS - 1 : iv;
+    return (face << 18) | morton9((uint32_t)iu) | (morton9((uint32_t)iv) << 1);
 }
 
-// Binning of segment b's occlusion records (a counting sort by sh_bin; the
-// order inside a bin is whatever the LDS atomics give): block k of
-// RT_SH_BLOCKS takes records [k n / NB, (k+1) n / NB).
+// Counting-sort pass over segment b's occlusion records, digit (key >> shift)
+// mod RT_SH_BINS, from srec[src] to srec[1 - src]: per-block LDS histograms,
+// one scan, then each block scatters its records (their order inside a block
+// is the LDS atomics', so a pass is stable only up to a block's range).  Two
+// passes (low digit, then high) order the records by key up to that fuzz:
+// neighbouring records are rays of nearly the same direction from the light.
+// Block k of RT_SH_BLOCKS takes records [k n / NB, (k+1) n / NB).
 __device__ __forceinline__ void sh_range(uint32_t n, uint32_t k, uint32_t& lo, uint32_t& hi) {
     lo = (uint32_t)((uint64_t)n * k / RT_SH_BLOCKS);
     hi = (uint32_t)((uint64_t)n * (k + 1) / RT_SH_BLOCKS);
 }
-__global__ void __launch_bounds__(1024) k_sh_hist(RtFrameParams fp, PathQs qs, int b) {
+__global__ void __launch_bounds__(1024) k_sh_hist(RtFrameParams fp, PathQs qs, int b, int src, int shift) {
     __shared__ uint32_t h[RT_SH_BINS];
     for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) h[i] = 0;
     __syncthreads();
@@ -244,8 +256,8 @@ __global__ void __launch_bounds__(1024) k_sh_hist(RtFrameParams fp, PathQs qs, i
     uint32_t lo, hi;
     sh_range(*qc_sh(qs, b), blockIdx.x, lo, hi);
     for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
-        const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
-        atomicAdd(&h[sh_bin(cam, r[0], r[1], r[2])], 1u);
+        const RT_G double* r = qs.srec[src] + 4 * (size_t)e;
+        atomicAdd(&h[(sh_key(cam, r[0], r[1], r[2]) >> shift) & (RT_SH_BINS - 1)], 1u);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x] = h[i];
@@ -282,7 +294,7 @@ __global__ void __launch_bounds__(1024) k_sh_scan(PathQs qs) {
         run[k] = v;
     }
 }
-__global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs, int b) {
+__global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs, int b, int src, int shift) {
     __shared__ uint32_t cur[RT_SH_BINS];
     for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) cur[i] = qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x];
     __syncthreads();
@@ -290,9 +302,10 @@ __global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs
     uint32_t lo, hi;
     sh_range(*qc_sh(qs, b), blockIdx.x, lo, hi);
     for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
-        const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
+        const RT_G double* r = qs.srec[src] + 4 * (size_t)e;
         const double x = r[0], y = r[1], z = r[2], w = r[3];
-        RT_G double* o = qs.srec[1] + 4 * (size_t)atomicAdd(&cur[sh_bin(cam, x, y, z)], 1u);
+        const uint32_t d = (sh_key(cam, x, y, z) >> shift) & (RT_SH_BINS - 1);
+        RT_G double* o = qs.srec[1 - src] + 4 * (size_t)atomicAdd(&cur[d], 1u);
         o[0] = x;
         o[1] = y;
         o[2] = z;
@@ -482,7 +495,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_
         double px = 0.0, py = 0.0, pz = 0.0;
         uint64_t td = 0;
         if (act) {
-            const RT_G double* r = qs.srec[1] + 4 * (size_t)e;
+            const RT_G double* r = qs.srec[0] + 4 * (size_t)e;  // (sorted: srec[0] -> [1] -> [0])
             px = r[0];
             py = r[1];
             pz = r[2];
@@ -728,7 +741,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         if (act && !fall)
             q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
                               sh_cast, sh_occ, qd, dst);
-        if constexpr (SH == 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
+        if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         wave_add<24>(fp.counters, segs);
@@ -742,6 +755,201 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
             wave_add<28>(fp.counters + 2, tot.tris);
             wave_add<28>(fp.counters + 3, tot.chain);
         }
+    }
+}
+
+// The split segment (RT_Q_SPLIT, default): k_q_walk is the fp32 walk alone —
+// no fp64, no path state, so it keeps fewer registers and more waves resident
+// to hide the node fetches' latency — and hands each entry's candidates to
+// k_q_shade through HBM (37 B per ray); k_q_shade resolves them in fp64 with
+// all 64 lanes busy, then k_q_segment's tail (bounce, occlusion, radiance).
+#ifndef RT_QW_WPE
+#define RT_QW_WPE 6  // waves per SIMD of k_q_walk
+#endif
+#ifndef RT_QW_STACK
+#define RT_QW_STACK 8  // LDS stack ring entries per lane in k_q_walk
+#endif
+template <int W, int S, int K, bool COUNT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_QW_WPE)))
+k_q_walk(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
+    static_assert(K <= RT_Q_KMAX, "candidate lists of the split segment");
+    __shared__ uint2 lds[S][256];
+    __shared__ uint2 cand[K][256];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int qin = (b - 1) & 1;
+    const uint32_t n = *qc_emit(qs, b - 1);
+    LaneStack<S> st;
+    st.attach(lds, aux, tid);
+    LaneCounts tot;
+    uint32_t segs = 0;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(qc_pull(qs, b), 64u);
+        base = (uint32_t)__shfl((int)base, 0);
+        if (base >= n) break;
+        const uint32_t e = base + (uint32_t)lane;
+        if (e >= n) continue;
+        Ray32 q;
+        float tsl;
+        {
+            const RT_G double* p = q_entry(qs, qin, e);
+            Ray64 ray;
+            ray.ox = p[0];
+            ray.oy = p[1];
+            ray.oz = p[2];
+            ray.dx = p[3];
+            ray.dy = p[4];
+            ray.dz = p[5];
+            ray.ix = ray.iy = ray.iz = 0.0;
+            q = make_ray32<true>(ray, ray_pad(sc, ray));
+            tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
+        }
+        LaneCounts lc;
+        float tcull;
+        int nc;
+        bool over;
+        lane_walk<W, S, K, COUNT, W == 8 && RT_QNODES>(sc, q, tsl, st, cand, lc, tcull, nc, over);
+        uint32_t m = 0;
+        if (!over) {
+            for (int c = 0; c < nc; c++) {
+                const uint2 v = cand[c][tid];
+                if (__uint_as_float(v.y) > tcull) continue;  // cannot beat a certain hit
+                reinterpret_cast<RT_G uint2*>(qs.wc)[(size_t)m * qs.cap + e] = v;
+                m++;
+            }
+        }
+        qs.wn[e] = over ? (uint8_t)0xFF : (uint8_t)m;
+        qs.wt[e] = tcull;
+        segs++;
+        if (COUNT) {
+            tot.nodes += lc.nodes;
+            tot.pre += lc.pre;
+        }
+    }
+    if (fp.counters) {
+        wave_add<24>(fp.counters, segs);
+        if (COUNT) {
+            wave_add<28>(fp.counters + 1, tot.nodes);
+            wave_add<28>(fp.counters + 6, tot.pre);
+        }
+    }
+}
+
+template <int W, int S, bool COUNT, int SH>
+__global__ void __launch_bounds__(256) RT_Q_ATTR k_q_shade(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
+                                                           PathQs qs, uint32_t frame, int b, int bounces) {
+    __shared__ uint2 lds[S][256];  // (the per-lane occlusion walk's stack, SH == 1)
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int qin = (b - 1) & 1, qout = b & 1;
+    const uint32_t n = *qc_emit(qs, b - 1);
+    LaneStack<S> st;
+    st.attach(lds, aux, tid);
+    const RtFrameCam cam = frame_cam(fp, 0);
+    uint32_t sh_cast = 0, sh_occ = 0;
+    LaneCounts tot;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 2, 64u);  // (the pull line's third word)
+        base = (uint32_t)__shfl((int)base, 0);
+        if (base >= n) break;
+        const uint32_t e = base + (uint32_t)lane;
+        const bool act = e < n;
+        bool emit = false, fall = false;
+        Ray64 nr;
+        Win win;
+        win.tri = -1;
+        double px = 0.0, py = 0.0, pz = 0.0;
+        uint32_t path = 0;
+        if (act) {
+            Ray64 ray;
+            double L[3];
+            q_load(qs, qin, e, ray, L, path);
+            const uint32_t cnt = qs.wn[e];
+            uint32_t fe = e | kQFromPass0;
+            fall = cnt == 0xFFu;
+            if (!fall) {
+                fe = e;
+                LaneCounts lc;
+                fall = resolve_cands<COUNT>(sc, with_inv(ray), [&](int c) { return reinterpret_cast<const RT_G uint2*>(qs.wc)[(size_t)c * qs.cap + e]; },
+                                            (int)cnt, qs.wt[e], win, lc) != 0;
+                if (COUNT) {
+                    tot.tris += lc.tris;
+                    tot.chain += lc.chain;
+                }
+            }
+            if (fall) {
+                qs.fb[qin * (size_t)qs.cap + atomicAdd(qc_fb(qs, b), 1u)] = fe;
+            } else if (win.tri >= 0) {
+                q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
+            }
+        }
+        const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        bool qd = false;
+        uint32_t dst = 0;
+        if (act && !fall)
+            q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
+                              sh_cast, sh_occ, qd, dst);
+        if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
+    }
+    if (fp.counters) {
+        if (SH == 1) {
+            wave_add<24>(fp.counters + 24, sh_cast);
+            wave_add<24>(fp.counters + 25, sh_occ);
+        }
+        if (COUNT) {
+            wave_add<28>(fp.counters + 2, tot.tris);
+            wave_add<28>(fp.counters + 3, tot.chain);
+        }
+    }
+}
+
+// Queued occlusion records walked per lane, in the order the segment kernel
+// appended them (RT_SHADOW_RAYS=rec: no binning): lane_occluded in a lean
+// kernel of its own.
+#ifndef RT_SL_WPE
+#define RT_SL_WPE 6
+#endif
+template <int W, int S>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SL_WPE)))
+k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
+    __shared__ uint2 lds[S][256];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t n = *qc_sh(qs, b);
+    LaneStack<S> st;
+    st.attach(lds, aux, tid);
+    const RtFrameCam cam = frame_cam(fp, 0);
+    uint32_t occl = 0, cast = 0;
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 1, 64u);
+        base = (uint32_t)__shfl((int)base, 0);
+        if (base >= n) break;
+        const uint32_t e = base + (uint32_t)lane;
+        if (e >= n) continue;
+        const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
+        const double px = r[0], py = r[1], pz = r[2];
+        const bool occ = lane_occluded<W, S, W == 8 && RT_QNODES>(sc, cam, px, py, pz, st);
+        cast++;
+        occl += occ;
+        if (!occ) {
+            const uint64_t td = (uint64_t)__double_as_longlong(r[3]);
+            const uint32_t tri = (uint32_t)td, dst = (uint32_t)(td >> 32);
+            const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)tri;
+            const double w = __builtin_ldexp(1.0, -b);
+            double c[3];
+            shade_at(cam, px, py, pz, T[RT_T64_NORMAL], T[RT_T64_NORMAL + 1], T[RT_T64_NORMAL + 2], c);
+            RT_G double* L = q_dst(qs, dst);
+            L[0] = L[0] + w * c[0];
+            L[1] = L[1] + w * c[1];
+            L[2] = L[2] + w * c[2];
+        }
+    }
+    if (fp.counters) {
+        wave_add<24>(fp.counters + 24, cast);
+        wave_add<24>(fp.counters + 25, occl);
     }
 }
 
@@ -809,7 +1017,7 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
         if (k < n)
             q_light<W, S, SH>(sc, qs, cam, b, b == 0 ? nullptr : q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit,
                               qout, slot, path, st, sh_cast, sh_occ, qd, dst);
-        if constexpr (SH == 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
+        if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         if (SH == 1) {

@@ -1318,19 +1318,36 @@ hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const 
 // Queued path tracing of one pose (queue_paths.h): the primary segments of
 // every path, then per bounce segment the compacted queue and its fall-back
 // list, then the pixel sums.  The control words are zeroed here.
+// RT_Q_SPLIT=1 (read per call): the walk and the resolve of a segment in two
+// kernels (k_q_walk, k_q_shade) instead of k_q_segment: 236 vs 167 ms per
+// pose on config c5 — the split exposes the resolve's fp64 record gathers,
+// which the fused kernel overlaps with other waves' walks
+bool q_split() {
+    const char* e = getenv("RT_Q_SPLIT");
+    return e && e[0] == '1';
+}
 template <int W, bool COUNT, int SH>
 void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                       uint32_t frame, int b, int bounces, hipStream_t s) {
     const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
-    hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
-                       bounces);
+    if (q_split()) {
+        hipLaunchKernelGGL((k_q_walk<W, RT_QW_STACK, RT_Q_K, COUNT>), grid, blk, 0, s, sc, fp, aux, qs, b);
+        hipLaunchKernelGGL((k_q_shade<W, RT_Q_STACK, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+    } else {
+        hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
+                           bounces);
+    }
     hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, COUNT, SH>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
+    if constexpr (SH == 3)  // the records in emission order, per lane
+        hipLaunchKernelGGL((k_sh_lane<W, RT_Q_STACK>), grid, blk, 0, s, sc, fp, aux, qs, b);
     if constexpr (SH == 2) {
         // the segment's occlusion records: binned by direction from the light,
         // then walked 64 at a time by the wave-cooperative any-hit walk
-        hipLaunchKernelGGL(k_sh_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b);
-        hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
-        hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b);
+        for (int pass = 0; pass < 2; pass++) {  // low digit 0 -> 1, high digit 1 -> 0
+            hipLaunchKernelGGL(k_sh_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, pass * RT_SH_BITS);
+            hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
+            hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, pass * RT_SH_BITS);
+        }
         hipLaunchKernelGGL((k_sh_walk<W, COUNT>), dim3((unsigned)aux.pgrid), blk, 0, s, sc, fp, aux, qs, b);
     }
 }
@@ -1347,11 +1364,13 @@ void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLa
                            bounces);
     for (int b = 1; b <= bounces; b++) {
         if (W == 8 && count) {
-            if (sh == 2) launch_q_segment<W, true, 2>(sc, fp, aux, qs, frame, b, bounces, s);
+            if (sh == 3) launch_q_segment<W, true, 3>(sc, fp, aux, qs, frame, b, bounces, s);
+            else if (sh == 2) launch_q_segment<W, true, 2>(sc, fp, aux, qs, frame, b, bounces, s);
             else if (sh == 1) launch_q_segment<W, true, 1>(sc, fp, aux, qs, frame, b, bounces, s);
             else launch_q_segment<W, true, 0>(sc, fp, aux, qs, frame, b, bounces, s);
         } else {
-            if (sh == 2) launch_q_segment<W, false, 2>(sc, fp, aux, qs, frame, b, bounces, s);
+            if (sh == 3) launch_q_segment<W, false, 3>(sc, fp, aux, qs, frame, b, bounces, s);
+            else if (sh == 2) launch_q_segment<W, false, 2>(sc, fp, aux, qs, frame, b, bounces, s);
             else if (sh == 1) launch_q_segment<W, false, 1>(sc, fp, aux, qs, frame, b, bounces, s);
             else launch_q_segment<W, false, 0>(sc, fp, aux, qs, frame, b, bounces, s);
         }
@@ -1362,10 +1381,13 @@ void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLa
 // RT_SHADOW_RAYS=lane: walked per lane inside the segment kernel (read per call).
 // (The any-hit walk's wave stack holds kPacketStack entries: deeper trees
 // walk their occlusion rays per lane.)
+// RT_SHADOW_RAYS=rec: queued, walked per lane in emission order (no binning).
 int queued_shadow_mode(const RtDevScene& sc, bool shadow) {
     if (!shadow) return 0;
     const char* e = getenv("RT_SHADOW_RAYS");
-    return (e && e[0] == 'l') || sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
+    if (e && e[0] == 'l') return 1;
+    if (e && e[0] == 'r') return 3;
+    return sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
 }
 
 hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,

@@ -453,7 +453,8 @@ PathWs ensure_pw(Replica& r, uint64_t P) {
 // Queued path-tracer workspace for P paths (grown, never shrunk): two
 // segment queues (80 B per entry), the final radiance (24 B per path), two
 // fall-back lists (4 B per path each) and the control words.
-constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4 + 2 * 32;  // (+ the occlusion records, 32 B twice)
+// (+ the occlusion records, 32 B twice, and the split segment's candidate lists, 37 B)
+constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4 + 2 * 32 + 8 * RT_Q_KMAX + 4 + 1;
 PathQs ensure_pq(Replica& r, uint64_t P) {
     if (r.pq_cap < P) {
         quiesce(r);  // earlier launches may still use it
@@ -461,7 +462,7 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
         r.d_pq = nullptr;
         r.pq_cap = 0;
         HIP_TRY(hipMalloc(&r.d_pq, P * kPqBytesPerPath + RT_QC_WORDS(64) * sizeof(uint32_t) +
-                                       (uint64_t)RT_SH_BINS * RT_SH_BLOCKS * sizeof(uint32_t) + 1024));
+                                       (uint64_t)RT_SH_BINS * RT_SH_BLOCKS * sizeof(uint32_t) + 2048));
         r.pq_cap = P;
     }
     uint8_t* base = static_cast<uint8_t*>(r.d_pq);
@@ -475,8 +476,13 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
     qs.srec[1] = reinterpret_cast<double*>(base + align_up<char>(c * 192) + c * 32);
     const uint64_t o_ctl = align_up<char>(align_up<char>(c * 192) + c * 64);
     qs.ctl = reinterpret_cast<uint32_t*>(base + o_ctl);
-    qs.bhist = reinterpret_cast<uint32_t*>(base + align_up<char>(o_ctl + RT_QC_WORDS(64) * sizeof(uint32_t)));
+    const uint64_t o_bh = align_up<char>(o_ctl + RT_QC_WORDS(64) * sizeof(uint32_t));
+    qs.bhist = reinterpret_cast<uint32_t*>(base + o_bh);
     qs.sh_blocks = RT_SH_BLOCKS;
+    const uint64_t o_wc = align_up<char>(o_bh + (uint64_t)RT_SH_BINS * RT_SH_BLOCKS * sizeof(uint32_t));
+    qs.wc = reinterpret_cast<uint64_t*>(base + o_wc);
+    qs.wt = reinterpret_cast<float*>(base + align_up<char>(o_wc + c * 8 * RT_Q_KMAX));
+    qs.wn = reinterpret_cast<uint8_t*>(base + align_up<char>(align_up<char>(o_wc + c * 8 * RT_Q_KMAX) + c * 4));
     qs.cap = (uint32_t)c;
     return qs;
 }

@@ -261,13 +261,21 @@ struct PathQs {
     RT_G double* srec[2];
     RT_G uint32_t* bhist;  // [bins][sh_blocks]
     uint32_t sh_blocks;
+    // the split segment (k_q_walk -> k_q_shade): per queue entry the walk's
+    // surviving candidates [RT_Q_KMAX][cap] {triangle, t lower bound}, their
+    // count (0xFF: overflow) and the culling distance
+    RT_G uint64_t* wc;     // (uint2 entries)
+    RT_G uint8_t* wn;
+    RT_G float* wt;
 };
+#define RT_Q_KMAX 4
 #define RT_QC_WORDS(bounces) (4 * ((bounces) + 1) * 16)
-// occlusion-ray bins: a cube map around the light, RT_SH_G x RT_SH_G tiles per face
-#ifndef RT_SH_G
-#define RT_SH_G 32
-#endif
-#define RT_SH_BINS (6 * RT_SH_G * RT_SH_G)
+// occlusion-ray order: a cube map around the light, 512 x 512 cells per face
+// in Morton order (21-bit keys), counting-sorted in two passes of RT_SH_BITS
+// bits (RT_SH_BINS bins, per-block counts of RT_SH_BLOCKS blocks)
+#define RT_SH_CELLS 512
+#define RT_SH_BITS 11
+#define RT_SH_BINS (1 << RT_SH_BITS)
 #define RT_SH_BLOCKS 256
 
 // Workspace of the wavefront path tracer (wavefront_paths.h), per replica.

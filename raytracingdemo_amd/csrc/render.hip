@@ -1326,11 +1326,19 @@ bool q_split() {
     const char* e = getenv("RT_Q_SPLIT");
     return e && e[0] == '1';
 }
+// RT_Q_DYN=1 (read per call): the segment kernel with lane refill (k_q_segment_dyn)
+bool q_dyn() {
+    const char* e = getenv("RT_Q_DYN");
+    return e && e[0] == '1';
+}
 template <int W, bool COUNT, int SH>
 void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                       uint32_t frame, int b, int bounces, hipStream_t s) {
     const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
-    if (q_split()) {
+    if (q_dyn()) {
+        hipLaunchKernelGGL((k_q_segment_dyn<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame,
+                           b, bounces);
+    } else if (q_split()) {
         hipLaunchKernelGGL((k_q_walk<W, RT_QW_STACK, RT_Q_K, COUNT>), grid, blk, 0, s, sc, fp, aux, qs, b);
         hipLaunchKernelGGL((k_q_shade<W, RT_Q_STACK, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
     } else {

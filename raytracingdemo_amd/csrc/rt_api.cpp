@@ -112,11 +112,37 @@ struct Slot {
     hipEvent_t ev = nullptr;
 };
 
+// Host-mapped words for k_fixup's redo counts (Slot::h_seen): one pinned
+// page for the process, handed out and taken back, never freed — a scene
+// destroyed at interpreter shutdown returns its words without a HIP call.
+std::mutex g_seen_mu;
+uint32_t* g_seen_page = nullptr;
+auto& g_seen_free = *new std::vector<uint32_t*>();  // (never destroyed: no static-destructor order at exit)
+uint32_t* seen_word_alloc() {
+    std::lock_guard<std::mutex> lk(g_seen_mu);
+    if (g_seen_free.empty()) {
+        constexpr size_t kWords = 4096 / sizeof(uint32_t);
+        void* p = nullptr;
+        HIP_TRY(hipHostMalloc(&p, kWords * sizeof(uint32_t), hipHostMallocMapped));
+        g_seen_page = static_cast<uint32_t*>(p);
+        for (size_t k = 0; k < kWords; k += 16) g_seen_free.push_back(g_seen_page + k);  // one 64-B line each
+    }
+    uint32_t* w = g_seen_free.back();
+    g_seen_free.pop_back();
+    __atomic_store_n(w, 0u, __ATOMIC_RELAXED);
+    return w;
+}
+void seen_word_free(uint32_t* w) {
+    std::lock_guard<std::mutex> lk(g_seen_mu);
+    g_seen_free.push_back(w);
+}
+
 struct Replica {
     int device = -1;
     void* blob = nullptr;       // one allocation for the whole scene
     size_t blob_bytes = 0;
     RtDevScene dev{};
+
     unsigned long long* d_counters = nullptr;  // RT_FLAG_COUNT counters
     // staging for the host-output frame call
     void* frame = nullptr;
@@ -248,7 +274,7 @@ void free_replica(Replica& r) {
         if (q.d_tiles) hipFree(q.d_tiles);
         if (q.d_spill) hipFree(q.d_spill);
         if (q.d_redo) hipFree(q.d_redo);
-        if (q.h_seen) hipHostFree(q.h_seen);
+        if (q.h_seen) seen_word_free(q.h_seen);
         if (q.d_pool) hipFree(q.d_pool);
         if (q.ev) hipEventDestroy(q.ev);
     }
@@ -280,8 +306,7 @@ void alloc_slot(Replica& r, Slot& q) {
     HIP_TRY(hipMalloc(&q.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
     HIP_TRY(hipMalloc(&q.d_pool, (size_t)r.pool_chunks * RT_POOL_CHUNK * sizeof(uint64_t)));
     HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&q.h_seen), sizeof(uint32_t), hipHostMallocMapped));
-    *q.h_seen = 0;
+    q.h_seen = seen_word_alloc();
 }
 
 void upload_one(rt_scene* s, int device) {

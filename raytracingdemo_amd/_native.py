@@ -114,10 +114,13 @@ def _share_hip_runtime_with_torch() -> None:
     spec = importlib.util.find_spec("torch")
     if spec is None or not spec.submodule_search_locations:
         return
-    for name in ("libamdhip64.so", "librccl.so"):  # (RCCL: opened by the library on a multi-device upload)
-        cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", name)
-        if os.path.exists(cand):
-            C.CDLL(cand, mode=C.RTLD_GLOBAL)
+    # Only the HIP runtime: torch's librccl.so mapped RTLD_GLOBAL ahead of
+    # `import torch` gets its static objects destroyed twice at exit ("double
+    # free or corruption").  RCCL is dlopen'ed by soname (librccl.so.1) on the
+    # first multi-device upload and so binds to torch's copy when torch is in.
+    cand = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        C.CDLL(cand, mode=C.RTLD_GLOBAL)
 
 
 def lib() -> C.CDLL:

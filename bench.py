@@ -260,8 +260,12 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
     shadow = not a.no_shadow
     os.environ["RT_PATHS"] = a.pipeline  # (read by the library per call)
     queued = a.pipeline == "queue"
-    shadow_mode = ("queued, binned by direction from the light, wave-walked" if queued and
-                   os.environ.get("RT_SHADOW_RAYS", "")[:1] != "l" else "per lane") if shadow else None
+    # occlusion-ray mode (render.hip queued_shadow_mode): the megakernel walks
+    # them per lane inline; the queued pipeline bins them (default), or per
+    # lane inline (RT_SHADOW_RAYS=lane) or from records (RT_SHADOW_RAYS=rec)
+    sh_env = os.environ.get("RT_SHADOW_RAYS", "")[:1]
+    shadow_kind = None if not shadow else ("inline" if not queued or sh_env == "l" else
+                                           "records" if sh_env == "r" else "binned")
     path = rt.CameraPath(rt.scene_center(tris), 36)
     rows = rows_per_rank(H, world, band=1)  # the paths kernel takes single interleaved rows
     my_rows = len(shard_rows(rank, world, H, band=1))
@@ -287,6 +291,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
     segs_per_pose = cs["rays"] / F
+    if shadow_kind == "binned" and cs["shadow_rays"] and not cs["shadow_wave_nodes"]:
+        shadow_kind = "inline"  # (a walk tree deeper than the binned walk's stack: per lane)
     # algorithmic bytes of one pose (the counting pass, W = 8): per segment the
     # lane's own node steps on the 96-B quantised nodes (walk_tree.cpp
     # quantize_wide8), 48-B fp32 triangle records through the pre-filter,
@@ -300,17 +306,30 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
     if queued:
         # the queued pipeline's own traffic (queue_paths.h): every bounce ray's
         # 80-B queue entry written once and read once, every path's final
-        # radiance written and read (24 B each way); every occlusion record
-        # (32 B) written, read by the two binning passes, written binned and
-        # read by the walk, the lit ones' radiance read and written (48 B); the
-        # occlusion walk's wave node steps (256 B) and triangle records (48 B)
+        # radiance written and read (24 B each way)
         samples = my_rows * W * S
         bounce_rays = (cs["rays"] / F) - samples
         q_bytes = bounce_rays * 160 + samples * 48
-        sh_bytes = (cs["shadow_rays"] * 160 + (cs["shadow_rays"] - cs["shadow_occluded"]) * 48 +
-                    cs["shadow_wave_nodes"] * 256 + cs["shadow_wave_tris"] * 48) / F
-        alg_pose += q_bytes + sh_bytes
-        alg_parts.update({"queues": round(q_bytes), "occlusion": round(sh_bytes)})
+        alg_pose += q_bytes
+        alg_parts["queues"] = round(q_bytes)
+    if shadow:
+        # occlusion rays: the walk's fetches — binned records walked by the
+        # wave (256-B nodes, 48-B triangle records once per wave), else per
+        # lane (96-B quantised nodes, 48-B fp32 records per lane) — plus, for
+        # queued records, each 32-B record's trips (binned: written, 2 sort
+        # passes of histogram read + scatter read/write, read by the walk =
+        # 8 x 32 B; per-lane records kernel: written and read) and the lit
+        # ones' radiance read and written (48 B)
+        sh_n = cs["shadow_rays"]
+        sh_lit = sh_n - cs["shadow_occluded"]
+        if shadow_kind == "binned":
+            sh_bytes = sh_n * 256 + sh_lit * 48 + cs["shadow_wave_nodes"] * 256 + cs["shadow_wave_tris"] * 48
+        else:
+            sh_bytes = cs["shadow_lane_nodes"] * 96 + cs["shadow_lane_tris"] * 48
+            if shadow_kind == "records":
+                sh_bytes += sh_n * 64 + sh_lit * 48
+        alg_pose += sh_bytes / F
+        alg_parts["occlusion"] = round(sh_bytes / F)
     # W warm-up steps, then render-only steps until SETTLE_S of GPU work (main())
     for w in range(a.warmup):
         step(w, timing=True)
@@ -385,7 +404,11 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
             "segments_per_sample": round(segs_per_pose / (W * H * S), 3),
             "pipeline": ("queued: wave-walked primaries, compacted per-segment bounce queues, per-lane bounce walks"
                          if queued else "megakernel (k_paths)"),
-            "shadow": {"on": shadow, "mode": shadow_mode, "rays_per_pose": round(cs["shadow_rays"] / F),
+            "shadow": {"on": shadow, "mode": {"binned": "queued records, sorted by direction from the light, "
+                                                     "walked by the wave (any hit)",
+                                           "records": "queued records walked per lane (any hit)",
+                                           "inline": "walked per lane where the vertex is shaded (any hit)",
+                                           None: None}[shadow_kind], "rays_per_pose": round(cs["shadow_rays"] / F),
                        "occluded_per_pose": round(cs["shadow_occluded"] / F),
                        "rays_per_sample": round(cs["shadow_rays"] / F / (W * my_rows * S), 3),
                        "note": "one occlusion ray toward the head-light per bounce vertex (RT_FLAG_SHADOW); not "
@@ -402,9 +425,10 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
                          "bytes": "per-lane node steps x 96 (quantised) + wave node steps x 256 and wave triangle "
                                   "records x 48 (primary segments walked by the wave) + pre-filter x 48 + fp64 tests "
                                   "x 72 + chain checks x 52 + segments x 56 + 3 per pixel; queued: + 160 per bounce "
-                                  "ray and 48 per sample (queues, final radiance) + per occlusion ray 160 (records "
-                                  "through the binning) + 48 per lit one + its wave walk's node steps x 256 and "
-                                  "triangle records x 48",
+                                  "ray and 48 per sample (queues, final radiance); occlusion rays: binned: 256 per "
+                                  "ray (record through the 2-pass sort) + 48 per lit one + wave node steps x 256 + "
+                                  "wave triangle records x 48; per lane: node steps x 96 + triangle records x 48 "
+                                  "(+ 64 per record and 48 per lit one from queued records)",
                          "convention": "a record once per fetching wave instruction: the wave walks' (primary, "
                                        "occlusion) nodes and triangles once per wave, the per-lane bounce walks' "
                                        "per lane (each lane's node is its own fetch)",

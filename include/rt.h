@@ -173,7 +173,8 @@ typedef struct {
     uint64_t side_jobs_kernel; /*   done by a de-interleave kernel after the render */
     uint64_t shadow_wave_nodes;/* queued occlusion rays: wave node steps of the any-hit walk */
     uint64_t shadow_wave_tris; /*   and triangle records it fetched, once per wave      */
-    uint64_t reserved[1];
+    uint64_t shadow_lane_nodes;/* per-lane occlusion walks: quantised node steps, per lane */
+    uint64_t shadow_lane_tris; /*   and fp32 triangle records they tested                  */
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */

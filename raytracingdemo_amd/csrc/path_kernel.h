@@ -287,9 +287,10 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
 // 2^-12 is far wider than the fp32 filter's error budget, so p's own triangle
 // (t = |e| up to rounding) is rejected in fp32 and costs no fp64 test.
 constexpr double kShadowScale = 1.0 - 0x1p-12;
-template <int W, int S, bool QN>
+// COUNT: the walk's node steps and triangle records go to oc->nodes / oc->pre.
+template <int W, int S, bool QN, bool COUNT = false>
 __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFrameCam& cam, double px, double py,
-                                              double pz, LaneStack<S>& st) {
+                                              double pz, LaneStack<S>& st, LaneCounts* oc = nullptr) {
     // the fp64 ray, built again for the rare fp64 test rather than held
     // (12 VGPRs) through the walk
     auto ray_of = [&](double& len) {
@@ -315,9 +316,10 @@ __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFram
     const double tmax = len * kShadowScale;
     const float tcert = (float)(tmax * 0.999);
     LaneCounts lc;
-    LaneWalk<W, S, 1, false, QN> w;
+    LaneWalk<W, S, 1, COUNT, QN> w;
     w.begin(sc, q, 0.f, st);
     w.tcull = round_up_f(tmax);
+    bool occ = false;
     while (w.cur != RT_INVALID_REF) {
         if (!(w.cur & RT_LEAF_BIT)) {
             w.visit_node(sc, st, lc);
@@ -328,16 +330,28 @@ __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFram
         for (uint32_t k = first; k < first + cnt; k++) {
             const float4* R = reinterpret_cast<const float4*>(sc.tri32 + 12 * (size_t)k);
             float tl, tu;
+            if (COUNT) lc.pre++;
             const int cls = tri_classify(R[0], R[1], R[2], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, w.tcull, tl, tu);
-            if (cls == 2 && tu < tcert) return true;
+            if (cls == 2 && tu < tcert) {
+                occ = true;
+                break;
+            }
             if (cls != 0) {
                 double t, l2;
-                if (mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, ray_of(l2), t) && t < tmax) return true;
+                if (mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, ray_of(l2), t) && t < tmax) {
+                    occ = true;
+                    break;
+                }
             }
         }
+        if (occ) break;
         w.pop_next(st);
     }
-    return false;
+    if (COUNT) {
+        oc->nodes += lc.nodes;
+        oc->pre += lc.pre;
+    }
+    return occ;
 }
 
 // Primary segments through wave_walk (PRIM, PACK on 8-wide trees whose stack
@@ -421,6 +435,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         uint32_t hits = 0, segs = 0;  // segs: ray segments traced (RT_FLAG_COUNT)
         uint32_t sh_cast = 0, sh_occ = 0;  // SHADOW: occlusion rays cast / occluded
         LaneCounts tot;               // COUNT: the lane's fetch counts over its paths
+        LaneCounts shc;               // COUNT: ... of its occlusion walks
         // PRIM: the primary segment of every lane of the wave (one sample per
         // lane) walked together, before the lanes go their own ways
         float p_tcull = 0.f;
@@ -499,7 +514,7 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                     bool lit = true;
                     if constexpr (SHADOW) {
                         if (b > 0) {
-                            lit = !lane_occluded<W, S, W == 8 && RT_QNODES>(sc, cam, hb.px, hb.py, hb.pz, st);
+                            lit = !lane_occluded<W, S, W == 8 && RT_QNODES, COUNT>(sc, cam, hb.px, hb.py, hb.pz, st, &shc);
                             sh_cast++;
                             sh_occ += !lit;
                         }
@@ -546,6 +561,10 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
         if (SHADOW && fp.counters) {
             wave_add<20>(fp.counters + 24, sh_cast);
             wave_add<20>(fp.counters + 25, sh_occ);
+            if (COUNT) {
+                wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 29, shc.pre);
+            }
         }
         if (COUNT && fp.counters) {
             wave_add<24>(fp.counters + 1, tot.nodes);

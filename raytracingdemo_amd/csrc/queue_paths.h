@@ -140,16 +140,18 @@ __device__ __forceinline__ void q_bounce(const RtDevScene& sc, const RtFramePara
 // queued: the radiance without this vertex goes to its destination now and
 // the occlusion record is returned in `queue` (q_shadow_append; the binned
 // occlusion pass adds the colour if the light sees the vertex).
-template <int W, int S, int SH>
+// COUNT (SH 1): the occlusion walk's fetch counts go to *shc.
+template <int W, int S, int SH, bool COUNT = false>
 __device__ __forceinline__ void q_light(const RtDevScene& sc, const PathQs& qs, const RtFrameCam& cam, int b,
                                         const RT_G double* Lin, int32_t tri, double px, double py, double pz,
                                         bool emit, int kout, uint32_t slot, uint32_t path, LaneStack<S>& st,
-                                        uint32_t& sh_cast, uint32_t& sh_occ, bool& queue, uint32_t& dst) {
+                                        uint32_t& sh_cast, uint32_t& sh_occ, bool& queue, uint32_t& dst,
+                                        LaneCounts* shc = nullptr) {
     bool lit = tri >= 0;
     queue = false;
     dst = emit ? (0x80000000u | ((uint32_t)kout << 30) | slot) : path;
     if (SH == 1 && lit && b > 0) {
-        lit = !lane_occluded<W, S, W == 8 && RT_QNODES>(sc, cam, px, py, pz, st);
+        lit = !lane_occluded<W, S, W == 8 && RT_QNODES, COUNT>(sc, cam, px, py, pz, st, shc);
         sh_cast++;
         sh_occ += !lit;
     }
@@ -680,6 +682,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t segs = 0, sh_cast = 0, sh_occ = 0;
+    LaneCounts shc;  // COUNT, SH 1: the occlusion walks' fetches
     LaneCounts tot;
     for (;;) {
         uint32_t base = 0;
@@ -739,8 +742,8 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         bool qd = false;
         uint32_t dst = 0;
         if (act && !fall)
-            q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
-                              sh_cast, sh_occ, qd, dst);
+            q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
+                              sh_cast, sh_occ, qd, dst, &shc);
         if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
@@ -748,6 +751,10 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         if (SH == 1) {
             wave_add<24>(fp.counters + 24, sh_cast);
             wave_add<24>(fp.counters + 25, sh_occ);
+            if (COUNT) {
+                wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 29, shc.pre);
+            }
         }
         if (COUNT) {
             wave_add<28>(fp.counters + 1, tot.nodes);
@@ -782,6 +789,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment_dyn(RtDevScene sc, 
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t segs = 0, sh_cast = 0, sh_occ = 0;
+    LaneCounts shc;  // COUNT, SH 1: the occlusion walks' fetches
     LaneCounts tot;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     uint32_t e = kNone;      // the lane's entry under walk
@@ -897,8 +905,8 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment_dyn(RtDevScene sc, 
             bool qd = false;
             uint32_t dst = 0;
             if (act && !fall)
-                q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, E) + 6, win.tri, px, py, pz, emit, qout, slot, path,
-                                  st, sh_cast, sh_occ, qd, dst);
+                q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, E) + 6, win.tri, px, py, pz, emit, qout, slot, path,
+                                  st, sh_cast, sh_occ, qd, dst, &shc);
             if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
             if (e != kNone) reload_q();
             continue;
@@ -910,6 +918,10 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment_dyn(RtDevScene sc, 
         if (SH == 1) {
             wave_add<24>(fp.counters + 24, sh_cast);
             wave_add<24>(fp.counters + 25, sh_occ);
+            if (COUNT) {
+                wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 29, shc.pre);
+            }
         }
         if (COUNT) {
             wave_add<28>(fp.counters + 1, tot.nodes);
@@ -1010,7 +1022,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_shade(RtDevScene sc, RtFram
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t sh_cast = 0, sh_occ = 0;
-    LaneCounts tot;
+    LaneCounts tot, shc;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 2, 64u);  // (the pull line's third word)
@@ -1051,14 +1063,18 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_shade(RtDevScene sc, RtFram
         bool qd = false;
         uint32_t dst = 0;
         if (act && !fall)
-            q_light<W, S, SH>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
-                              sh_cast, sh_occ, qd, dst);
+            q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
+                              sh_cast, sh_occ, qd, dst, &shc);
         if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         if (SH == 1) {
             wave_add<24>(fp.counters + 24, sh_cast);
             wave_add<24>(fp.counters + 25, sh_occ);
+            if (COUNT) {
+                wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 29, shc.pre);
+            }
         }
         if (COUNT) {
             wave_add<28>(fp.counters + 2, tot.tris);
@@ -1073,7 +1089,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_shade(RtDevScene sc, RtFram
 #ifndef RT_SL_WPE
 #define RT_SL_WPE 6
 #endif
-template <int W, int S>
+template <int W, int S, bool COUNT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SL_WPE)))
 k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
     __shared__ uint2 lds[S][256];
@@ -1084,6 +1100,7 @@ k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t occl = 0, cast = 0;
+    LaneCounts shc;
     for (;;) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 1, 64u);
@@ -1093,7 +1110,7 @@ k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
         if (e >= n) continue;
         const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
         const double px = r[0], py = r[1], pz = r[2];
-        const bool occ = lane_occluded<W, S, W == 8 && RT_QNODES>(sc, cam, px, py, pz, st);
+        const bool occ = lane_occluded<W, S, W == 8 && RT_QNODES, COUNT>(sc, cam, px, py, pz, st, &shc);
         cast++;
         occl += occ;
         if (!occ) {
@@ -1112,6 +1129,10 @@ k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
     if (fp.counters) {
         wave_add<24>(fp.counters + 24, cast);
         wave_add<24>(fp.counters + 25, occl);
+        if (COUNT) {
+            wave_add<28>(fp.counters + 28, shc.nodes);
+            wave_add<28>(fp.counters + 29, shc.pre);
+        }
     }
 }
 
@@ -1133,7 +1154,7 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
     const uint32_t stride = gridDim.x * 256u;
     const uint32_t iters = (n + stride - 1) / stride;
     uint32_t sh_cast = 0, sh_occ = 0;
-    LaneCounts tot;
+    LaneCounts tot, shc;
     for (uint32_t it = 0; it < iters; it++) {
         const uint32_t k = it * stride + blockIdx.x * 256u + (uint32_t)tid;
         bool emit = false;
@@ -1177,14 +1198,18 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
         bool qd = false;
         uint32_t dst = 0;
         if (k < n)
-            q_light<W, S, SH>(sc, qs, cam, b, b == 0 ? nullptr : q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit,
-                              qout, slot, path, st, sh_cast, sh_occ, qd, dst);
+            q_light<W, S, SH, COUNT>(sc, qs, cam, b, b == 0 ? nullptr : q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit,
+                              qout, slot, path, st, sh_cast, sh_occ, qd, dst, &shc);
         if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         if (SH == 1) {
             wave_add<24>(fp.counters + 24, sh_cast);
             wave_add<24>(fp.counters + 25, sh_occ);
+            if (COUNT) {
+                wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 29, shc.pre);
+            }
         }
         if (COUNT) {
             wave_add<28>(fp.counters + 1, tot.nodes);

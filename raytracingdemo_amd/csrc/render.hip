@@ -1347,7 +1347,7 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
     }
     hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, COUNT, SH>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
     if constexpr (SH == 3)  // the records in emission order, per lane
-        hipLaunchKernelGGL((k_sh_lane<W, RT_Q_STACK>), grid, blk, 0, s, sc, fp, aux, qs, b);
+        hipLaunchKernelGGL((k_sh_lane<W, RT_Q_STACK, COUNT>), grid, blk, 0, s, sc, fp, aux, qs, b);
     if constexpr (SH == 2) {
         // the segment's occlusion records: binned by direction from the light,
         // then walked 64 at a time by the wave-cooperative any-hit walk

@@ -669,9 +669,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
 #else
 #define RT_Q_ATTR
 #endif
-template <int W, int S, int K, bool COUNT, int SH>
+// WAVE (W = 8, stack bound <= 128): the wave's 64 entries walked together by
+// wave_walk (path_kernel.h: scalar child records once per wave, each lane's
+// own slab tests and fp32 triangle filter) instead of 64 per-lane walks; the
+// wave stack is row 0 of the per-lane stack's LDS block, free during the walk.
+template <int W, int S, int K, bool COUNT, int SH, bool WAVE = false>
 __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                              PathQs qs, uint32_t frame, int b, int bounces) {
+    static_assert(!WAVE || (W == 8 && RT_PATHS_DEFER), "wave-walked segments: 8-wide trees");
     __shared__ uint2 lds[S][256];
     __shared__ uint2 cand[K][256];
     const int tid = threadIdx.x;
@@ -697,11 +702,29 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         win.tri = -1;
         double px = 0.0, py = 0.0, pz = 0.0;
         uint32_t path = 0;
+        float tcull = -1.f;
+        int nc = 0;
+        bool over = false;
+        if constexpr (WAVE) {
+            Ray64 ray;
+            double L[3];
+            if (act) {
+                q_load(qs, qin, e, ray, L, path);
+            } else {  // (a lane past the queue's end: valid = false, it enters no box)
+                ray.ox = ray.oy = ray.oz = 0.0;
+                ray.dx = 1.0;
+                ray.dy = ray.dz = 0.0;
+            }
+            const float pd = ray_pad(sc, ray);
+            const Ray32 q = make_ray32<true>(ray, pd);
+            const float tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
+            uint32_t* wstack = reinterpret_cast<uint32_t*>(&lds[0][tid & ~63]);  // 128 u32 of this wave's row
+            LaneCounts lc;
+            wave_walk<W, K, COUNT>(sc, fp, q, pd, tsl, act, wstack, cand, tid, lc, tcull, nc, over);
+            if (COUNT) tot.pre += lc.pre;
+        }
         if (act) {
-            float tcull;
-            int nc;
-            bool over;
-            {
+            if constexpr (!WAVE) {
                 // only the fp32 view of the ray lives through the walk
                 Ray64 ray;
                 double L[3];
@@ -745,173 +768,6 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
             q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
                               sh_cast, sh_occ, qd, dst, &shc);
         if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
-    }
-    if (fp.counters) {
-        wave_add<24>(fp.counters, segs);
-        if (SH == 1) {
-            wave_add<24>(fp.counters + 24, sh_cast);
-            wave_add<24>(fp.counters + 25, sh_occ);
-            if (COUNT) {
-                wave_add<28>(fp.counters + 28, shc.nodes);
-                wave_add<28>(fp.counters + 29, shc.pre);
-            }
-        }
-        if (COUNT) {
-            wave_add<28>(fp.counters + 1, tot.nodes);
-            wave_add<28>(fp.counters + 6, tot.pre);
-            wave_add<28>(fp.counters + 2, tot.tris);
-            wave_add<28>(fp.counters + 3, tot.chain);
-        }
-    }
-}
-
-// Segment b with lane refill (RT_Q_DYN=1): a lane whose walk ends hands its
-// candidates to HBM (the split segment's lists), puts its entry on the wave's
-// done list in LDS and takes the next queued ray at once, so the walk keeps
-// its lanes busy instead of waiting for the wave's longest walk; when 64
-// entries are done (or the queue is drained) the wave resolves and shades
-// them together, one per lane, as k_q_shade does.  The fp32 view of a lane's
-// ray is rebuilt from its queue entry after each such batch rather than held
-// through it.
-template <int W, int S, int K, bool COUNT, int SH>
-__global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment_dyn(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
-                                                                 PathQs qs, uint32_t frame, int b, int bounces) {
-    static_assert(K <= RT_Q_KMAX, "candidate lists of the split segment");
-    __shared__ uint2 lds[S][256];
-    __shared__ uint2 cand[K][256];
-    __shared__ uint32_t done_e[4][128];  // per wave: entries whose walk ended, not yet resolved
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wv = tid >> 6;
-    const int qin = (b - 1) & 1, qout = b & 1;
-    const uint32_t n = *qc_emit(qs, b - 1);
-    LaneStack<S> st;
-    st.attach(lds, aux, tid);
-    const RtFrameCam cam = frame_cam(fp, 0);
-    uint32_t segs = 0, sh_cast = 0, sh_occ = 0;
-    LaneCounts shc;  // COUNT, SH 1: the occlusion walks' fetches
-    LaneCounts tot;
-    constexpr uint32_t kNone = 0xFFFFFFFFu;
-    uint32_t e = kNone;      // the lane's entry under walk
-    uint32_t ndone = 0;      // (wave-uniform) entries on the done list
-    bool drained = false;    // (wave-uniform) the queue has no entry left
-    LaneWalk<W, S, K, COUNT, W == 8 && RT_QNODES> w;
-    auto start = [&](uint32_t k) {  // the walk of entry k from the root
-        const RT_G double* p = q_entry(qs, qin, k);
-        Ray64 ray;
-        ray.ox = p[0];
-        ray.oy = p[1];
-        ray.oz = p[2];
-        ray.dx = p[3];
-        ray.dy = p[4];
-        ray.dz = p[5];
-        ray.ix = ray.iy = ray.iz = 0.0;
-        const Ray32 q = make_ray32<true>(ray, ray_pad(sc, ray));
-        w.begin(sc, q, round_up_f(0x1p-40 * ((double)q.co + 1.0)), st);
-    };
-    auto reload_q = [&]() {  // the fp32 view again after a batch (walk state other than q is kept)
-        const RT_G double* p = q_entry(qs, qin, e);
-        Ray64 ray;
-        ray.ox = p[0];
-        ray.oy = p[1];
-        ray.oz = p[2];
-        ray.dx = p[3];
-        ray.dy = p[4];
-        ray.dz = p[5];
-        ray.ix = ray.iy = ray.iz = 0.0;
-        w.q = make_ray32<true>(ray, ray_pad(sc, ray));
-    };
-    for (;;) {
-        // refill the lanes without a ray (one atomic per wave)
-        if (!drained) {
-            const uint64_t need = __ballot(e == kNone);
-            if (need) {
-                const int leader = __builtin_ctzll(need);
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(qc_pull(qs, b), (uint32_t)__builtin_popcountll(need));
-                base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-                if (base + (uint32_t)__builtin_popcountll(need) >= n) drained = true;
-                if (e == kNone) {
-                    const uint32_t k = base + (uint32_t)__builtin_popcountll(need & ((1ull << lane) - 1ull));
-                    if (k < n) {
-                        e = k;
-                        start(k);
-                    }
-                }
-            }
-        }
-        const bool walking = e != kNone;
-        // one node or leaf visit
-        if (walking && w.cur != RT_INVALID_REF) w.step(sc, st, cand, tot);
-        // walks that ended: their lists to HBM, their entries to the done list
-        const bool fin = walking && w.cur == RT_INVALID_REF;
-        const uint64_t fm = __ballot(fin);
-        if (fin) {
-            uint32_t m = 0;
-            if (!w.over) {
-                for (int c = 0; c < w.nc; c++) {
-                    const uint2 v = cand[c][tid];
-                    if (__uint_as_float(v.y) > w.tcull) continue;
-                    reinterpret_cast<RT_G uint2*>(qs.wc)[(size_t)m * qs.cap + e] = v;
-                    m++;
-                }
-            }
-            qs.wn[e] = w.over ? (uint8_t)0xFF : (uint8_t)m;
-            qs.wt[e] = w.tcull;
-            done_e[wv][ndone + (uint32_t)__builtin_popcountll(fm & ((1ull << lane) - 1ull))] = e;
-            e = kNone;
-            segs++;
-        }
-        ndone += (uint32_t)__builtin_popcountll(fm);
-        const bool last = drained && __ballot(e != kNone) == 0;
-        if (ndone >= 64 || (last && ndone > 0)) {
-            // resolve, shade and bounce up to 64 done entries, one per lane
-            const uint32_t take = ndone < 64 ? ndone : 64;
-            ndone -= take;
-            const bool act = (uint32_t)lane < take;
-            const uint32_t E = act ? done_e[wv][ndone + (uint32_t)lane] : 0u;
-            bool emit = false, fall = false;
-            Ray64 nr;
-            Win win;
-            win.tri = -1;
-            double px = 0.0, py = 0.0, pz = 0.0;
-            uint32_t path = 0;
-            if (act) {
-                Ray64 ray;
-                double L[3];
-                q_load(qs, qin, E, ray, L, path);
-                const uint32_t cnt = qs.wn[E];
-                uint32_t fe = E | kQFromPass0;
-                fall = cnt == 0xFFu;
-                if (!fall) {
-                    fe = E;
-                    LaneCounts lc;
-                    fall = resolve_cands<COUNT>(
-                               sc, with_inv(ray),
-                               [&](int c) { return reinterpret_cast<const RT_G uint2*>(qs.wc)[(size_t)c * qs.cap + E]; },
-                               (int)cnt, qs.wt[E], win, lc) != 0;
-                    if (COUNT) {
-                        tot.tris += lc.tris;
-                        tot.chain += lc.chain;
-                    }
-                }
-                if (fall) {
-                    qs.fb[qin * (size_t)qs.cap + atomicAdd(qc_fb(qs, b), 1u)] = fe;
-                } else if (win.tri >= 0) {
-                    q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
-                }
-            }
-            const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
-            bool qd = false;
-            uint32_t dst = 0;
-            if (act && !fall)
-                q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, E) + 6, win.tri, px, py, pz, emit, qout, slot, path,
-                                  st, sh_cast, sh_occ, qd, dst, &shc);
-            if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
-            if (e != kNone) reload_q();
-            continue;
-        }
-        if (last) break;
     }
     if (fp.counters) {
         wave_add<24>(fp.counters, segs);

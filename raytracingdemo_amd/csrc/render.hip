@@ -1326,25 +1326,42 @@ bool q_split() {
     const char* e = getenv("RT_Q_SPLIT");
     return e && e[0] == '1';
 }
-// RT_Q_DYN=1 (read per call): the segment kernel with lane refill (k_q_segment_dyn)
-bool q_dyn() {
-    const char* e = getenv("RT_Q_DYN");
-    return e && e[0] == '1';
+// A persistent grid of `kernel` (256-thread workgroups) filling every CU to
+// its occupancy (the query, once per process per kernel: every device of a
+// run is a gfx950).
+template <class K>
+dim3 occupancy_grid(K kernel) {
+    int dev = 0, cus = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 256, 0) != hipSuccess || n < 1) n = 1;
+    return dim3((unsigned)(cus * n));
+}
+// RT_Q_WAVE=n (read per call): bounce segments 1 .. n walked by the wave
+// (k_q_segment's WAVE instantiation; 8-wide trees within the wave stack)
+int q_wave_segments() {
+    const char* e = getenv("RT_Q_WAVE");
+    return e ? atoi(e) : 0;
 }
 template <int W, bool COUNT, int SH>
 void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                       uint32_t frame, int b, int bounces, hipStream_t s) {
     const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
-    if (q_dyn()) {
-        hipLaunchKernelGGL((k_q_segment_dyn<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame,
-                           b, bounces);
-    } else if (q_split()) {
+    if constexpr (W == 8) {
+        if (b <= q_wave_segments() && paths_primary_wave(sc)) {
+            hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH, true>), grid, blk, 0, s, sc, fp, aux, qs,
+                               frame, b, bounces);
+            goto fallback;
+        }
+    }
+    if (q_split()) {
         hipLaunchKernelGGL((k_q_walk<W, RT_QW_STACK, RT_Q_K, COUNT>), grid, blk, 0, s, sc, fp, aux, qs, b);
         hipLaunchKernelGGL((k_q_shade<W, RT_Q_STACK, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
     } else {
         hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
                            bounces);
     }
+fallback:
     hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, COUNT, SH>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
     if constexpr (SH == 3)  // the records in emission order, per lane
         hipLaunchKernelGGL((k_sh_lane<W, RT_Q_STACK, COUNT>), grid, blk, 0, s, sc, fp, aux, qs, b);
@@ -1356,7 +1373,8 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
             hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
             hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, pass * RT_SH_BITS);
         }
-        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), dim3((unsigned)aux.pgrid), blk, 0, s, sc, fp, aux, qs, b);
+        static const dim3 wgrid = occupancy_grid(k_sh_walk<W, COUNT>);
+        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), wgrid, blk, 0, s, sc, fp, aux, qs, b);
     }
 }
 // sh: 0 no occlusion rays, 1 per lane in the segment kernel, 2 queued and binned
@@ -1413,8 +1431,8 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     if (sh == 2 && (!qs.srec[0] || !qs.srec[1] || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
     // the wave-walked primary kernel uses no per-lane stack (no spill
-    // columns): the packet kernel's grid, 7 workgroups per CU
-    const dim3 pgrid((unsigned)(aux.pgrid > aux.grid ? aux.pgrid : aux.grid));
+    // columns): its own occupancy's grid
+    static const dim3 pgrid = occupancy_grid(k_q_primary<8, 1, false, true, true>);
     if (ev) (void)hipEventRecord(ev[0], s);
     switch (sc.width) {
         case 2:

@@ -788,157 +788,6 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
     }
 }
 
-// The split segment (RT_Q_SPLIT=1): k_q_walk is the fp32 walk alone —
-// no fp64, no path state, so it keeps fewer registers and more waves resident
-// to hide the node fetches' latency — and hands each entry's candidates to
-// k_q_shade through HBM (37 B per ray); k_q_shade resolves them in fp64 with
-// all 64 lanes busy, then k_q_segment's tail (bounce, occlusion, radiance).
-#ifndef RT_QW_WPE
-#define RT_QW_WPE 6  // waves per SIMD of k_q_walk
-#endif
-#ifndef RT_QW_STACK
-#define RT_QW_STACK 8  // LDS stack ring entries per lane in k_q_walk
-#endif
-template <int W, int S, int K, bool COUNT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_QW_WPE)))
-k_q_walk(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
-    static_assert(K <= RT_Q_KMAX, "candidate lists of the split segment");
-    __shared__ uint2 lds[S][256];
-    __shared__ uint2 cand[K][256];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int qin = (b - 1) & 1;
-    const uint32_t n = *qc_emit(qs, b - 1);
-    LaneStack<S> st;
-    st.attach(lds, aux, tid);
-    LaneCounts tot;
-    uint32_t segs = 0;
-    for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qc_pull(qs, b), 64u);
-        base = (uint32_t)__shfl((int)base, 0);
-        if (base >= n) break;
-        const uint32_t e = base + (uint32_t)lane;
-        if (e >= n) continue;
-        Ray32 q;
-        float tsl;
-        {
-            const RT_G double* p = q_entry(qs, qin, e);
-            Ray64 ray;
-            ray.ox = p[0];
-            ray.oy = p[1];
-            ray.oz = p[2];
-            ray.dx = p[3];
-            ray.dy = p[4];
-            ray.dz = p[5];
-            ray.ix = ray.iy = ray.iz = 0.0;
-            q = make_ray32<true>(ray, ray_pad(sc, ray));
-            tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
-        }
-        LaneCounts lc;
-        float tcull;
-        int nc;
-        bool over;
-        lane_walk<W, S, K, COUNT, W == 8 && RT_QNODES>(sc, q, tsl, st, cand, lc, tcull, nc, over);
-        uint32_t m = 0;
-        if (!over) {
-            for (int c = 0; c < nc; c++) {
-                const uint2 v = cand[c][tid];
-                if (__uint_as_float(v.y) > tcull) continue;  // cannot beat a certain hit
-                reinterpret_cast<RT_G uint2*>(qs.wc)[(size_t)m * qs.cap + e] = v;
-                m++;
-            }
-        }
-        qs.wn[e] = over ? (uint8_t)0xFF : (uint8_t)m;
-        qs.wt[e] = tcull;
-        segs++;
-        if (COUNT) {
-            tot.nodes += lc.nodes;
-            tot.pre += lc.pre;
-        }
-    }
-    if (fp.counters) {
-        wave_add<24>(fp.counters, segs);
-        if (COUNT) {
-            wave_add<28>(fp.counters + 1, tot.nodes);
-            wave_add<28>(fp.counters + 6, tot.pre);
-        }
-    }
-}
-
-template <int W, int S, bool COUNT, int SH>
-__global__ void __launch_bounds__(256) RT_Q_ATTR k_q_shade(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
-                                                           PathQs qs, uint32_t frame, int b, int bounces) {
-    __shared__ uint2 lds[S][256];  // (the per-lane occlusion walk's stack, SH == 1)
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int qin = (b - 1) & 1, qout = b & 1;
-    const uint32_t n = *qc_emit(qs, b - 1);
-    LaneStack<S> st;
-    st.attach(lds, aux, tid);
-    const RtFrameCam cam = frame_cam(fp, 0);
-    uint32_t sh_cast = 0, sh_occ = 0;
-    LaneCounts tot, shc;
-    for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 2, 64u);  // (the pull line's third word)
-        base = (uint32_t)__shfl((int)base, 0);
-        if (base >= n) break;
-        const uint32_t e = base + (uint32_t)lane;
-        const bool act = e < n;
-        bool emit = false, fall = false;
-        Ray64 nr;
-        Win win;
-        win.tri = -1;
-        double px = 0.0, py = 0.0, pz = 0.0;
-        uint32_t path = 0;
-        if (act) {
-            Ray64 ray;
-            double L[3];
-            q_load(qs, qin, e, ray, L, path);
-            const uint32_t cnt = qs.wn[e];
-            uint32_t fe = e | kQFromPass0;
-            fall = cnt == 0xFFu;
-            if (!fall) {
-                fe = e;
-                LaneCounts lc;
-                fall = resolve_cands<COUNT>(sc, with_inv(ray), [&](int c) { return reinterpret_cast<const RT_G uint2*>(qs.wc)[(size_t)c * qs.cap + e]; },
-                                            (int)cnt, qs.wt[e], win, lc) != 0;
-                if (COUNT) {
-                    tot.tris += lc.tris;
-                    tot.chain += lc.chain;
-                }
-            }
-            if (fall) {
-                qs.fb[qin * (size_t)qs.cap + atomicAdd(qc_fb(qs, b), 1u)] = fe;
-            } else if (win.tri >= 0) {
-                q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
-            }
-        }
-        const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
-        bool qd = false;
-        uint32_t dst = 0;
-        if (act && !fall)
-            q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
-                              sh_cast, sh_occ, qd, dst, &shc);
-        if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
-    }
-    if (fp.counters) {
-        if (SH == 1) {
-            wave_add<24>(fp.counters + 24, sh_cast);
-            wave_add<24>(fp.counters + 25, sh_occ);
-            if (COUNT) {
-                wave_add<28>(fp.counters + 28, shc.nodes);
-                wave_add<28>(fp.counters + 29, shc.pre);
-            }
-        }
-        if (COUNT) {
-            wave_add<28>(fp.counters + 2, tot.tris);
-            wave_add<28>(fp.counters + 3, tot.chain);
-        }
-    }
-}
-
 // Queued occlusion records walked per lane, in the order the segment kernel
 // appended them (RT_SHADOW_RAYS=rec: no binning): lane_occluded in a lean
 // kernel of its own.

@@ -1318,14 +1318,6 @@ hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const 
 // Queued path tracing of one pose (queue_paths.h): the primary segments of
 // every path, then per bounce segment the compacted queue and its fall-back
 // list, then the pixel sums.  The control words are zeroed here.
-// RT_Q_SPLIT=1 (read per call): the walk and the resolve of a segment in two
-// kernels (k_q_walk, k_q_shade) instead of k_q_segment: 236 vs 167 ms per
-// pose on config c5 — the split exposes the resolve's fp64 record gathers,
-// which the fused kernel overlaps with other waves' walks
-bool q_split() {
-    const char* e = getenv("RT_Q_SPLIT");
-    return e && e[0] == '1';
-}
 // A persistent grid of `kernel` (256-thread workgroups) filling every CU to
 // its occupancy (the query, once per process per kernel: every device of a
 // run is a gfx950).
@@ -1354,13 +1346,8 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
             goto fallback;
         }
     }
-    if (q_split()) {
-        hipLaunchKernelGGL((k_q_walk<W, RT_QW_STACK, RT_Q_K, COUNT>), grid, blk, 0, s, sc, fp, aux, qs, b);
-        hipLaunchKernelGGL((k_q_shade<W, RT_Q_STACK, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
-    } else {
-        hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
-                           bounces);
-    }
+    hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
+                       bounces);
 fallback:
     hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, COUNT, SH>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
     if constexpr (SH == 3)  // the records in emission order, per lane

@@ -478,8 +478,8 @@ PathWs ensure_pw(Replica& r, uint64_t P) {
 // Queued path-tracer workspace for P paths (grown, never shrunk): two
 // segment queues (80 B per entry), the final radiance (24 B per path), two
 // fall-back lists (4 B per path each) and the control words.
-// (+ the occlusion records, 32 B twice, and the split segment's candidate lists, 37 B)
-constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4 + 2 * 32 + 8 * RT_Q_KMAX + 4 + 1;
+// (+ the occlusion records, 32 B twice)
+constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4 + 2 * 32;
 PathQs ensure_pq(Replica& r, uint64_t P) {
     if (r.pq_cap < P) {
         quiesce(r);  // earlier launches may still use it
@@ -504,10 +504,6 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
     const uint64_t o_bh = align_up<char>(o_ctl + RT_QC_WORDS(64) * sizeof(uint32_t));
     qs.bhist = reinterpret_cast<uint32_t*>(base + o_bh);
     qs.sh_blocks = RT_SH_BLOCKS;
-    const uint64_t o_wc = align_up<char>(o_bh + (uint64_t)RT_SH_BINS * RT_SH_BLOCKS * sizeof(uint32_t));
-    qs.wc = reinterpret_cast<uint64_t*>(base + o_wc);
-    qs.wt = reinterpret_cast<float*>(base + align_up<char>(o_wc + c * 8 * RT_Q_KMAX));
-    qs.wn = reinterpret_cast<uint8_t*>(base + align_up<char>(align_up<char>(o_wc + c * 8 * RT_Q_KMAX) + c * 4));
     qs.cap = (uint32_t)c;
     return qs;
 }

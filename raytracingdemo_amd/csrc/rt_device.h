@@ -261,14 +261,7 @@ struct PathQs {
     RT_G double* srec[2];
     RT_G uint32_t* bhist;  // [bins][sh_blocks]
     uint32_t sh_blocks;
-    // the split segment (k_q_walk -> k_q_shade): per queue entry the walk's
-    // surviving candidates [RT_Q_KMAX][cap] {triangle, t lower bound}, their
-    // count (0xFF: overflow) and the culling distance
-    RT_G uint64_t* wc;     // (uint2 entries)
-    RT_G uint8_t* wn;
-    RT_G float* wt;
 };
-#define RT_Q_KMAX 4
 #define RT_QC_WORDS(bounces) (4 * ((bounces) + 1) * 16)
 // occlusion-ray order: a cube map around the light, 512 x 512 cells per face
 // in Morton order (21-bit keys), counting-sorted in two passes of RT_SH_BITS

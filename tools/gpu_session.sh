@@ -66,7 +66,8 @@ for s in $STEPS; do
                run pmcpw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcp -o write \
                    -- python bench.py --paths --steps 1 --warmup 0 --no-cpu && \
                python tools/pmc_traffic.py gpurun_out/pmcp/fetch_counter_collection.csv \
-                   gpurun_out/pmcp/write_counter_collection.csv gpurun_out/pmcp_key.txt gpurun_out/pmc_traffic_paths.json k_paths ;;
+                   gpurun_out/pmcp/write_counter_collection.csv gpurun_out/pmcp_key.txt gpurun_out/pmc_traffic_paths.json \
+                   ${PATHS_KERNEL:-queue} ;;
         profpaths) run profp 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profp -o paths \
                    -- python bench.py --paths --steps 3 --warmup 1 --no-cpu ;;
         variants) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
@@ -98,8 +99,9 @@ for s in $STEPS; do
                    run sqp$pn 900 rocprofv3 --pmc $pass --output-format csv -d gpurun_out/sqp -o sqp$pn \
                        -- python bench.py --paths --steps 1 --warmup 0 --no-cpu --key-out gpurun_out/pmcp_key.txt || exit 1
                done
-               python tools/pmc_summary.py gpurun_out/sqp/sqp*_counter_collection.csv --match k_paths > gpurun_out/sqp_summary.txt
-               python tools/pmc_valu.py --kernel k_paths gpurun_out/pmcp_key.txt gpurun_out/pmc_valu_paths.json \
+               for k in k_q_ k_sh_; do python tools/pmc_summary.py gpurun_out/sqp/sqp*_counter_collection.csv --match $k; done \
+                   > gpurun_out/sqp_summary.txt
+               python tools/pmc_valu.py --kernel ${PATHS_KERNEL:-queue} gpurun_out/pmcp_key.txt gpurun_out/pmc_valu_paths.json \
                    gpurun_out/sqp/sqp*_counter_collection.csv ;;
         ab)    # A/B over environment settings: AB_ENVS="A=1 B=2;A=3;..." (one bench per entry)
                i=0; IFS=';' read -ra cfgs <<< "${AB_ENVS:-}"

@@ -19,7 +19,9 @@ read bytes = F_walk + 2 (F_fused - F_walk); without it, 2 x FETCH_SIZE (an
 upper bound for a kernel with scalar reads).  WRITE_SIZE is taken as is.
 
 Usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV KEY_FILE OUT_JSON [KERNEL [WALK_CSV]]
-(KERNEL: k_trace_packet, the default, or k_paths for config c5)
+(KERNEL: k_trace_packet, the default, k_paths for config c5's megakernel, or
+"queue" for the queued path tracer: every k_q_* / k_sh_* dispatch of a pose,
+summed, per pose)
 """
 import collections
 import csv
@@ -36,7 +38,47 @@ def counting(name):
     return bool(m and m.group(1) == "true")
 
 
+QUEUE = re.compile(r"k_q_|k_sh_")
+
+
+def queue_counting(name):
+    """The queued pipeline's COUNT instantiations (queue_paths.h):
+    k_q_primary<W, S, COUNT, ..>, k_q_segment<W, S, K, COUNT, ..>,
+    k_q_fallback<W, S, COUNT, ..>, k_sh_walk<W, COUNT>, k_sh_lane<W, S, COUNT>."""
+    m = (re.search(r"k_q_primary<\d+, \d+, (true|false)", name) or re.search(r"k_q_segment<\d+, \d+, \d+, (true|false)", name)
+         or re.search(r"k_q_fallback<\d+, \d+, (true|false)", name) or re.search(r"k_sh_walk<\d+, (true|false)", name)
+         or re.search(r"k_sh_lane<\d+, \d+, (true|false)", name))
+    return bool(m and m.group(1) == "true")
+
+
+def per_pose(path):
+    """KERNEL "queue": the queued path tracer's kernels summed per pose.  The
+    counting pose (first) is skipped: every dispatch before the first
+    non-counting k_q_primary; a pose starts at each non-counting k_q_primary."""
+    rows = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for r in csv.DictReader(open(path)):
+        if not QUEUE.search(r["Kernel_Name"]):
+            continue
+        d = int(r["Dispatch_Id"])
+        names[d] = r["Kernel_Name"]
+        rows[d][r["Counter_Name"]] += float(r["Counter_Value"])
+    poses = collections.defaultdict(lambda: collections.defaultdict(float))
+    pose = -1
+    for d in sorted(rows):
+        n = names[d]
+        if "k_q_primary<" in n and not queue_counting(n):
+            pose += 1
+        if pose < 0 or queue_counting(n):
+            continue
+        for c, v in rows[d].items():
+            poses[pose][c] += v
+    return poses
+
+
 def per_dispatch(path, kernel_sub):
+    if kernel_sub == "queue":
+        return per_pose(path)
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]

@@ -18,10 +18,12 @@ SIMDs' issue cycles its VALU and SALU instructions take,
 instruction issues in 1), with the VALU and SALU shares beside it.
 
 Usage: tools/pmc_valu.py [--kernel NAME] KEY_FILE OUT_JSON SQ_CSV [SQ_CSV ...]
-  NAME: k_trace_packet (default) or k_paths
+  NAME: k_trace_packet (default), k_paths, or queue (the queued path tracer's
+  kernels summed per pose)
 """
 import collections
 import csv
+import os
 import re
 import json
 import sys
@@ -45,14 +47,22 @@ def main():
     key_file, out = args[:2]
     tot = collections.defaultdict(float)
     disp = collections.defaultdict(set)
-    for path in args[2:]:
+    if kernel == "queue":  # the queued path tracer: its kernels summed per pose (pmc_traffic.per_pose)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from pmc_traffic import per_pose
+        for path in args[2:]:
+            for pose, cs in per_pose(path).items():
+                for c, v in cs.items():
+                    tot[c] += v
+                    disp[c].add((path, pose))
+    for path in args[2:] if kernel != "queue" else []:
         for r in csv.DictReader(open(path)):
             n = r["Kernel_Name"]
             if kernel + "<" not in n or counting(n):
                 continue
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
             disp[r["Counter_Name"]].add((path, r["Dispatch_Id"]))
-    per = {c: tot[c] / max(len(disp[c]), 1) for c in tot}  # per dispatch
+    per = {c: tot[c] / max(len(disp[c]), 1) for c in tot}  # per dispatch (queue: per pose)
     cycles = per["GRBM_GUI_ACTIVE"] / 8.0
     valu = per["SQ_INSTS_VALU"]
     salu = per.get("SQ_INSTS_SALU")

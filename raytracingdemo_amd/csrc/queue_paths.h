@@ -669,14 +669,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
 #else
 #define RT_Q_ATTR
 #endif
-// WAVE (W = 8, stack bound <= 128): the wave's 64 entries walked together by
-// wave_walk (path_kernel.h: scalar child records once per wave, each lane's
-// own slab tests and fp32 triangle filter) instead of 64 per-lane walks; the
-// wave stack is row 0 of the per-lane stack's LDS block, free during the walk.
-template <int W, int S, int K, bool COUNT, int SH, bool WAVE = false>
+template <int W, int S, int K, bool COUNT, int SH>
 __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                              PathQs qs, uint32_t frame, int b, int bounces) {
-    static_assert(!WAVE || (W == 8 && RT_PATHS_DEFER), "wave-walked segments: 8-wide trees");
     __shared__ uint2 lds[S][256];
     __shared__ uint2 cand[K][256];
     const int tid = threadIdx.x;
@@ -702,29 +697,11 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         win.tri = -1;
         double px = 0.0, py = 0.0, pz = 0.0;
         uint32_t path = 0;
-        float tcull = -1.f;
-        int nc = 0;
-        bool over = false;
-        if constexpr (WAVE) {
-            Ray64 ray;
-            double L[3];
-            if (act) {
-                q_load(qs, qin, e, ray, L, path);
-            } else {  // (a lane past the queue's end: valid = false, it enters no box)
-                ray.ox = ray.oy = ray.oz = 0.0;
-                ray.dx = 1.0;
-                ray.dy = ray.dz = 0.0;
-            }
-            const float pd = ray_pad(sc, ray);
-            const Ray32 q = make_ray32<true>(ray, pd);
-            const float tsl = round_up_f(0x1p-40 * ((double)q.co + 1.0));
-            uint32_t* wstack = reinterpret_cast<uint32_t*>(&lds[0][tid & ~63]);  // 128 u32 of this wave's row
-            LaneCounts lc;
-            wave_walk<W, K, COUNT>(sc, fp, q, pd, tsl, act, wstack, cand, tid, lc, tcull, nc, over);
-            if (COUNT) tot.pre += lc.pre;
-        }
         if (act) {
-            if constexpr (!WAVE) {
+            float tcull;
+            int nc;
+            bool over;
+            {
                 // only the fp32 view of the ray lives through the walk
                 Ray64 ray;
                 double L[3];

@@ -1329,26 +1329,12 @@ dim3 occupancy_grid(K kernel) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 256, 0) != hipSuccess || n < 1) n = 1;
     return dim3((unsigned)(cus * n));
 }
-// RT_Q_WAVE=n (read per call): bounce segments 1 .. n walked by the wave
-// (k_q_segment's WAVE instantiation; 8-wide trees within the wave stack)
-int q_wave_segments() {
-    const char* e = getenv("RT_Q_WAVE");
-    return e ? atoi(e) : 0;
-}
 template <int W, bool COUNT, int SH>
 void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                       uint32_t frame, int b, int bounces, hipStream_t s) {
     const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
-    if constexpr (W == 8) {
-        if (b <= q_wave_segments() && paths_primary_wave(sc)) {
-            hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH, true>), grid, blk, 0, s, sc, fp, aux, qs,
-                               frame, b, bounces);
-            goto fallback;
-        }
-    }
     hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
                        bounces);
-fallback:
     hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, COUNT, SH>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
     if constexpr (SH == 3)  // the records in emission order, per lane
         hipLaunchKernelGGL((k_sh_lane<W, RT_Q_STACK, COUNT>), grid, blk, 0, s, sc, fp, aux, qs, b);
@@ -1390,17 +1376,18 @@ void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLa
     }
 }
 
-// Occlusion rays of the queued pipeline: queued and binned (default), or
-// RT_SHADOW_RAYS=lane: walked per lane inside the segment kernel (read per call).
-// (The any-hit walk's wave stack holds kPacketStack entries: deeper trees
-// walk their occlusion rays per lane.)
-// RT_SHADOW_RAYS=rec: queued, walked per lane in emission order (no binning).
+// Occlusion rays of the queued pipeline (RT_SHADOW_RAYS, read per call):
+// walked per lane inside the segment kernel where the vertex is shaded
+// (default, "lane"); "rec": queued as records, walked per lane in emission
+// order by k_sh_lane; "bin": queued, sorted by direction from the light and
+// walked by the wave (k_sh_walk; its wave stack holds kPacketStack entries,
+// deeper trees stay per lane).  Config c5: 241 / 242 / 266 ms per pose.
 int queued_shadow_mode(const RtDevScene& sc, bool shadow) {
     if (!shadow) return 0;
     const char* e = getenv("RT_SHADOW_RAYS");
-    if (e && e[0] == 'l') return 1;
     if (e && e[0] == 'r') return 3;
-    return sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
+    if (e && e[0] == 'b') return sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
+    return 1;
 }
 
 hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,

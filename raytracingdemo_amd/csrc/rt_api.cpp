@@ -512,13 +512,17 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
 // "queue" — the queued tracer (queue_paths.h: compacted segment queues, lean
 // per-segment kernels); "mega" — the megakernel (path_kernel.h k_paths);
 // RT_PATHS_WF=1 — the round-2 wavefront tracer (wavefront_paths.h).
+// Unset: the faster of the two on config c5 — the queued tracer with
+// occlusion rays (241 vs 250 ms per pose), the megakernel without (157 vs
+// 166).
 enum class PathPipe { mega, queue, wf };
-PathPipe path_pipe() {
+PathPipe path_pipe(bool shadow) {
     const char* w = std::getenv("RT_PATHS_WF");
     if (w && std::atoi(w) != 0) return PathPipe::wf;
     const char* e = std::getenv("RT_PATHS");
     if (e && e[0] == 'q') return PathPipe::queue;
-    return PathPipe::mega;
+    if (e && e[0] == 'm') return PathPipe::mega;
+    return shadow ? PathPipe::queue : PathPipe::mega;
 }
 
 void check_camera(const rt_scene* s, const rt_camera* c) {
@@ -1298,7 +1302,7 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             tev = r->tev[r->tev_used++].data();
         }
         hipError_t e;
-        const PathPipe pipe = path_pipe();
+        const PathPipe pipe = path_pipe((flags & RT_FLAG_SHADOW) != 0);
         if (pipe == PathPipe::queue) {
             const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows * (uint64_t)spp;
             const PathQs qs = ensure_pq(*r, P);

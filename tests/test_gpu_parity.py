@@ -567,23 +567,21 @@ def test_paths_shadow_sponza_proxy_band(oracle):
     assert np.array_equal(sh["rgb"], full["rgb"].reshape(H, W, 3)[rows].reshape(-1, 3))
 
 
-@pytest.mark.parametrize("model,spp,bounces,shadow", [("stanford-bunny.obj", 16, 4, "queue"),
-                                                      ("suzanne.obj", 3, 3, "queue"), ("suzanne.obj", 3, 3, "lane"),
-                                                      ("stanford-bunny.obj", 16, 4, "wave"), ("teapot.obj", 4, 3, "rec"),
+@pytest.mark.parametrize("model,spp,bounces,shadow", [("stanford-bunny.obj", 16, 4, "bin"),
+                                                      ("suzanne.obj", 3, 3, "bin"), ("suzanne.obj", 3, 3, "lane"),
+                                                      ("stanford-bunny.obj", 16, 4, "lane"),
+                                                      ("teapot.obj", 4, 3, "rec"),
                                                       ("teapot.obj", 4, 2, None), ("stanford-bunny.obj", 1, 0, None)])
 def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, shadow, monkeypatch):
     """The queued pipeline (RT_PATHS=queue, queue_paths.h: the primary segments
     by the wave walk, then per bounce one compacted queue of every path's rays,
     a fall-back list for the exact per-lane traversal, and the pixel sums)
     renders the same bits as the megakernel and the oracle: packed (spp 16, 4)
-    and one-sample (spp 3, 1) primary tiles, occlusion rays (queued, binned by
+    and one-sample (spp 3, 1) primary tiles, occlusion rays (RT_SHADOW_RAYS=
+    lane, the default: per lane in the segment kernel; bin: queued, sorted by
     direction from the light and walked by the wave-cooperative any-hit walk;
-    or RT_SHADOW_RAYS=lane: per lane in the segment kernel; rec: from queued
-    records, per lane), the bounce segments walked by the wave (RT_Q_WAVE), a
-    strided shard, and the counts of segments and occlusion rays."""
-    if shadow == "wave":
-        monkeypatch.setenv("RT_Q_WAVE", "4")
-        shadow = "lane"
+    rec: from queued records, per lane), a strided shard, and the counts of
+    segments and occlusion rays."""
     if shadow:
         monkeypatch.setenv("RT_SHADOW_RAYS", shadow)
     shadow = shadow is not None

@@ -369,7 +369,12 @@ int rt_render_batch_spp_device(rt_scene *s, int device, const rt_camera *cams, i
  * (row * width + i) * spp + s; hit_count += samples whose primary ray hit.
  * Row shard as rt_render_rows_device; asynchronous on `stream`.  flags:
  * RT_FLAG_COUNT adds the ray segments traced to rt_frame_stats' rays,
- * RT_FLAG_TIMING times the kernel (trace_ms). */
+ * RT_FLAG_TIMING times the kernel (trace_ms).  Pipeline (same results
+ * either way): with RT_FLAG_SHADOW the queued tracer (every path of the pose
+ * in HBM queues, one kernel per bounce segment, 256 B of workspace per
+ * path), without it the megakernel; the environment variable RT_PATHS=queue
+ * or RT_PATHS=mega (read per call) overrides, and RT_SHADOW_RAYS=lane|rec|bin
+ * picks how the queued tracer walks its occlusion rays. */
 int rt_render_paths_device(rt_scene *s, int device, const rt_camera *cam, int frame, int spp, int bounces, int row0,
                            int row_stride, int nrows, const rt_device_out *out, void *stream, uint32_t flags);
 

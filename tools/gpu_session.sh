@@ -51,7 +51,7 @@ for s in $STEPS; do
         paths0) RT_PATHS_PRIMARY=0 run bench_paths0 300 python bench.py --paths --no-cpu --steps 3 --warmup 1 ;;
         paths) run bench_paths 300 python bench.py --paths --steps 3 --warmup 1 ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
-                   -- python bench.py --steps 10 --warmup 2 --no-cpu --no-dropin ;;
+                   -- python bench.py --steps 30 --warmup 4 --no-cpu --no-dropin ;;
         pmc)   run pmc 900 rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_sum --output-format csv -d gpurun_out/pmc -o fetch \
                    -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin --key-out gpurun_out/pmc_key.txt && \
                run pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc -o write \

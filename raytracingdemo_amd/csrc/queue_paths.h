@@ -35,7 +35,7 @@
 #pragma once
 
 #ifndef RT_Q_WPE
-#define RT_Q_WPE 5  // waves per SIMD of k_q_segment (register cap 96; the compiler ignores 6 with 24 KB of LDS per block)
+#define RT_Q_WPE 6  // waves per SIMD of k_q_segment (80 VGPRs): c5 234 vs 243 ms per pose at 5 (96 VGPRs)
 #endif
 #ifndef RT_Q_K
 #define RT_Q_K 4  // LDS candidates per lane in k_q_segment

@@ -447,6 +447,7 @@ __device__ __forceinline__ bool chain_fast_ok32(const float (&b)[6], const Ray64
 // at the same depth share cache lines instead of each dirtying its own.
 template <int S>
 struct LaneStack {
+    static_assert(S > 0 && (S & (S - 1)) == 0, "the LDS ring is indexed modulo S: a power of two");
     uint2 (*lds)[256];
     uint2* spill;     // this lane's column: aux.spill + global lane index
     uint32_t stride;  // lanes of the grid (aux.grid * 256)

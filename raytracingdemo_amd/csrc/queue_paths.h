@@ -315,52 +315,6 @@ __global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs
     }
 }
 
-// RT_Q_ORDER=1: queue (b - 1) & 1's entries grouped by the cell of their
-// origin (the bounce vertex) in the scene box, 16 x 16 x 8 cells in Morton
-// order (RT_SH_BINS bins), so the waves of one moment walk rays that start
-// near each other and share the nodes they fetch in L2.  One counting pass
-// (k_qo_hist, k_sh_scan, k_qo_scatter) writes the queue slots in that order
-// to qs.order; the segment kernel pulls through it.
-__device__ __forceinline__ uint32_t qo_key(const RtDevScene& sc, const RT_G double* o) {
-    const float lx = sc.root_box[0], hx = sc.root_box[1], ly = sc.root_box[2], hy = sc.root_box[3];
-    const float lz = sc.root_box[4], hz = sc.root_box[5];
-    auto cell = [](float v, float lo, float hi, int n) {
-        const float t = hi > lo ? (v - lo) / (hi - lo) * (float)n : 0.f;
-        const int c = (int)t;
-        return (uint32_t)(c < 0 ? 0 : c >= n ? n - 1 : c);
-    };
-    const uint32_t x = cell((float)o[0], lx, hx, 16), y = cell((float)o[1], ly, hy, 16), z = cell((float)o[2], lz, hz, 8);
-    uint32_t k = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        k |= ((x >> i) & 1u) << (3 * i);
-        k |= ((y >> i) & 1u) << (3 * i + 1);
-        if (i < 3) k |= ((z >> i) & 1u) << (3 * i + 2);
-    }
-    return k;  // 11 bits
-}
-__global__ void __launch_bounds__(1024) k_qo_hist(RtDevScene sc, PathQs qs, int b) {
-    __shared__ uint32_t h[RT_SH_BINS];
-    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) h[i] = 0;
-    __syncthreads();
-    const int qin = (b - 1) & 1;
-    uint32_t lo, hi;
-    sh_range(*qc_emit(qs, b - 1), blockIdx.x, lo, hi);
-    for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) atomicAdd(&h[qo_key(sc, q_entry(qs, qin, e))], 1u);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x] = h[i];
-}
-__global__ void __launch_bounds__(1024) k_qo_scatter(RtDevScene sc, PathQs qs, int b) {
-    __shared__ uint32_t cur[RT_SH_BINS];
-    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) cur[i] = qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x];
-    __syncthreads();
-    const int qin = (b - 1) & 1;
-    uint32_t lo, hi;
-    sh_range(*qc_emit(qs, b - 1), blockIdx.x, lo, hi);
-    for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024)
-        qs.order[atomicAdd(&cur[qo_key(sc, q_entry(qs, qin, e))], 1u)] = e;
-}
-
 // The wave-cooperative any-hit walk of 64 occlusion rays that share the light
 // as origin (one bin's worth of directions): wave_walk's loop with the
 // scalar child records and `ballot`, each lane's interval [0, tmax]; a lane
@@ -735,8 +689,8 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         if (lane == 0) base = atomicAdd(qc_pull(qs, b), 64u);
         base = (uint32_t)__shfl((int)base, 0);
         if (base >= n) break;
-        const bool act = base + (uint32_t)lane < n;
-        const uint32_t e = qs.order && act ? qs.order[base + lane] : base + (uint32_t)lane;
+        const uint32_t e = base + (uint32_t)lane;
+        const bool act = e < n;
         bool emit = false, fall = false;
         Ray64 nr;
         Win win;

@@ -1333,11 +1333,6 @@ template <int W, bool COUNT, int SH>
 void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                       uint32_t frame, int b, int bounces, hipStream_t s) {
     const dim3 grid((unsigned)aux.grid), blk(256), fgrid(64);
-    if (qs.order) {  // RT_Q_ORDER: the segment's entries grouped by their origin's cell
-        hipLaunchKernelGGL(k_qo_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, sc, qs, b);
-        hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
-        hipLaunchKernelGGL(k_qo_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, sc, qs, b);
-    }
     hipLaunchKernelGGL((k_q_segment<W, RT_Q_STACK, RT_Q_K, COUNT, SH>), grid, blk, 0, s, sc, fp, aux, qs, frame, b,
                        bounces);
     hipLaunchKernelGGL((k_q_fallback<W, kLdsStack, COUNT, SH>), fgrid, blk, 0, s, sc, fp, aux, qs, frame, b, bounces);
@@ -1395,16 +1390,8 @@ int queued_shadow_mode(const RtDevScene& sc, bool shadow) {
     return 1;
 }
 
-// RT_Q_ORDER=1 (read per call): bounce segments pulled in the order of their
-// origin's cell (k_qo_hist / k_qo_scatter) instead of queue order.
-bool q_order() {
-    const char* e = getenv("RT_Q_ORDER");
-    return e && e[0] == '1';
-}
-hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs_in,
+hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                           uint32_t frame, int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev) {
-    PathQs qs = qs_in;
-    if (!q_order()) qs.order = nullptr;
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
     const uint64_t paths = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.spp;
     if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.spill || aux.grid <= 0 || !qs.ctl ||

@@ -478,8 +478,8 @@ PathWs ensure_pw(Replica& r, uint64_t P) {
 // Queued path-tracer workspace for P paths (grown, never shrunk): two
 // segment queues (80 B per entry), the final radiance (24 B per path), two
 // fall-back lists (4 B per path each) and the control words.
-// (+ the occlusion records, 32 B twice, and the origin order, 4 B)
-constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4 + 2 * 32 + 4;
+// (+ the occlusion records, 32 B twice)
+constexpr uint64_t kPqBytesPerPath = 2 * 80 + 24 + 2 * 4 + 2 * 32;
 PathQs ensure_pq(Replica& r, uint64_t P) {
     if (r.pq_cap < P) {
         quiesce(r);  // earlier launches may still use it
@@ -504,8 +504,6 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
     const uint64_t o_bh = align_up<char>(o_ctl + RT_QC_WORDS(64) * sizeof(uint32_t));
     qs.bhist = reinterpret_cast<uint32_t*>(base + o_bh);
     qs.sh_blocks = RT_SH_BLOCKS;
-    qs.order = reinterpret_cast<uint32_t*>(
-        base + align_up<char>(o_bh + (uint64_t)RT_SH_BINS * RT_SH_BLOCKS * sizeof(uint32_t)));
     qs.cap = (uint32_t)c;
     return qs;
 }

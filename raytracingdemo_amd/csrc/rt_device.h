@@ -261,9 +261,6 @@ struct PathQs {
     RT_G double* srec[2];
     RT_G uint32_t* bhist;  // [bins][sh_blocks]
     uint32_t sh_blocks;
-    // RT_Q_ORDER: a segment's queue entries in the order of their origin's
-    // cell (queue slots, [cap]); nullptr: queue order
-    RT_G uint32_t* order;
 };
 #define RT_QC_WORDS(bounces) (4 * ((bounces) + 1) * 16)
 // occlusion-ray order: a cube map around the light, 512 x 512 cells per face

@@ -570,7 +570,6 @@ def test_paths_shadow_sponza_proxy_band(oracle):
 @pytest.mark.parametrize("model,spp,bounces,shadow", [("stanford-bunny.obj", 16, 4, "bin"),
                                                       ("suzanne.obj", 3, 3, "bin"), ("suzanne.obj", 3, 3, "lane"),
                                                       ("stanford-bunny.obj", 16, 4, "lane"),
-                                                      ("stanford-bunny.obj", 16, 4, "order"),
                                                       ("teapot.obj", 4, 3, "rec"),
                                                       ("teapot.obj", 4, 2, None), ("stanford-bunny.obj", 1, 0, None)])
 def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, shadow, monkeypatch):
@@ -582,11 +581,7 @@ def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, 
     lane, the default: per lane in the segment kernel; bin: queued, sorted by
     direction from the light and walked by the wave-cooperative any-hit walk;
     rec: from queued records, per lane), a strided shard, and the counts of
-    segments and occlusion rays; "order": the bounce segments pulled in the
-    order of their origin's cell (RT_Q_ORDER=1)."""
-    if shadow == "order":
-        monkeypatch.setenv("RT_Q_ORDER", "1")
-        shadow = "lane"
+    segments and occlusion rays."""
     if shadow:
         monkeypatch.setenv("RT_SHADOW_RAYS", shadow)
     shadow = shadow is not None

@@ -293,9 +293,11 @@ def test_redo_pool_overflow_retries_the_launch(oracle, monkeypatch, env):
             torch.cuda.synchronize()
             fs = s.frame_stats(0, reset=True)
             res[cap] = (ids.cpu().numpy().view(np.uint32).reshape(2, -1, spp), rgb.cpu().numpy().reshape(2, -1, 3),
-                        cnt.cpu().numpy(), fs["redo_rays"])
+                        cnt.cpu().numpy(), fs["redo_rays"], fs["node_fetches"])
             monkeypatch.delenv("RT_REDO_CAP", raising=False)
         assert res["1"][3] > 1, "the redo list did not overflow"
+        # the retry re-traces every pixel without counting: no fetches counted twice
+        assert 0 < res["1"][4] <= res[None][4], (res["1"][4], res[None][4])
         for f, (p, d) in enumerate(cams):
             o = ob.render(p, d, Wd, Hd) if spp == 1 else ob.render_spp(p, d, Wd, Hd, spp)
             oid = o["id"].reshape(-1, spp)

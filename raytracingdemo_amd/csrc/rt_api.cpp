@@ -1051,6 +1051,7 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
                 }
                 try {
                     wt = rt::build_walk_tree_device(s->soup, walk_device, rt::walk_max_leaf(), rt::walk_node_cost());
+                    rt::restructure_treelets(wt, rt::walk_treelet_passes());
                     rt::plan_wide_collapse(wt, 8);
                 } catch (...) {
                     if (ref.joinable()) ref.join();
@@ -1066,6 +1067,7 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
                 s->tree = rt::build_tree(s->soup, algo, k, collapse);
                 t2 = clk::now();
                 wt = rt::build_walk_tree(s->soup);
+                rt::restructure_treelets(wt, rt::walk_treelet_passes());
                 rt::plan_wide_collapse(wt, 8);
                 t3 = clk::now();
             }

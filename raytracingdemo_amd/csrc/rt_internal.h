@@ -83,6 +83,10 @@ WalkTree build_walk_tree(const Soup& s);
 // Rewrites the chosen subtrees as leaves in place and records the slots of
 // every wide node.  RT_WALK_COLLAPSE=greedy leaves the tree untouched.
 void plan_wide_collapse(WalkTree& w, int W);
+// Treelet restructuring of the binary walk tree (RT_WALK_TREELET = passes,
+// 0 = off; walk_tree.cpp), before plan_wide_collapse.
+void restructure_treelets(WalkTree& w, int passes);
+int walk_treelet_passes();
 // The same binned-SAH tree built on a gfx950 device (walk_build.hip): equal
 // splits, device-stable order inside nodes.
 WalkTree build_walk_tree_device(const Soup& s, int device, int lmax, double node_cost);

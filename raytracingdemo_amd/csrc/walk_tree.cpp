@@ -192,6 +192,144 @@ double env_cost(const char* name, double dflt) {
 
 }  // namespace
 
+// Treelet restructuring of the binary walk tree (Karras and Aila, "Fast
+// parallel construction of high-quality bounding volume hierarchies", HPG
+// 2013), before the wide collapse: for every inner node r, children before
+// parents, the treelet of up to 7 leaves grown from r by opening its largest
+// inner member is rebuilt with the SAH-optimal binary topology over those
+// leaves (a dynamic programme over the 2^7 leaf subsets), reusing the
+// treelet's inner nodes.  Cost model: inner A * RT_WALK_CT, leaf A * count.
+// Triangles never move between leaves, so the result is still a tree over
+// every triangle once; the leaves' ranges are then laid out again depth
+// first, so every subtree is a contiguous range of `order` for the collapse.
+void restructure_treelets(WalkTree& w, int passes) {
+    const size_t N = w.nodes.size();
+    if (N < 3 || w.nodes[0].left < 0 || passes < 1) return;
+    const double CI = node_cost();
+    auto box_of = [&](int32_t b) {
+        BBox bb;
+        for (int a = 0; a < 3; a++) { bb.mn[a] = w.nodes[b].mn[a]; bb.mx[a] = w.nodes[b].mx[a]; }
+        return bb;
+    };
+    std::vector<double> C(N, 0.0);
+    // post-order of the original shape (a restructured treelet's root keeps
+    // its id, and its other members were visited before it)
+    std::vector<int32_t> post;
+    post.reserve(N);
+    {
+        std::vector<std::pair<int32_t, bool>> st{{0, false}};
+        while (!st.empty()) {
+            auto [b, done] = st.back();
+            st.pop_back();
+            if (done || w.nodes[b].left < 0) { post.push_back(b); continue; }
+            st.push_back({b, true});
+            st.push_back({w.nodes[b].right, false});
+            st.push_back({w.nodes[b].left, false});
+        }
+    }
+    constexpr int TL = 7, NS = 1 << TL;
+    for (int pass = 0; pass < passes; pass++) {
+        for (int32_t r : post) {
+            WalkNode& nr = w.nodes[r];
+            if (nr.left < 0) { C[r] = box_of(r).area() * nr.count; continue; }
+            int32_t leaf[TL], inner[TL];
+            int nl = 2, ni = 1;
+            leaf[0] = nr.left;
+            leaf[1] = nr.right;
+            inner[0] = r;
+            while (nl < TL) {
+                int pick = -1;
+                double pa = -1.0;
+                for (int i = 0; i < nl; i++)
+                    if (w.nodes[leaf[i]].left >= 0) {
+                        const double a = box_of(leaf[i]).area();
+                        if (a > pa) { pa = a; pick = i; }
+                    }
+                if (pick < 0) break;
+                const int32_t m = leaf[pick];
+                inner[ni++] = m;
+                leaf[pick] = w.nodes[m].left;
+                leaf[nl++] = w.nodes[m].right;
+            }
+            // current cost of r (its children's C are final)
+            const double cur = box_of(r).area() * CI + C[nr.left] + C[nr.right];
+            if (nl < 3) { C[r] = cur; continue; }
+            const int full = (1 << nl) - 1;
+            BBox sb[NS];
+            double cost[NS], area[NS];
+            int part[NS];
+            for (int S = 1; S <= full; S++) {
+                const int low = S & -S;
+                if (S == low) {
+                    const int i = __builtin_ctz((unsigned)S);
+                    sb[S] = box_of(leaf[i]);
+                    cost[S] = C[leaf[i]];
+                } else {
+                    sb[S] = sb[S ^ low];
+                    sb[S].grow(sb[low]);
+                }
+                area[S] = sb[S].area();
+            }
+            for (int S = 1; S <= full; S++) {
+                if ((S & (S - 1)) == 0) continue;  // (one leaf: its subtree's cost)
+                // subsets in increasing value: every proper subset of S is smaller
+                double best = std::numeric_limits<double>::infinity();
+                int bp = 0;
+                const int low = S & -S;
+                for (int P = (S - 1) & S; P > 0; P = (P - 1) & S) {
+                    if (!(P & low)) continue;  // each split once: P holds S's lowest leaf
+                    const double v = cost[P] + cost[S ^ P];
+                    if (v < best) { best = v; bp = P; }
+                }
+                cost[S] = area[S] * CI + best;
+                part[S] = bp;
+            }
+            if (!(cost[full] < cur * (1.0 - 1e-9))) { C[r] = cur; continue; }
+            // rebuild: subset S -> node id (r for the whole set, then the
+            // treelet's other inner nodes in turn)
+            int next_inner = 1;
+            auto build = [&](auto&& self, int S) -> int32_t {
+                if ((S & (S - 1)) == 0) return leaf[__builtin_ctz((unsigned)S)];
+                const int32_t id = S == full ? r : inner[next_inner++];
+                const int32_t a = self(self, part[S]);
+                const int32_t b = self(self, S ^ part[S]);
+                WalkNode& m = w.nodes[id];
+                m.left = a;
+                m.right = b;
+                m.first = m.count = 0;
+                for (int k = 0; k < 3; k++) { m.mn[k] = sb[S].mn[k]; m.mx[k] = sb[S].mx[k]; }
+                C[id] = cost[S];
+                return id;
+            };
+            build(build, full);
+        }
+    }
+    // leaves' ranges depth first: subtrees contiguous again
+    std::vector<uint32_t> order(w.order.size());
+    uint32_t at = 0;
+    std::vector<int32_t> st{0};
+    while (!st.empty()) {
+        const int32_t b = st.back();
+        st.pop_back();
+        WalkNode& n = w.nodes[b];
+        if (n.left < 0) {
+            for (uint32_t i = 0; i < n.count; i++) order[at + i] = w.order[n.first + i];
+            n.first = at;
+            at += n.count;
+            continue;
+        }
+        st.push_back(n.right);
+        st.push_back(n.left);
+    }
+    if (at != order.size()) throw Error{RT_ERR_RUNTIME, "treelet restructuring lost triangles"};
+    w.order.swap(order);
+}
+int walk_treelet_passes() {
+    const char* e = std::getenv("RT_WALK_TREELET");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 0 && v <= 8 ? v : 0;
+}
+
 // The collapse as a dynamic programme (the SAH-optimal wide-BVH conversion of
 // Ylitie, Karras and Laine, HPG 2017), costs in the packet kernel's units:
 //   leaf(n)        = A(n) (c_leaf + c_tri cnt(n))        cnt(n) <= P

@@ -296,6 +296,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
     torch.cuda.synchronize(dev)
     cs = scene.frame_stats(local, reset=True)
     segs_per_pose = cs["rays"] / F
+    sh_per_pose = cs["shadow_rays"] / F  # occlusion rays (0 without RT_FLAG_SHADOW)
     if shadow_kind == "binned" and cs["shadow_rays"] and not cs["shadow_wave_nodes"]:
         shadow_kind = "inline"  # (a walk tree deeper than the binned walk's stack: per lane)
     # algorithmic bytes of one pose (the counting pass, W = 8): per segment the
@@ -361,9 +362,9 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         t = coll(torch.tensor([elapsed], dtype=torch.float64, device=dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        sg = coll(torch.tensor([segs_per_pose], dtype=torch.float64, device=dev))
+        sg = coll(torch.tensor([segs_per_pose, sh_per_pose], dtype=torch.float64, device=dev))
         dist.all_reduce(sg, op=dist.ReduceOp.SUM)
-        segs_per_pose = float(sg.item())
+        segs_per_pose, sh_per_pose = float(sg[0].item()), float(sg[1].item())
     nominal = a.steps * F * W * H * S * (1 + B)
     kernel_s = ks["trace_ms"] / max(ks["timed_launches"], 1) / 1e3
     if rank == 0:
@@ -406,6 +407,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
                        **({"ranks": {**ranks, "gather_bytes_per_step": world * rows * W * 3 * F}} if ranks else {}),
                        **({"rehearsal_not_a_measurement": True} if rehearse else {})},
             "segments_traced_per_s_M": round(segs_per_pose * a.steps * F / elapsed / 1e6, 2),
+            # every ray the pose traced: path segments plus occlusion rays
+            "rays_traced_per_s_M": round((segs_per_pose + sh_per_pose) * a.steps * F / elapsed / 1e6, 2),
             "segments_per_sample": round(segs_per_pose / (W * H * S), 3),
             "pipeline": ("queued: wave-walked primaries, compacted per-segment bounce queues, per-lane bounce walks"
                          if queued else "megakernel (k_paths)"),

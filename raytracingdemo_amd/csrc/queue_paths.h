@@ -544,6 +544,9 @@ constexpr uint32_t kQFromPass0 = 0x80000000u;
 #ifndef RT_QP_WPE
 #define RT_QP_WPE 6  // waves per SIMD of k_q_primary (wave-walked)
 #endif
+#ifndef RT_QP_CLAIM
+#define RT_QP_CLAIM 1  // units claimed per atomic by k_q_primary
+#endif
 template <int W, int S, bool COUNT, bool PACK, bool PRIM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ? RT_QP_WPE : RT_PATHS_WPE))) k_q_primary(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                                  PathQs qs, uint32_t frame, int bounces) {
@@ -567,10 +570,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
     for (;;) {
-        int unit = 0;
-        if (lane == 0) unit = (int)atomicAdd(qc_pull(qs, 0), 1u);
-        unit = __shfl(unit, 0);
-        if (unit >= units) break;
+        // RT_QP_CLAIM consecutive units per claim (one atomic on the shared
+        // counter per claim, not per unit)
+        int u0 = 0;
+        if (lane == 0) u0 = (int)atomicAdd(qc_pull(qs, 0), (uint32_t)RT_QP_CLAIM);
+        u0 = __shfl(u0, 0);
+        if (u0 >= units) break;
+        const int u1 = u0 + RT_QP_CLAIM < units ? u0 + RT_QP_CLAIM : units;
+        for (int unit = u0; unit < u1; unit++) {
         int i, r, s;
         if constexpr (PACK) {
             const int pl = lane / spp;
@@ -657,6 +664,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
             wave_add<24>(fp.counters + 6, lc.pre);
             wave_add<24>(fp.counters + 2, lc.tris);
             wave_add<24>(fp.counters + 3, lc.chain);
+        }
         }
     }
 }

@@ -513,8 +513,8 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
 // per-segment kernels); "mega" — the megakernel (path_kernel.h k_paths);
 // RT_PATHS_WF=1 — the round-2 wavefront tracer (wavefront_paths.h).
 // Unset: the faster of the two on config c5 — the queued tracer with
-// occlusion rays (241 vs 250 ms per pose), the megakernel without (157 vs
-// 166).
+// occlusion rays (234 vs 250 ms per pose), the megakernel without (156 vs
+// 161).
 enum class PathPipe { mega, queue, wf };
 PathPipe path_pipe(bool shadow) {
     const char* w = std::getenv("RT_PATHS_WF");

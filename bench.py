@@ -384,6 +384,11 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         except (OSError, ValueError, KeyError):
             pass
         achieved = alg_pose / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        # the per-lane convention beside it: the primary segments' wave-walk
+        # records counted once per lane (64) instead of once per wave; every
+        # other walk here is per lane in both
+        per_lane_pose = alg_pose + 63.0 * (cs["wave_nodes"] * 256 + cs["wave_tris"] * 48) / F
+        achieved_pl = per_lane_pose / kernel_s / 1e9 if kernel_s > 0 else 0.0
         valu = None
         try:
             pv = json.load(open(os.path.join(ROOT, "profiles", "pmc_valu_paths.json")))
@@ -424,6 +429,9 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
             "kernel_ms_avg": round(ks["trace_ms"] / max(ks["timed_launches"], 1), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac_per_lane": round(achieved_pl / HBM_PEAK_GBS, 4),
+                         "frac_dram": (round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
+                                       if traffic and kernel_s > 0 else None),
                          "kernel": ("queued pipeline (k_q_primary, k_q_segment, k_q_fallback, k_sh_*, k_q_accum; "
                                     "HIP events around the pose)" if queued else "k_paths"),
                          "alg_bytes_per_launch": round(alg_pose), "alg_bytes_parts": alg_parts,

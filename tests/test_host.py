@@ -208,3 +208,32 @@ def test_planned_collapse_is_deterministic_and_smaller(monkeypatch):
     assert g["layout_digest"] != a["layout_digest"]
     assert a["wide_nodes"] < 0.7 * g["wide_nodes"], (a["wide_nodes"], g["wide_nodes"])
     assert a["triangles"] == g["triangles"] and a["max_leaf_size"] <= 16
+
+
+def test_pmc_traffic_sums_the_queued_pipeline_per_pose(tmp_path):
+    """tools/pmc_traffic.py "queue": the queued path tracer's kernels summed per
+    pose, the counting pose (COUNT instantiations and everything before the
+    first timed k_q_primary) left out; pmc_valu.py reads the same sums."""
+    import csv
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import pmc_traffic
+    rows = []
+    names = ["k_q_primary<8, 1, true, true, true>(", "k_q_segment<8, 8, 4, true, 1>(", "k_q_accum(",  # counting pose
+             "k_q_primary<8, 1, false, true, true>(", "k_q_segment<8, 8, 4, false, 1>(", "k_sh_scatter(", "k_q_accum(",
+             "k_trace_packet<8, 128, 8, false, true, false, false>(",  # not the pipeline's
+             "k_q_primary<8, 1, false, true, true>(", "k_q_segment<8, 8, 4, false, 1>(", "k_q_accum("]
+    for d, n in enumerate(names):
+        rows.append({"Dispatch_Id": str(d + 1), "Kernel_Name": "void (anonymous namespace)::" + n + "RtDevScene)",
+                     "Counter_Name": "FETCH_SIZE", "Counter_Value": str(10.0 * (d + 1))})
+    path = tmp_path / "f.csv"
+    with open(path, "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    poses = pmc_traffic.per_pose(str(path))
+    assert sorted(poses) == [0, 1]
+    assert poses[0]["FETCH_SIZE"] == 40 + 50 + 60 + 70
+    assert poses[1]["FETCH_SIZE"] == 90 + 100 + 110
+    assert pmc_traffic.queue_counting("k_sh_lane<8, 8, true>(") and not pmc_traffic.queue_counting("k_sh_lane<8, 8, false>(")

@@ -38,7 +38,7 @@
 #define RT_Q_WPE 6  // waves per SIMD of k_q_segment (80 VGPRs): c5 234 vs 243 ms per pose at 5 (96 VGPRs)
 #endif
 #ifndef RT_Q_K
-#define RT_Q_K 4  // LDS candidates per lane in k_q_segment
+#define RT_Q_K 5  // LDS candidates per lane in k_q_segment (26 KB of LDS per block: 6 blocks per CU); c5 232.5 vs 233.9 ms at 4
 #endif
 #ifndef RT_Q_STACK
 #define RT_Q_STACK 8  // LDS stack ring entries per lane in k_q_segment

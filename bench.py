@@ -398,7 +398,11 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         except (OSError, ValueError, KeyError):
             pass
         line = {
-            "metric": f"Mrays/sec (primary + {B} diffuse bounces, {S}spp) on Sponza {W}x{H}",
+            # (the occlusion rays change the work per nominal ray: they are in
+            # the metric's name, so a no-shadow line stays comparable with the
+            # round-3 lines of the same name)
+            "metric": f"Mrays/sec (primary + {B} diffuse bounces, {S}spp" + (" + head-light occlusion" if shadow else "")
+                      + f") on Sponza {W}x{H}",
             "value": round(nominal / elapsed / 1e6, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "settle_steps": settled,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,

@@ -400,6 +400,11 @@ const char *rt_last_error(void);
 int rt_abi_version(void);
 /* device name of ordinal `device` (for reports); "" when unavailable */
 const char *rt_device_name(int device);
+/* Diagnostics: opens RCCL as the first multi-device render does — the copy
+ * the process has mapped already (PyTorch's), else ROCm's, never a second
+ * one — and returns the path of the mapped file (NULL: none, see
+ * rt_last_error). */
+const char *rt_rccl_path(void);
 
 #ifdef __cplusplus
 }

@@ -156,6 +156,8 @@ class Scene:
         return self._h
 
     def upload(self, devices=(0,)):
+        if len(devices) > 1:
+            N.prefer_torch_rccl()  # one RCCL per process (the multi-device render's gather)
         devs = (C.c_int * len(devices))(*devices)
         N.check(N.lib().rt_scene_upload(self._h, devs, len(devices)))
         self.devices = list(devices)

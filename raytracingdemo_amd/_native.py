@@ -36,7 +36,7 @@ EXPORTS = [
     "rt_render_frame", "rt_render_rows_device", "rt_render_batch_device", "rt_render_batch_spp_device", "rt_render_paths_device", "rt_frame_stats", "rt_scene_stats", "rt_scene_tree_dump",
     "rt_scene_destroy", "rt_last_error", "rt_abi_version", "rt_device_name", "rt_diag_raw",
     "rt_render_batch_multi", "rt_deinterleave_rows", "rt_scene_create_on_device", "rt_scene_build_times",
-    "rt_render_shard_device", "rt_shard_height", "rt_render_shard_device_job",
+    "rt_render_shard_device", "rt_shard_height", "rt_render_shard_device_job", "rt_rccl_path",
 ]
 
 
@@ -136,6 +136,8 @@ def lib() -> C.CDLL:
     L.rt_last_error.restype = C.c_char_p
     L.rt_device_name.restype = C.c_char_p
     L.rt_device_name.argtypes = [C.c_int]
+    if hasattr(L, "rt_rccl_path"):
+        L.rt_rccl_path.restype = C.c_char_p
     L.rt_abi_version.restype = C.c_int
     L.rt_load_obj.argtypes = [C.c_char_p, C.c_double, C.POINTER(dp), u64p]
     L.rt_free.argtypes = [C.c_void_p]
@@ -175,6 +177,16 @@ def lib() -> C.CDLL:
     L.rt_scene_destroy.argtypes = [C.c_void_p]
     _lib = L
     return L
+
+
+def prefer_torch_rccl() -> None:
+    """Map PyTorch's RCCL before the library opens one (a multi-device
+    upload), so the process holds one copy: the library reuses the mapped one
+    (rt_api.cpp rccl())."""
+    import importlib.util
+
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401  (libtorch_hip maps torch/lib/librccl.so)
 
 
 def check(status: int) -> None:

@@ -445,19 +445,32 @@ __device__ __forceinline__ bool chain_fast_ok32(const float (&b)[6], const Ray64
 // older entries spill to a global buffer interleaved over the lanes of the
 // grid (spill entry e of lane g at spill[e * stride + g]), so lanes of a wave
 // at the same depth share cache lines instead of each dirtying its own.
-template <int S>
+// C: columns of the LDS ring (256: one per thread of a 256-thread block; 64:
+// one wave's own ring, the packet kernel's exit path).
+template <int S, int C = 256>
 struct LaneStack {
     static_assert(S > 0 && (S & (S - 1)) == 0, "the LDS ring is indexed modulo S: a power of two");
-    uint2 (*lds)[256];
+    uint2 (*lds)[C];
     uint2* spill;     // this lane's column: aux.spill + global lane index
     uint32_t stride;  // lanes of the grid (aux.grid * 256)
     int tid;
     int top;
-    __device__ __forceinline__ void attach(uint2 (*l)[256], const RtLaunchAux& aux, int t) {
+    __device__ __forceinline__ void attach(uint2 (*l)[C], const RtLaunchAux& aux, int t) {
+        static_assert(C == 256, "one column per thread of the block");
         lds = l;
         spill = reinterpret_cast<uint2*>(aux.spill) + ((size_t)blockIdx.x * 256 + (size_t)t);
         stride = (uint32_t)aux.grid * 256u;
         tid = t;
+        top = 0;
+    }
+    // A wave's own ring (C = 64, column = lane) spilling at global lane
+    // `lane_g` of a grid of `lanes` lanes.
+    __device__ __forceinline__ void attach_wave(uint2 (*l)[C], RT_G uint64_t* sp, uint32_t lane_g, uint32_t lanes,
+                                                int lane) {
+        lds = l;
+        spill = reinterpret_cast<uint2*>(sp) + lane_g;
+        stride = lanes;
+        tid = lane;
         top = 0;
     }
     __device__ __forceinline__ void push(uint32_t ref, float t) {

@@ -90,6 +90,17 @@ __device__ __forceinline__ uint32_t lanes_of(const uint32_t (&ref)[W]) {
 }
 
 constexpr uint32_t kRedoPass1 = 0x80000000u;  // redo entry: start directly with the inline-verifying pass
+// An empty redo-list entry.  The list is all kRedoEmpty between launches
+// (whoever takes an entry resets it), so a wave that takes entries inside
+// the launch (packet_exit) can tell one whose store has not landed yet; no
+// entry is kRedoEmpty (launch pixels < 2^31).  Entries are swapped in and out
+// with device-scope atomics, performed at the memory side, so a reader on
+// another XCD sees them while the launch runs.
+constexpr uint32_t kRedoEmpty = 0xFFFFFFFFu;
+__device__ __forceinline__ void redo_put(const RtLaunchAux& aux, uint32_t v) {
+    const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
+    if (slot < aux.redo_cap) (void)atomicExch(aux.redo + slot, v);
+}
 // triangle records fetched per scalar round trip (walk-tree leaves hold ~2:
 // 2 measured 2% faster than 4)
 constexpr int kLeafChunk = 2;
@@ -750,8 +761,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
         if (spp == 1) {
             if (redo) {
                 // k_fixup redoes the pixel with the exact per-lane path
-                const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-                if (slot < aux.redo_cap) aux.redo[slot] = ob | (redo == 2u ? kRedoPass1 : 0u);
+                redo_put(aux, ob | (redo == 2u ? kRedoPass1 : 0u));
             } else {
                 store_sample(fp, ob, out, sh);
                 double c[3];
@@ -785,8 +795,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
             if (lane == base) {
                 const size_t pix = out_index(fp, pose, po);
                 if (bad) {
-                    const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-                    if (slot < aux.redo_cap) aux.redo[slot] = (uint32_t)pix;
+                    redo_put(aux, (uint32_t)pix);
                 } else {
                     store_rgb(fp, pix, acc);
                     res.hits = (uint32_t)__builtin_popcountll(hm);
@@ -929,8 +938,7 @@ __global__ void __launch_bounds__(256) k_resolve(RtDevScene sc, RtFrameParams fp
     if (active) {
         if (redo_any) {
             // k_fixup redoes every sample of the pixel with the exact per-lane path
-            const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-            if (slot < aux.redo_cap) aux.redo[slot] = (uint32_t)pix;
+            redo_put(aux, (uint32_t)pix);
             hits = 0;
         } else {
             store_rgb(fp, pix, acc);
@@ -991,8 +999,7 @@ __global__ void __launch_bounds__(256) k_average(RtFrameParams fp, RtLaunchAux a
         }
         const size_t pix = out_index(fp, p, po);
         if (redo) {
-            const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-            if (slot < aux.redo_cap) aux.redo[slot] = (uint32_t)pix;
+            redo_put(aux, (uint32_t)pix);
             hits = 0;
         } else {
             store_rgb(fp, pix, acc);
@@ -1082,6 +1089,124 @@ __device__ __forceinline__ bool side_copy(args_p A, int lane, uint32_t xq) {
     if (c >= (uint32_t)a.job_F * (uint32_t)a.job_H) return false;
     side_copy_row(a, c, lane);
     return true;
+}
+
+// Sum of a u32 over the wave's active lanes, in every lane.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
+// The end of a packet launch without a trailing kernel (aux.self_fix; the
+// host sets it when the redo list holds an entry for every pixel of the
+// launch, so the launch never needs a whole retry).  A trailing k_fixup
+// could only start once the next launch's persistent grid, issued on the
+// other stream, had drained — it holds every CU's wave slots, SGPRs and LDS
+// — so a launch ended one launch late.  Instead every wave,
+// once out of tiles:
+//  1. waits for its own hit-partial atomics (`s_waitcnt vmcnt(0)`: a
+//     device-scope atomic counts as complete once performed), so they are in
+//     before its exit ticket;
+//  2. takes redo-list entries while untaken ones exist, up to 64 at a time,
+//     by a compare-and-swap that never moves the claim counter past the
+//     count — an entry is taken only after its append, and the wave that
+//     appended it runs this loop afterwards, so every entry is taken — and
+//     finishes those pixels with k_fixup's per-lane exact path (its LDS ring
+//     is the wave's candidate list, its spill the slot's stack buffer);
+//  3. takes an exit ticket.  The wave with the last ticket (every other wave
+//     is past steps 1 and 2) folds the per-pose hit partials into the
+//     caller's counters, reports the redo count to the host and clears the
+//     work-queue block for the next launch — k_fixup's bookkeeping.
+// Step 2 out of line, so the kernel body's registers stay as they are
+// (inlined, the per-lane exact path raised the fused kernel's spills from
+// 36 B to 4 KB of scratch per lane).
+template <int W, int K, bool COUNT>
+__device__ __noinline__ void packet_redo(args_p A, uint2* ring, int lane) {
+    // (a call's arguments arrive in VGPRs: the argument block's address made
+    // uniform again)
+    A = (args_p)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)A);
+    A = launder(A);
+    const RtLaunchAux aux = kload(&A->aux);
+    RT_G uint32_t* const ctr = aux.tile_ctr;
+    const uint32_t cap = aux.redo_cap < 0xFFFFFFFFull ? (uint32_t)aux.redo_cap : 0xFFFFFFFFu;
+    LaneStack<K, 64> st;
+    st.attach_wave(reinterpret_cast<uint2(*)[64]>(ring), aux.spill,
+                   blockIdx.x * (64u * kPacketWaves) + threadIdx.x, gridDim.x * (64u * kPacketWaves), lane);
+    for (;;) {
+        uint32_t lo = 0, hi = 0;
+        if (lane == 0) {
+            const uint32_t n = __builtin_elementwise_min(atomicAdd(ctr + RT_REDO_COUNT, 0u), cap);
+            uint32_t c = atomicAdd(ctr + RT_REDO_CLAIM, 0u);
+            while (c < n) {
+                const uint32_t e = __builtin_elementwise_min(n, c + 64u);
+                const uint32_t prev = atomicCAS(ctr + RT_REDO_CLAIM, c, e);
+                if (prev == c) {
+                    lo = c;
+                    hi = e;
+                    break;
+                }
+                c = prev;
+            }
+        }
+        lo = uni(lo);
+        hi = uni(hi);
+        if (lo >= hi) break;
+        if ((uint32_t)lane < hi - lo) {
+            uint32_t v;
+            // (the append's count came first: its entry lands within a round trip)
+            while ((v = atomicExch(aux.redo + lo + (uint32_t)lane, kRedoEmpty)) == kRedoEmpty)
+                __builtin_amdgcn_s_sleep(2);
+            const RtDevScene sc = kload(&A->sc);
+            const RtFrameParams fp = kload(&A->fp);
+            const uint32_t npix = (uint32_t)fp.W * (uint32_t)fp.nrows;
+            const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: pose * npix + pixel
+            const int p = (int)(ob / npix);
+            const uint32_t o = ob - (uint32_t)p * npix;
+            trace_pixel<W, K, COUNT>(sc, fp, p, (int)(o % (uint32_t)fp.W), (int)(o / (uint32_t)fp.W), st,
+                                     (v & kRedoPass1) ? 1 : 0, true);
+        }
+    }
+}
+
+template <int W, int K, bool COUNT>
+__device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    A = launder(A);
+    RT_G uint32_t* const ctr = kload(&A->aux.tile_ctr);
+    // (a cheap check first: the call only when entries are waiting)
+    uint32_t pending = 0;
+    if (lane == 0) pending = atomicAdd(ctr + RT_REDO_COUNT, 0u) > atomicAdd(ctr + RT_REDO_CLAIM, 0u);
+    if (uni(pending)) packet_redo<W, K, COUNT>(A, ring, lane);
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(ctr + RT_EXIT_COUNT, 1u) + 1u;
+    if (uni(tk) != gridDim.x * (uint32_t)kPacketWaves) return;
+    // the last wave: per pose, the 64 spread partials (one per lane) summed
+    A = launder(A);
+    const int poses = kword(&A->fp.nframes) / kword(&A->fp.spp);
+    RT_G unsigned long long* const hc = kload(&A->fp.hit_count);
+    uint32_t part[RT_MAX_BATCH];
+#pragma unroll
+    for (int m = 0; m < RT_MAX_BATCH; m++)
+        part[m] = m < poses ? atomicExch(ctr + RT_HIT_BASE + (m * RT_HIT_SLOTS + lane) * RT_QUEUE_STRIDE, 0u) : 0u;
+#pragma unroll
+    for (int m = 0; m < RT_MAX_BATCH; m++) {
+        if (m >= poses) break;
+        const uint32_t s = wave_sum_u32(part[m]);
+        if (lane == 0 && hc && s) atomicAdd(hc + m, (unsigned long long)s);
+    }
+    if (lane < RT_QUEUES) {
+        (void)atomicExch(ctr + lane * RT_QUEUE_STRIDE, 0u);
+        (void)atomicExch(ctr + RT_COPY_BASE + lane * RT_QUEUE_STRIDE, 0u);
+    }
+    if (lane == 0) {
+        const uint32_t n = atomicExch(ctr + RT_REDO_COUNT, 0u);
+        uint32_t* const seen = kload(&A->aux.redo_seen);
+        if (seen) __hip_atomic_store(seen, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        (void)atomicExch(ctr + RT_POOL_COUNT, 0u);
+        (void)atomicExch(ctr + RT_REDO_CLAIM, 0u);
+        (void)atomicExch(ctr + RT_EXIT_COUNT, 0u);
+    }
 }
 
 // JOB: the launch carries a side de-interleave job (RtLaunchAux::job_*; its
@@ -1195,6 +1320,8 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     if (FUSED && hacc != 0 && lane == 0)
         atomicAdd(kload(&launder(A)->aux.tile_ctr) + RT_HIT_BASE + (hf * RT_HIT_SLOTS + hslot) * RT_QUEUE_STRIDE,
                   hacc);
+    if constexpr (FUSED)
+        if (kword(&launder(A)->aux.self_fix)) packet_exit<W, K, COUNT>(A, cands[wv], lane);
 }
 
 // v_mbcnt_lo_u32_b32: bits of m set below this lane (lanes 0-31; m = ~0: the
@@ -1486,8 +1613,7 @@ __device__ __forceinline__ uint32_t trace_packet_r(args_p A, int f, int i0, int 
                 drop[k], out, sh, rc);
             const uint32_t ob = ob0 + (uint32_t)k;
             if (redo) {
-                const uint32_t slot = atomicAdd(aux.tile_ctr + RT_REDO_COUNT, 1u);
-                if (slot < aux.redo_cap) aux.redo[slot] = ob | (redo == 2u ? kRedoPass1 : 0u);
+                redo_put(aux, ob | (redo == 2u ? kRedoPass1 : 0u));
             } else {
                 store_sample(fp, ob, out, sh);
                 double c[3];

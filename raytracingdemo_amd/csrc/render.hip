@@ -137,8 +137,8 @@ struct LaneCounts {
 // semantics (stack_bvh.hpp:611-644) over the walk tree: ray_of() returns the
 // fp64 ray (with reciprocals) — rebuilt on demand rather than held in
 // registers — and pad is a slab margin valid for it (frame_pad's bound).
-template <int W, int S, bool COUNT, class RayFn>
-__device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S>& st,
+template <int W, int S, bool COUNT, class RayFn, int C>
+__device__ __forceinline__ Win trace_core(const RtDevScene& sc, RayFn&& ray_of, float pad, LaneStack<S, C>& st,
                                           int pass0, LaneCounts& lc) {
     constexpr int G = W < 4 ? W : 4;  // children tested per load group
     Ray32 q;
@@ -566,9 +566,9 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
 }
 
 // Exact per-lane traversal of the primary ray of pixel (i, r) of frame f.
-template <int W, int S, bool COUNT>
+template <int W, int S, bool COUNT, int C>
 __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
-                                            LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
+                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
     const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
     const RtFrameCam cam = frame_cam(fp, f);
     auto ray_of = [&]() { return gen_ray(fp, cam, opaque(i), j); };
@@ -629,9 +629,9 @@ __device__ __forceinline__ void wave_add_keyed(RT_G unsigned long long* base, in
 // All spp samples of pixel (i, r) of pose p with the per-lane exact kernel:
 // per-sample outputs, the averaged colour and the pose's hit count (the
 // lanes of a wave may hold pixels of different poses).
-template <int W, int S, bool COUNT>
+template <int W, int S, bool COUNT, int C>
 __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameParams& fp, int p, int i, int r,
-                                            LaneStack<S>& st, int pass0 = 0, bool fixup = false) {
+                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
     const size_t po = out_index(fp, p, (size_t)r * fp.W + i);
     double acc[3] = {0.0, 0.0, 0.0};
     uint32_t hits = 0;
@@ -653,7 +653,6 @@ __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameP
 
 #include "packet_kernel.h"
 #include "path_kernel.h"
-#include "wavefront_paths.h"
 #include "queue_paths.h"
 
 // Finishes the pixels the packet pipeline handed over (redo list, count in
@@ -715,7 +714,9 @@ __global__ void __launch_bounds__(256) k_fixup(RtDevScene sc, RtFrameParams fp, 
     st.attach(lds, aux, tid);
     // (grid-stride over the redo list; every thread reaches the exit test)
     for (uint32_t e = blockIdx.x * 256u + (uint32_t)tid; e < n; e += gridDim.x * 256u) {
-        const uint32_t v = retry ? e : aux.redo[e];
+        // (each entry taken is left kRedoEmpty for the next launch)
+        if (retry && e < n_sh && e < aux.redo_cap) aux.redo[e] = kRedoEmpty;
+        const uint32_t v = retry ? e : atomicExch(aux.redo + e, kRedoEmpty);
         const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: pose * npix + pixel
         const int p = (int)(ob / npix);
         const uint32_t o = ob - (uint32_t)p * npix;
@@ -843,7 +844,6 @@ constexpr int kLdsStack = 16;      // per-lane kernel: LDS ring entries per lane
 constexpr int kPathStack = RT_PATHS_STACK;  // path kernel: LDS ring entries per lane
 constexpr int kPacketStack = 128;  // packet kernel: wave-uniform stack entries (4 B each)
 constexpr int kCandidates = RT_CAND_LDS;  // packet kernel: LDS candidate list entries per lane (8 B each)
-static_assert(RT_PW_K <= RT_CAND_LDS, "wavefront walk lists share the candidate buffers");
 // k_fixup blocks: the redo list is short (~0 entries on the sponza proxy), and
 // 32 blocks (32 KB of LDS each) start on the first CUs the launch frees, while
 // the next launch on the other stream fills the rest (256 blocks: -1.2% at
@@ -915,9 +915,18 @@ bool split_resolve(int spp) {
 bool needs_cand(int spp, bool pack) { return (spp > 1 && !pack) || split_resolve(spp); }
 
 template <int W>
-hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, bool count,
+hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux_in, bool count,
                         hipStream_t s, const hipEvent_t* ev) {
-    const dim3 grid((unsigned)aux.grid), blk(256), pgrid((unsigned)aux.pgrid), pblk(64 * kPacketWaves);
+    const dim3 grid((unsigned)aux_in.grid), blk(256), pgrid((unsigned)aux_in.pgrid), pblk(64 * kPacketWaves);
+    // aux.self_fix (the host's offer: the redo list holds every pixel of the
+    // launch and the spill the packet grid's lanes) is taken by the fused
+    // packet kernel when it resolves every sample itself — spp = 1 or packed
+    // samples, one ray per lane: its own waves then finish the redo list and
+    // the bookkeeping (packet_exit) and no k_fixup follows, so the launch
+    // ends with its traversal kernel
+    RtLaunchAux aux = aux_in;
+    const bool packet_r = W == 8 && fp.spp == 1 && !fp.pack && !aux_in.job_src && packet_rays() == 2;
+    aux.self_fix = aux_in.self_fix && !split_resolve(fp.spp) && (fp.spp == 1 || fp.pack) && !packet_r ? 1 : 0;
     // RT_FLAG_TIMING: two markers bracket the traversal kernel only (the
     // rest of the pipeline is timed as frame minus traversal by the caller)
     if (ev) (void)hipEventRecord(ev[0], s);
@@ -990,8 +999,11 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
             if (count) hipLaunchKernelGGL((k_resolve<true>), rgrid, blk, 0, s, sc, fp, aux);
             else hipLaunchKernelGGL((k_resolve<false>), rgrid, blk, 0, s, sc, fp, aux);
         }
-        if (count) hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, blk, 0, s, sc, fp, aux);
-        else hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, blk, 0, s, sc, fp, aux);
+        if (aux.self_fix) {
+        } else if (count)
+            hipLaunchKernelGGL((k_fixup<W, kLdsStack, true>), fgrid, blk, 0, s, sc, fp, aux);
+        else
+            hipLaunchKernelGGL((k_fixup<W, kLdsStack, false>), fgrid, blk, 0, s, sc, fp, aux);
     } else {
         // per-lane kernel (trees deeper than the packet stack): one launch
         // per frame of the batch, each on a zeroed work queue
@@ -1067,10 +1079,9 @@ int packet_blocks_per_cu(int width) {
 // the smallest LDS ring of the per-lane kernels (spill sizing)
 int exact_lds_stack() {
     int a = kLdsStack < kPathStack ? kLdsStack : kPathStack;
-    a = a < RT_PW_STACK ? a : RT_PW_STACK;
     return a < RT_Q_STACK ? a : RT_Q_STACK;
 }
-int packet_candidates() { return RT_CAND_LDS; }  // HBM list entries per pixel (spp > 1, wavefront paths)
+int packet_candidates() { return RT_CAND_LDS; }  // candidate entries per pixel (spp > 1 lists; packet_exit's ring)
 bool packet_split(int spp, bool pack) { return needs_cand(spp, pack); }
 uint32_t params_bytes() { return (uint32_t)sizeof(RtFrameParams); }
 
@@ -1274,47 +1285,6 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     return hipGetLastError();
 }
 
-// Wavefront path tracing of one pose (wavefront_paths.h): per sample, walk +
-// shade for each of the 1 + bounces segments, then the accumulation.  ws.ctl
-// must be zero on entry (the kernels leave it zero).
-hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
-                           uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev) {
-    if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
-    if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.spill || aux.grid <= 0 || !aux.cand ||
-        aux.cand_cap < ws.P || ws.P != (uint32_t)fp.W * (uint32_t)fp.nrows || RT_PW_K > RT_CAND_LDS ||
-        aux.spill_cap + RT_PW_STACK < sc.stack_bound || aux.spill_cap + kLdsStack < sc.stack_bound)
-        return hipErrorInvalidValue;
-    const dim3 grid((unsigned)aux.grid), blk(256), agrid((ws.P + 255u) / 256u);
-    if (ev) (void)hipEventRecord(ev[0], s);
-    for (uint32_t smp = 0; smp < (uint32_t)fp.spp; smp++) {
-        for (int b = 0; b <= bounces; b++) {
-            switch (sc.width) {
-                case 2:
-                    hipLaunchKernelGGL((k_pw_walk<2, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
-                    hipLaunchKernelGGL((k_pw_shade<2, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
-                    break;
-                case 4:
-                    hipLaunchKernelGGL((k_pw_walk<4, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
-                    hipLaunchKernelGGL((k_pw_shade<4, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
-                    break;
-                case 8:
-                    hipLaunchKernelGGL((k_pw_walk<8, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
-                    hipLaunchKernelGGL((k_pw_shade<8, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
-                    break;
-                case 16:
-                    hipLaunchKernelGGL((k_pw_walk<16, RT_PW_STACK, RT_PW_K>), grid, blk, 0, s, sc, fp, aux, ws, b, smp, frame);
-                    hipLaunchKernelGGL((k_pw_shade<16, kLdsStack>), grid, blk, 0, s, sc, fp, aux, ws, b, bounces, smp, frame);
-                    break;
-                default:
-                    return hipErrorInvalidValue;
-            }
-        }
-        hipLaunchKernelGGL(k_pw_accum, agrid, blk, 0, s, fp, ws, smp);
-    }
-    if (ev) (void)hipEventRecord(ev[1], s);
-    return hipGetLastError();
-}
-
 // Queued path tracing of one pose (queue_paths.h): the primary segments of
 // every path, then per bounce segment the compacted queue and its fall-back
 // list, then the pixel sums.  The control words are zeroed here.
@@ -1382,9 +1352,13 @@ void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLa
 // order by k_sh_lane; "bin": queued, sorted by direction from the light and
 // walked by the wave (k_sh_walk; its wave stack holds kPacketStack entries,
 // deeper trees stay per lane).  Config c5: 241 / 242 / 266 ms per pose.
-int queued_shadow_mode(const RtDevScene& sc, bool shadow) {
+// A queued record names its destination in one word (q_light: bit 31, the
+// queue in bit 30, the slot in bits 0-29), so pools of 2^30 paths or more
+// stay per lane too.
+int queued_shadow_mode(const RtDevScene& sc, bool shadow, uint64_t paths) {
     if (!shadow) return 0;
     const char* e = getenv("RT_SHADOW_RAYS");
+    if (paths >= (1ull << 30)) return 1;
     if (e && e[0] == 'r') return 3;
     if (e && e[0] == 'b') return sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
     return 1;
@@ -1401,7 +1375,7 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     hipError_t e = hipMemsetAsync(qs.ctl, 0, RT_QC_WORDS(bounces) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const bool count = fp.counters != nullptr;
-    const int sh = queued_shadow_mode(sc, shadow);
+    const int sh = queued_shadow_mode(sc, shadow, paths);
     if (sh == 2 && (!qs.srec[0] || !qs.srec[1] || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
     // the wave-walked primary kernel uses no per-lane stack (no spill

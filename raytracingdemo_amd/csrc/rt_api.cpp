@@ -29,8 +29,6 @@ int exact_blocks_per_cu(int width, uint32_t stack_bound);
 int packet_blocks_per_cu(int width);
 hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, uint32_t frame,
                         int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev);
-hipError_t launch_paths_wf(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathWs& ws,
-                           uint32_t frame, int bounces, hipStream_t s, const hipEvent_t* ev);
 hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                           uint32_t frame, int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
@@ -153,13 +151,15 @@ struct Replica {
     Slot slot[kSlots];
     int next_slot = 0;
     uint32_t spill_cap = 0;
+    // stack spill words per slot: the per-lane kernels' (grid * 256 lanes x
+    // spill_cap) or the packet kernel's exit path (pgrid * 256 lanes x the
+    // stack bound past its LDS ring), whichever is larger
+    size_t spill_words = 0;
     int grid = 0;                // per-lane kernels: 256-thread workgroups
     int pgrid = 0;               // packet kernel: 64 * kPacketWaves-thread workgroups
     uint32_t pool_chunks = 0;
     void* d_cand = nullptr;      // spp > 1 / wavefront paths: candidate lists in HBM
     uint64_t cand_cap = 0;       // pixels
-    void* d_pw = nullptr;        // wavefront path tracer workspace (PathWs), pw_cap paths
-    uint64_t pw_cap = 0;
     void* d_pq = nullptr;        // queued path tracer workspace (PathQs), pq_cap paths
     uint64_t pq_cap = 0;
     // RT_FLAG_TIMING: events around the traversal kernel per timed launch,
@@ -200,9 +200,14 @@ struct rt_scene {
 
 namespace {
 
-// RCCL, opened on the first multi-device upload (dlopen, so single-device
-// users never initialise it): the process's copy when one is mapped already
-// (PyTorch's librccl.so.1, preloaded by the Python binding), else ROCm's.
+// RCCL, opened on the first multi-device render (dlopen, so single-device
+// users never initialise it).  One copy per process: the one already mapped
+// (PyTorch's: torch/lib/librccl.so, soname librccl.so.1 — the Python binding
+// imports torch before a multi-device upload when torch is installed), else
+// ROCm's, opened RTLD_LOCAL.  Never RTLD_GLOBAL: an RCCL mapped globally ahead
+// of torch interposes its symbols on torch's libraries, and objects shared
+// that way were destroyed twice at exit ("double free or corruption", round
+// 4; tests/test_host.py pins both import orders).
 struct Rccl {
     decltype(&ncclCommInitAll) init_all = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
@@ -214,8 +219,9 @@ struct Rccl {
 const Rccl& rccl() {
     static const Rccl r = [] {
         Rccl x;
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
         if (!h) throw rt::Error{RT_ERR_RUNTIME, std::string("RCCL not found: ") + dlerror()};
         x.init_all = (decltype(x.init_all))dlsym(h, "ncclCommInitAll");
         x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
@@ -279,7 +285,6 @@ void free_replica(Replica& r) {
         if (q.ev) hipEventDestroy(q.ev);
     }
     if (r.d_cand) hipFree(r.d_cand);
-    if (r.d_pw) hipFree(r.d_pw);
     if (r.d_pq) hipFree(r.d_pq);
     for (auto& a : r.tev)
         for (hipEvent_t e : a) hipEventDestroy(e);
@@ -303,7 +308,7 @@ void alloc_slot(Replica& r, Slot& q) {
     if (q.d_tiles) return;
     HIP_TRY(hipMalloc(&q.d_tiles, RT_QUEUE_WORDS * sizeof(uint32_t)));
     HIP_TRY(hipMemset(q.d_tiles, 0, RT_QUEUE_WORDS * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&q.d_spill, (size_t)r.grid * 256 * r.spill_cap * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&q.d_spill, r.spill_words * sizeof(uint64_t)));
     HIP_TRY(hipMalloc(&q.d_pool, (size_t)r.pool_chunks * RT_POOL_CHUNK * sizeof(uint64_t)));
     HIP_TRY(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
     q.h_seen = seen_word_alloc();
@@ -390,6 +395,9 @@ void upload_one(rt_scene* s, int device) {
     r.pgrid = prop.multiProcessorCount * rt::packet_blocks_per_cu(f.width);
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
+    const uint32_t K = (uint32_t)rt::packet_candidates();  // packet_exit's LDS ring (render.hip)
+    r.spill_words = std::max((size_t)r.grid * 256 * r.spill_cap,
+                             (size_t)r.pgrid * 256 * (f.stack_bound > K ? f.stack_bound - K : 1u));
     r.pool_chunks = kPoolChunks;
     if (const char* e = std::getenv("RT_POOL_CHUNKS")) {  // test hook: a small pool runs dry
         const long v = std::atol(e);
@@ -411,32 +419,45 @@ void quiesce(Replica& r) {
     for (Slot& q : r.slot) quiesce_slot(q);
 }
 
-// Redo list: a fixed pool of entries, not one per pose pixel (on the sponza
-// proxy ~0 pixels are redone; a launch whose redo count passes the pool is
-// retried whole by k_fixup).  k_fixup reports each launch's count to a
-// host-mapped word of the slot; a slot that overflowed gets a longer list
+// Redo list: one entry per pose pixel of a launch (4 B each: 298 MB for
+// the 36-pose 1080p orbit), so no launch can overflow it and the fused packet
+// kernel finishes the list itself (aux.self_fix, packet_exit) instead of a
+// trailing k_fixup that would start only after the next launch's
+// persistent grid.  On the sponza proxy ~0 pixels are redone.
+// If that allocation fails the list is a fixed pool of kRedoEntries and
+// k_fixup runs after every launch: a launch whose redo count passes the pool
+// is retried whole there; k_fixup reports each launch's count to a
+// host-mapped word of the slot, and a slot that overflowed gets a longer list
 // (twice the count, up to kRedoGrow entries) and, while its launches still
 // overflow, the full fix-up grid for the retry.  RT_REDO_CAP (read per call;
-// a test hook) lowers the entries a launch may use.
+// a test hook) lowers the entries a launch may use, which forces the k_fixup
+// path.  Entries are kRedoEmpty between launches (packet_kernel.h).
 constexpr uint64_t kRedoEntries = 1u << 20;  // 4 MiB
 constexpr uint64_t kRedoGrow = 1u << 26;     // 256 MiB
 uint64_t redo_limit() {
     const char* e = std::getenv("RT_REDO_CAP");
     const long long v = e ? std::atoll(e) : 0;
-    return v > 0 ? std::min<uint64_t>((uint64_t)v, kRedoEntries) : kRedoEntries;
+    return v > 0 ? (uint64_t)v : UINT64_MAX;
 }
 
 // Redo list of a slot for a launch of `pixels` pose pixels (grown, never
-// shrunk; at most kRedoEntries).
+// shrunk): every pixel, or past a failed allocation at most `most`.
 void ensure_redo(Slot& q, uint64_t pixels, uint64_t most = kRedoEntries) {
-    pixels = std::min<uint64_t>(std::max<uint64_t>(pixels, 1), most);
+    pixels = std::max<uint64_t>(pixels, 1);
     if (q.redo_cap >= pixels) return;
     quiesce_slot(q);
+    const uint64_t had = q.redo_cap;
     if (q.d_redo) HIP_TRY(hipFree(q.d_redo));
     q.d_redo = nullptr;
     q.redo_cap = 0;
-    HIP_TRY(hipMalloc(&q.d_redo, pixels * sizeof(uint32_t)));
-    q.redo_cap = pixels;
+    uint64_t n = pixels;
+    if (hipMalloc(&q.d_redo, n * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        n = std::min<uint64_t>(pixels, std::max<uint64_t>(most, had));
+        HIP_TRY(hipMalloc(&q.d_redo, n * sizeof(uint32_t)));
+    }
+    HIP_TRY(hipMemset(q.d_redo, 0xFF, n * sizeof(uint32_t)));  // kRedoEmpty
+    q.redo_cap = n;
 }
 
 // Candidate lists in HBM for `pixels` sample pixels (spp > 1 resolve, the
@@ -451,28 +472,6 @@ void ensure_cand(Replica& r, uint64_t pixels) {
     r.cand_cap = 0;
     HIP_TRY(hipMalloc(&r.d_cand, pixels * kCandBytesPerPixel));
     r.cand_cap = pixels;
-}
-
-// Wavefront path-tracer workspace for P paths (grown, never shrunk): two
-// segment queues (64 B per entry), L and acc (24 B per path), control words.
-PathWs ensure_pw(Replica& r, uint64_t P) {
-    if (r.pw_cap < P) {
-        quiesce(r);  // earlier launches may still use it
-        if (r.d_pw) HIP_TRY(hipFree(r.d_pw));
-        r.d_pw = nullptr;
-        r.pw_cap = 0;
-        HIP_TRY(hipMalloc(&r.d_pw, P * (2 * 64 + 2 * 24) + 256));
-        r.pw_cap = P;
-    }
-    uint8_t* base = static_cast<uint8_t*>(r.d_pw);
-    PathWs ws{};
-    ws.qray[0] = reinterpret_cast<double*>(base);
-    ws.qray[1] = reinterpret_cast<double*>(base + r.pw_cap * 64);
-    ws.L = reinterpret_cast<double*>(base + r.pw_cap * 128);
-    ws.acc = reinterpret_cast<double*>(base + r.pw_cap * 152);
-    ws.ctl = reinterpret_cast<uint32_t*>(base + r.pw_cap * 176);
-    ws.P = (uint32_t)P;
-    return ws;
 }
 
 // Queued path-tracer workspace for P paths (grown, never shrunk): two
@@ -510,15 +509,17 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
 
 // Path pipeline (RT_PATHS, read per call: tests switch it in-process):
 // "queue" — the queued tracer (queue_paths.h: compacted segment queues, lean
-// per-segment kernels); "mega" — the megakernel (path_kernel.h k_paths);
-// RT_PATHS_WF=1 — the round-2 wavefront tracer (wavefront_paths.h).
+// per-segment kernels); "mega" — the megakernel (path_kernel.h k_paths).
 // Unset: the faster of the two on config c5 — the queued tracer with
 // occlusion rays (234 vs 250 ms per pose), the megakernel without (156 vs
-// 161).
-enum class PathPipe { mega, queue, wf };
+// 161).  (The round-2 wavefront tracer, 1.45x slower than
+// either, was removed in round 5.)
+enum class PathPipe { mega, queue };
+bool path_pipe_forced() {
+    const char* e = std::getenv("RT_PATHS");
+    return e && (e[0] == 'q' || e[0] == 'm');
+}
 PathPipe path_pipe(bool shadow) {
-    const char* w = std::getenv("RT_PATHS_WF");
-    if (w && std::atoi(w) != 0) return PathPipe::wf;
     const char* e = std::getenv("RT_PATHS");
     if (e && e[0] == 'q') return PathPipe::queue;
     if (e && e[0] == 'm') return PathPipe::mega;
@@ -707,6 +708,8 @@ void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int
     RtLaunchAux a = aux_of(r, q);
     a.redo_seen = q.h_seen;
     if (seen > a.redo_cap) a.fgrid = r.grid;
+    // the packet kernel may end the launch itself: no retry is possible
+    a.self_fix = a.redo_cap >= lpix ? 1 : 0;
     set_job(a, job);
     if (a.job_src) {
         const bool empty = fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0;
@@ -940,6 +943,22 @@ extern "C" {
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 const char* rt_last_error(void) { return g_err.c_str(); }
 void rt_free(void* p) { std::free(p); }
+
+const char* rt_rccl_path(void) {
+    static std::string path;
+    try {
+        Dl_info info{};
+        if (!dladdr(reinterpret_cast<void*>(rccl().gather), &info) || !info.dli_fname) {
+            fail(RT_ERR_RUNTIME, "RCCL mapped but its file is unknown");
+            return nullptr;
+        }
+        path = info.dli_fname;
+        return path.c_str();
+    } catch (const rt::Error& e) {
+        fail(e.status, e.msg);
+        return nullptr;
+    }
+}
 
 const char* rt_device_name(int device) {
     static thread_local std::string name;
@@ -1304,22 +1323,25 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             tev = r->tev[r->tev_used++].data();
         }
         hipError_t e;
-        const PathPipe pipe = path_pipe((flags & RT_FLAG_SHADOW) != 0);
+        PathPipe pipe = path_pipe((flags & RT_FLAG_SHADOW) != 0);
+        PathQs qs{};
         if (pipe == PathPipe::queue) {
+            // the queued workspace (256 B per path: 34 GB for a c5 pose);
+            // when the library chose the queue itself and the workspace
+            // cannot be had, the megakernel renders the same bits with none
             const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows * (uint64_t)spp;
-            const PathQs qs = ensure_pq(*r, P);
+            try {
+                qs = ensure_pq(*r, P);
+            } catch (const rt::Error&) {
+                if (path_pipe_forced()) throw;
+                (void)hipGetLastError();
+                pipe = PathPipe::mega;
+            }
+        }
+        if (pipe == PathPipe::queue) {
             Slot& q = take_slot(*r, st, true);  // (the replica-wide workspace: after every slot's launches)
             e = rt::launch_paths_q(r->dev, fp, aux_of(*r, q), qs, (uint32_t)frame, bounces,
                                    (flags & RT_FLAG_SHADOW) != 0, st, tev);
-        } else if (pipe == PathPipe::wf) {
-            if (flags & RT_FLAG_SHADOW) return fail(RT_ERR_INVALID_ARGUMENT, "RT_PATHS_WF=1 has no occlusion rays");
-            const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows;
-            ensure_cand(*r, P);  // candidate lists, stride P
-            const PathWs ws = ensure_pw(*r, P);
-            Slot& q = take_slot(*r, st, true);
-            HIP_TRY(hipMemsetAsync(ws.ctl, 0, 16 * sizeof(uint32_t), st));
-            e = rt::launch_paths_wf(r->dev, fp, aux_of(*r, q), ws, (uint32_t)frame, bounces, st, tev);
-            q.fresh = false;  // the work queue is left dirty: the next packet launch clears it
         } else {
             Slot& q = take_slot(*r, st, (flags & RT_FLAG_COUNT) != 0);
             e = rt::launch_paths(r->dev, fp, aux_of(*r, q), (uint32_t)frame, bounces, (flags & RT_FLAG_SHADOW) != 0,

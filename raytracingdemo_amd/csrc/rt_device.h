@@ -47,6 +47,10 @@
 #define RT_POOL_COUNT (RT_REDO_COUNT + RT_QUEUE_STRIDE)
 // k_fixup blocks that have read the redo count (the last one clears it)
 #define RT_FIXUP_DONE (RT_REDO_COUNT + 2 * RT_QUEUE_STRIDE)
+// redo-list entries taken so far by the packet kernel's own waves, and its
+// exit tickets (RtLaunchAux::self_fix: the launch ends without k_fixup)
+#define RT_REDO_CLAIM (RT_REDO_COUNT + 3 * RT_QUEUE_STRIDE)
+#define RT_EXIT_COUNT (RT_REDO_COUNT + 4 * RT_QUEUE_STRIDE)
 // rows of the side de-interleave job (RtLaunchAux::job_*) claimed so far,
 // one counter per XCD queue (queue x takes rows x, x + RT_QUEUES, ...: a
 // counter shared by all XCDs would serialise on cross-XCD atomics)
@@ -171,11 +175,14 @@ struct RtLaunchAux {
     RT_G uint64_t* spill;      // traversal-stack spill: spill_cap entries per lane
     uint32_t spill_cap;
     int32_t grid;         // persistent blocks (CUs x resident blocks per CU)
-    RT_G uint32_t* redo;       // packet kernel -> k_fixup: pixel index | start-pass bit
+    RT_G uint32_t* redo;       // packet kernel -> k_fixup: pixel index | start-pass bit (kRedoEmpty: none)
     uint64_t redo_cap;    // entries (a fixed pool: past it k_fixup retries the whole launch)
     uint32_t* redo_seen;  // host-mapped word: k_fixup reports the launch's redo count there (or null);
                           // the host grows the slot's list for its next launches from it
     int32_t fgrid;        // k_fixup blocks (0: the default kFixupGrid)
+    int32_t self_fix;     // 1: the fused packet kernel's own waves finish the redo list and the
+                          // bookkeeping (packet_exit), no k_fixup (redo_cap >= the launch's pixels;
+                          // spill sized for the packet grid)
     RT_G uint64_t* pool;       // candidate overflow pool: pool_chunks x RT_POOL_CHUNK entries
     uint32_t pool_chunks;
     int32_t pgrid;             // workgroups of the packet kernel (64 * kPacketWaves threads each)
@@ -271,11 +278,3 @@ struct PathQs {
 #define RT_SH_BINS (1 << RT_SH_BITS)
 #define RT_SH_BLOCKS 256
 
-// Workspace of the wavefront path tracer (wavefront_paths.h), per replica.
-struct PathWs {
-    RT_G double* qray[2];  // segment queues: 8 doubles per entry {o, d, path id (low word of [6]), -}
-    RT_G double* L;        // 3 per path: the current sample's radiance
-    RT_G double* acc;      // 3 per pixel: sum of the samples' radiance
-    RT_G uint32_t* ctl;    // [0], [1]: entries in qray[0], qray[1]; [2]: walk cursor (zero between launches)
-    uint32_t P;            // paths per sample = pixels of the shard
-};

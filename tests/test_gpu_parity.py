@@ -605,28 +605,6 @@ def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, 
     assert q["rgb"].max() > 0
 
 
-@pytest.mark.parametrize("model,spp,bounces", [("stanford-bunny.obj", 3, 4), ("teapot.obj", 2, 1)])
-def test_paths_wavefront_matches_megakernel_and_oracle(oracle, model, spp, bounces, monkeypatch):
-    """The wavefront pipeline (RT_PATHS_WF=1: walk / shade / accumulate
-    kernels with compacted segment queues) renders the same bits as the
-    megakernel and the oracle, including a strided row shard."""
-    tris = golden_scene(model)
-    s = scene(model, "bsah", 8)
-    pos, d = rt.CameraPath(rt.scene_center(tris), 36).circular_path(7)
-    W, H = 64, 36
-    mega = _paths_render(s, pos, d, W, H, 7, spp, bounces)
-    mega_sh = _paths_render(s, pos, d, W, H, 7, spp, bounces, row0=2, stride=3)
-    monkeypatch.setenv("RT_PATHS_WF", "1")
-    wf = _paths_render(s, pos, d, W, H, 7, spp, bounces)
-    wf_sh = _paths_render(s, pos, d, W, H, 7, spp, bounces, row0=2, stride=3)
-    for k in ("id", "dist", "rgb"):
-        assert np.array_equal(wf[k], mega[k]), k
-        assert np.array_equal(wf_sh[k], mega_sh[k]), k
-    assert wf["hits"] == mega["hits"] and wf_sh["hits"] == mega_sh["hits"]
-    o = oracle.bvh(tris, "bsah", 8).render_paths(pos, d, W, H, 7, spp, bounces)
-    assert np.array_equal(wf["rgb"], o["rgb"])
-
-
 def test_errors_fail_loudly():
     with pytest.raises(rt.RTError, match="Unknown algorithm"):
         rt.Scene(golden_scene("teapot.obj"), "quick", 2)

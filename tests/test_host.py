@@ -237,3 +237,51 @@ def test_pmc_traffic_sums_the_queued_pipeline_per_pose(tmp_path):
     assert poses[0]["FETCH_SIZE"] == 40 + 50 + 60 + 70
     assert poses[1]["FETCH_SIZE"] == 90 + 100 + 110
     assert pmc_traffic.queue_counting("k_sh_lane<8, 8, true>(") and not pmc_traffic.queue_counting("k_sh_lane<8, 8, false>(")
+
+
+# One process, one RCCL, and a clean exit in either import order.  Round 4
+# found "double free or corruption (!prev)" at exit after torch's librccl.so
+# had been mapped RTLD_GLOBAL ahead of `import torch` (fixed in _native.py);
+# the library now reuses the RCCL the process holds and opens ROCm's
+# RTLD_LOCAL only when none is mapped (rt_api.cpp rccl()).
+_CHILD = r"""
+import sys
+sys.path.insert(0, {root!r})
+order = {order!r}
+if order == "torch_first":
+    import torch
+    import raytracingdemo_amd as rt
+    rt._native.lib()
+else:
+    import raytracingdemo_amd as rt
+    rt._native.lib()
+    import torch
+    # the multi-device upload path's own step: torch's RCCL first
+    rt._native.prefer_torch_rccl()
+L = rt._native.lib()
+p = L.rt_rccl_path()
+assert p, L.rt_last_error()
+maps = {{ln.split()[-1] for ln in open("/proc/self/maps") if "librccl" in ln}}
+print("RCCL", p.decode(), "MAPPED", sorted(maps))
+"""
+
+
+@pytest.mark.parametrize("order", ["torch_first", "library_first"])
+def test_import_orders_exit_cleanly_with_one_rccl(order):
+    import os
+    import subprocess
+    import sys
+
+    import torch
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _CHILD.format(root=root, order=order)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "double free" not in r.stderr and "corruption" not in r.stderr, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RCCL ")][-1]
+    path, mapped = line[5:].split(" MAPPED ")
+    mapped = eval(mapped)  # a list literal printed by the child
+    assert len(mapped) == 1, mapped           # never two copies
+    torch_rccl = os.path.realpath(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+    assert os.path.realpath(path) == torch_rccl  # the process's (PyTorch's) copy

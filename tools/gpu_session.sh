@@ -33,6 +33,9 @@ for s in $STEPS; do
         shards) for n in 2 4 8; do run bench_shard$n 300 python bench.py --no-cpu --no-dropin --steps 10 --shard-of $n || exit 1; done ;;
         rccl)  run rccl 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rccl -o rccl \
                    -- python tools/rccl_group_probe.py ;;
+        fixup) run fixup 900 python -u -m pytest tests/test_gpu_headline.py tests/test_gpu_parity.py -x -v --timeout 300 \
+                   --timeout-method thread -p no:cacheprovider \
+                   -k "headline or consecutive or side_deinterleave or c4 or overflow or redo or packed or rccl or sharded or concurrent or edge or ties or stratified" ;;
         c5)    run c5 900 python -u -m pytest tests/test_gpu_headline.py -x -v --timeout 600 --timeout-method thread \
                    -p no:cacheprovider -k "c5 or c3_shape" ;;
         rcclt) run rcclt 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \

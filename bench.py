@@ -33,6 +33,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec (primary, 1spp) on Sponza 1920×1080; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# what `traffic` counts (tools/pmc_traffic.py): the L2's memory-side requests
+# (FETCH_SIZE with the gfx950 unit correction per access type, + WRITE_SIZE);
+# Infinity-Cache (MALL) hits are included, so it is L2-miss / fabric traffic,
+# an upper bound of the HBM bytes
+TRAFFIC_COUNTS = ("L2-miss (fabric) bytes: FETCH_SIZE (x2 for vector reads, calibrated) + WRITE_SIZE; "
+                  "Infinity-Cache hits included, so an upper bound of HBM bytes")
 TRI32_BYTES = 48       # fp32 pre-filter record (v0, e1, e2 + 3 bounds)
 TRI64_BYTES = 128      # fp64 record (v0, e1, e2, normal, id, leaf, leaf box) per exact test
 MT64_BYTES = 72        # its Moller-Trumbore part (v0, e1, e2) per exact test (fused resolve)
@@ -434,8 +440,12 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "frac_per_lane": round(achieved_pl / HBM_PEAK_GBS, 4),
-                         "frac_dram": (round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
-                                       if traffic and kernel_s > 0 else None),
+                         # measured bytes past L2 (FETCH_SIZE x 2 + WRITE_SIZE): fabric
+                         # requests, Infinity-Cache hits included (MI355X guide, HBM
+                         # section) — an upper bound of HBM traffic, not HBM itself
+                         "frac_l2_miss": (round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
+                                          if traffic and kernel_s > 0 else None),
+                         "traffic_counts": TRAFFIC_COUNTS,
                          "kernel": ("queued pipeline (k_q_primary, k_q_segment, k_q_fallback, k_sh_*, k_q_accum; "
                                     "HIP events around the pose)" if queued else "k_paths"),
                          "alg_bytes_per_launch": round(alg_pose), "alg_bytes_parts": alg_parts,
@@ -918,7 +928,8 @@ def main():
                              "frac_walk": round(rates["walk_only"] / HBM_PEAK_GBS, 4),
                              "frac_walk_and_outputs": round(rates["walk_and_outputs"] / HBM_PEAK_GBS, 4),
                              "frac_per_lane_resolve": round(rates["per_lane_resolve"] / HBM_PEAK_GBS, 4),
-                             **({"frac_dram": round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4)}
+                             **({"frac_l2_miss": round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+                                 "traffic_counts": TRAFFIC_COUNTS}
                                 if traffic else {})} if rates else {}),
                          "valu": valu,
                          "kernel": ("k_trace_packet (walk + fused exact resolve)" if fused else

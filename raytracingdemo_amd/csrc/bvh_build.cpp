@@ -896,13 +896,16 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
         f.root_ref = F.ref_of(0, 0);
         if (f.n_wide == 0) F.alloc_node();  // root is a leaf: keep a valid node array
     }
-    // Each child record's pad word carries the CHILD node's ordering meta
-    // (sort axis | valid slots << 2; slot 0's pad held the node's own meta
-    // until here), so the packet kernel knows a node's valid slots before it
-    // loads the node and loads and tests only those (packet_kernel.h); leaf
-    // and empty slots get 0.  The root's meta is root_meta.  The packet
-    // kernel carries a node's meta in bits 24-30 of its ref: node ids stay
-    // below 2^24.
+    // Each child record's pad word carries the child's ref with the CHILD
+    // node's ordering meta (sort axis | valid slots << 2; slot 0's pad held
+    // the node's own meta until here) in bits 24-30 — node ids stay below
+    // 2^24 — so the wave walks (packet_kernel.h, path_kernel.h wave_walk,
+    // queue_paths.h k_sh_walk) take a node's next ref from one word, with
+    // its valid slots known before the node is loaded, and no scalar
+    // instructions combine ref and meta in every node step (16 SALU per step
+    // of 8 children in round 4).  Leaf slots hold the leaf ref there, empty
+    // slots RT_INVALID_REF; the ref word stays the plain ref for the per-lane
+    // walks.  The root's meta is root_meta.
     if (f.n_wide >= (1u << 24)) throw Error{RT_ERR_INVALID_ARGUMENT, "scene too large (wide nodes)"};
     {
         const uint64_t nb = rt_node_bytes(W);
@@ -912,7 +915,7 @@ Flat flatten(const Soup& s, const Tree& t, int width_hint, const WalkTree* walk)
             uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + x * nb);
             for (int c = 0; c < W; c++) {
                 const uint32_t r = p[8 * c + RT_CHILD_REF];
-                p[8 * c + 7] = (r != RT_INVALID_REF && !(r & RT_LEAF_BIT)) ? meta[r] : 0u;
+                p[8 * c + 7] = (r != RT_INVALID_REF && !(r & RT_LEAF_BIT)) ? (r | meta[r] << 24) : r;
             }
         }
         f.root_meta = (f.root_ref != RT_INVALID_REF && !(f.root_ref & RT_LEAF_BIT)) ? meta[f.root_ref] : 0u;

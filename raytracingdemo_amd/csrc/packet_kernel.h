@@ -576,7 +576,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                     // the ref words come with the boxes (same scalar loads);
                     // an inner child's ref gets its node's meta (leaf pads are 0)
 #pragma unroll
-                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref | (ch[c].pad << 24);
+                    for (int c = 0; c < W; c++) rs[c] = ch[c].pad;  // ref | meta << 24 (bvh_build.cpp flatten)
                     mask = node_mask<W, OCT>(bx, q, nox, noy, noz, tcull, nv);
                 }
                 if (COUNT) w_empty += mask == 0;
@@ -1433,7 +1433,7 @@ __device__ __forceinline__ uint32_t trace_packet_r(args_p A, int f, int i0, int 
                         bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
                     }
 #pragma unroll
-                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref | (ch[c].pad << 24);
+                    for (int c = 0; c < W; c++) rs[c] = ch[c].pad;  // ref | meta << 24 (bvh_build.cpp flatten)
                     // child c is needed if any ray of any lane enters it
 #pragma unroll
                     for (int c = 0; c < W; c++) {

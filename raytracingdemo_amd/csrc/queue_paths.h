@@ -390,7 +390,7 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
                         bx[c][3] = ch[c].hy; bx[c][4] = ch[c].lz; bx[c][5] = ch[c].hz;
                     }
 #pragma unroll
-                    for (int c = 0; c < W; c++) rs[c] = ch[c].ref | (ch[c].pad << 24);
+                    for (int c = 0; c < W; c++) rs[c] = ch[c].pad;  // ref | meta << 24 (bvh_build.cpp flatten)
                     child_hits<W, OCT>(bx, q, nox, noy, noz, tcull, hm);
                 }
                 const uint32_t mask = any_mask<W>(hm) & ((1u << (meta >> 2)) - 1u);

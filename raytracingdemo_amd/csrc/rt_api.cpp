@@ -392,7 +392,12 @@ void upload_one(rt_scene* s, int device) {
         if (v >= 1 && v < bpc) bpc = v;
     }
     r.grid = prop.multiProcessorCount * bpc;
-    r.pgrid = prop.multiProcessorCount * rt::packet_blocks_per_cu(f.width);
+    int pbpc = rt::packet_blocks_per_cu(f.width);
+    if (const char* e = std::getenv("RT_PACKET_BLOCKS_PER_CU")) {  // diagnostic: leave block slots free per CU
+        const int v = std::atoi(e);
+        if (v >= 1 && v < pbpc) pbpc = v;
+    }
+    r.pgrid = prop.multiProcessorCount * pbpc;
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
     const uint32_t K = (uint32_t)rt::packet_candidates();  // packet_exit's LDS ring (render.hip)

@@ -212,23 +212,27 @@ void restructure_treelets(WalkTree& w, int passes) {
         return bb;
     };
     std::vector<double> C(N, 0.0);
-    // post-order of the original shape (a restructured treelet's root keeps
-    // its id, and its other members were visited before it)
     std::vector<int32_t> post;
     post.reserve(N);
-    {
-        std::vector<std::pair<int32_t, bool>> st{{0, false}};
-        while (!st.empty()) {
-            auto [b, done] = st.back();
-            st.pop_back();
-            if (done || w.nodes[b].left < 0) { post.push_back(b); continue; }
-            st.push_back({b, true});
-            st.push_back({w.nodes[b].right, false});
-            st.push_back({w.nodes[b].left, false});
-        }
-    }
     constexpr int TL = 7, NS = 1 << TL;
     for (int pass = 0; pass < passes; pass++) {
+        // post-order of the current shape, taken again every pass: within a
+        // pass a restructured treelet's root keeps its id and its other
+        // members were visited before it, but a pass renumbers inner nodes,
+        // so the next pass's children-before-parents order (and the costs C
+        // of finished children it relies on) must come from the new shape
+        post.clear();
+        {
+            std::vector<std::pair<int32_t, bool>> st{{0, false}};
+            while (!st.empty()) {
+                auto [b, done] = st.back();
+                st.pop_back();
+                if (done || w.nodes[b].left < 0) { post.push_back(b); continue; }
+                st.push_back({b, true});
+                st.push_back({w.nodes[b].right, false});
+                st.push_back({w.nodes[b].left, false});
+            }
+        }
         for (int32_t r : post) {
             WalkNode& nr = w.nodes[r];
             if (nr.left < 0) { C[r] = box_of(r).area() * nr.count; continue; }

@@ -106,6 +106,9 @@ for s in $STEPS; do
                    > gpurun_out/sqp_summary.txt
                python tools/pmc_valu.py --kernel ${PATHS_KERNEL:-queue} gpurun_out/pmcp_key.txt gpurun_out/pmc_valu_paths.json \
                    gpurun_out/sqp/sqp*_counter_collection.csv ;;
+        xprobe) # exchange beside the render (tools/exchange_probe.py): all blocks, one block slot free per CU
+               run xprobe7 300 python tools/exchange_probe.py --shard-of 8 --steps 200 && \
+               RT_PACKET_BLOCKS_PER_CU=6 run xprobe6 300 python tools/exchange_probe.py --shard-of 8 --steps 200 ;;
         ab)    # A/B over environment settings: AB_ENVS="A=1 B=2;A=3;..." (one bench per entry)
                i=0; IFS=';' read -ra cfgs <<< "${AB_ENVS:-}"
                for c in "${cfgs[@]}"; do i=$((i+1))

@@ -650,6 +650,15 @@ def main():
     # gathered shards are not de-interleaved yet; the timed region ends after
     # the last ones are.  RT_BENCH_FUSED_DEINT=0: a de-interleave kernel per step.
     fused_deint = os.environ.get("RT_BENCH_FUSED_DEINT", "1") != "0" and not rehearse
+    # With an exchange (N > 1, or its simulation) every render leaves one
+    # workgroup slot per CU free (RT_FLAG_SIDE_SLOT), so the gather's RCCL
+    # kernels run beside the next render instead of waiting for its persistent
+    # grid to drain: on one GPU at the per-GPU size of 8 GPUs, a one-rank RCCL
+    # gather of the 28-MB payload finished 0.23 ms after its render instead
+    # of 0.69 ms, the simulated rank-0 step took 0.612 instead of 0.670 ms,
+    # and the render alone 0.565 vs 0.566 ms (tools/exchange_probe.py,
+    # DESIGN.md §8).  RT_BENCH_SIDE_SLOT=0 turns it off.
+    side_slot = (world > 1 or ship_sim > 0) and os.environ.get("RT_BENCH_SIDE_SLOT", "1") != "0"
     pending = [False] * NB
     mode = a.mode
 
@@ -669,7 +678,8 @@ def main():
             # 8 rows interleaved over the ranks)
             scene.render_shard_device(local, cams, W, H, srank, sworld, hit_id=r_ids[b].data_ptr(),
                                       dist=dists[b].data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
-                                      stream=sb.cuda_stream, mode=mode, timing=timing, count=count, spp=S, job=job)
+                                      stream=sb.cuda_stream, mode=mode, timing=timing, count=count, spp=S, job=job,
+                                      side_slot=side_slot)
             if padded:
                 ids[b][:, :my_rows] = r_ids[b]
                 rgb[b][:, :my_rows] = r_rgb[b]
@@ -910,6 +920,7 @@ def main():
                        "triangles": int(st["triangles"]), "mode": mode,
                        **({"diagnostic_shard_of": sworld} if sworld != world else {}),
                        **({"diagnostic_ship_sim": ship_sim} if ship_sim else {}),
+                       **({"side_slot": True} if side_slot else {}),
                        "parallelism": f"8-row image bands interleaved x{world}" +
                                       (" + RCCL gather of rgb (overlapped)" if world > 1 else ""),
                        **({"gather_verified": verified} if world > 1 else {}),

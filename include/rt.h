@@ -89,6 +89,12 @@ extern "C" {
                              launching stream (rt_frame_stats)              */
 #define RT_FLAG_SHADOW 4u /* rt_render_paths_device: one occlusion ray toward the
                              head-light from every bounce vertex            */
+#define RT_FLAG_SIDE_SLOT 8u /* primary-ray renders: the persistent traversal
+                             grid leaves one workgroup slot per CU free, so a
+                             kernel on another stream — a collective shipping
+                             the previous step's frames — runs beside the
+                             render instead of after it (one-process-per-GPU
+                             drivers)                         */
 
 #define RT_MISS 0xFFFFFFFFu
 

@@ -260,19 +260,21 @@ class Scene:
 
     def render_shard_device(self, device: int, cams, W: int, H: int, shard: int, nshards: int, hit_id=0, dist=0,
                             hit_pos=0, rgb=0, hit_count=0, stream=0, mode: str = "exact", count: bool = False,
-                            timing: bool = False, spp: int = 1, job: dict | None = None):
+                            timing: bool = False, spp: int = 1, job: dict | None = None, side_slot: bool = False):
         """Shard `shard` of `nshards` of every pose (bands of 8 rows interleaved,
         include/rt.h rt_render_shard_device) into device pointers: pose f's
         outputs start f * W * shard_height(H, nshards, shard) pixels in.
         job: the fields of an rt_deinterleave_job (gathered, block_bytes,
         section_offset, shards, frames, height, width, elem_bytes, frame_rows,
         frames_out) carried out on the side by this render's kernel
-        (rt_render_shard_device_job)."""
+        (rt_render_shard_device_job).  side_slot: RT_FLAG_SIDE_SLOT (one
+        workgroup slot per CU left free for a collective on another stream)."""
         n = len(cams)
         arr = (N.rt_camera * max(n, 1))(*[_camera(p, d, W, H) for p, d in cams])
         o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
         m = N.RT_MODE_FP64 if mode in ("fp64", "literal") else N.RT_MODE_EXACT
-        fl = (N.RT_FLAG_COUNT if count else 0) | (N.RT_FLAG_TIMING if timing else 0)
+        fl = ((N.RT_FLAG_COUNT if count else 0) | (N.RT_FLAG_TIMING if timing else 0) |
+              (N.RT_FLAG_SIDE_SLOT if side_slot else 0))
         if job is None:
             N.check(N.lib().rt_render_shard_device(self._h, int(device), arr, n, int(spp), m, int(shard),
                                                    int(nshards), C.byref(o), C.c_void_p(stream or None), fl))

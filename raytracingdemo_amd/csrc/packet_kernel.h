@@ -598,7 +598,8 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                         sp += __builtin_popcount(pm);
                     }
                     // the near child's ref, picked on the scalar unit (a
-                    // readlane from the lanes measured 0.5% slower)
+                    // readlane from the lanes measured 0.5% slower, a scalar
+                    // reload of the record's word +-0)
                     uint32_t nr = rs[0];
 #pragma unroll
                     for (int c = 1; c < W; c++) nr = near_c == c ? rs[c] : nr;

@@ -157,6 +157,7 @@ struct Replica {
     size_t spill_words = 0;
     int grid = 0;                // per-lane kernels: 256-thread workgroups
     int pgrid = 0;               // packet kernel: 64 * kPacketWaves-thread workgroups
+    int cus = 0;                 // compute units of the device
     uint32_t pool_chunks = 0;
     void* d_cand = nullptr;      // spp > 1 / wavefront paths: candidate lists in HBM
     uint64_t cand_cap = 0;       // pixels
@@ -398,6 +399,7 @@ void upload_one(rt_scene* s, int device) {
         if (v >= 1 && v < pbpc) pbpc = v;
     }
     r.pgrid = prop.multiProcessorCount * pbpc;
+    r.cus = prop.multiProcessorCount;
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
     const uint32_t K = (uint32_t)rt::packet_candidates();  // packet_exit's LDS ring (render.hip)
@@ -646,7 +648,7 @@ Slot& take_slot(Replica& r, hipStream_t st, bool shared) {
 
 // Runs the pipeline and tracks whether its work-queue block is left zeroed.
 void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
-            const hipEvent_t* tev, const rt_deinterleave_job* job = nullptr);
+            const hipEvent_t* tev, const rt_deinterleave_job* job = nullptr, bool side_slot = false);
 
 // A side de-interleave job (include/rt.h) in the launch's aux block.
 void set_job(RtLaunchAux& a, const rt_deinterleave_job* j) {
@@ -702,7 +704,7 @@ uint32_t literal_stack_bound(const rt_scene* s) {
 }
 
 void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
-            const hipEvent_t* tev, const rt_deinterleave_job* job) {
+            const hipEvent_t* tev, const rt_deinterleave_job* job, bool side_slot) {
     bool fresh_after = false;
     // a slot whose last launch overflowed its redo list (the count k_fixup
     // reported, possibly from a launch still running: a sizing hint only)
@@ -715,6 +717,8 @@ void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int
     if (seen > a.redo_cap) a.fgrid = r.grid;
     // the packet kernel may end the launch itself: no retry is possible
     a.self_fix = a.redo_cap >= lpix ? 1 : 0;
+    // RT_FLAG_SIDE_SLOT: one workgroup slot per CU left to other streams
+    if (side_slot && r.pgrid > r.cus) a.pgrid = r.pgrid - r.cus;
     set_job(a, job);
     if (a.job_src) {
         const bool empty = fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0;
@@ -778,7 +782,8 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
             }
             tev = r->tev[r->tev_used++].data();
         }
-        launch(s, *r, q, fp, mode, count, st, tev, f0 == 0 ? job : nullptr);  // (the job rides the first launch)
+        launch(s, *r, q, fp, mode, count, st, tev, f0 == 0 ? job : nullptr,  // (the job rides the first launch)
+               (flags & RT_FLAG_SIDE_SLOT) != 0);
     }
 }
 

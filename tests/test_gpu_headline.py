@@ -97,14 +97,16 @@ def test_headline_orbit_full_size_matches_oracle(oracle, monkeypatch, rays):
           f"redo {fs['redo_rays']} (chain {fs['redo_chain']}) of {fs['rays']} rays")
 
 
-@pytest.mark.parametrize("shard_of", [1, 8])
-def test_consecutive_launches_on_two_streams_equal_one_stream(shard_of):
+@pytest.mark.parametrize("shard_of,side_slot", [(1, False), (8, False), (8, True)])
+def test_consecutive_launches_on_two_streams_equal_one_stream(shard_of, side_slot):
     """bench.py's overlapped steps: consecutive orbit renders issued on two
     streams (the library alternates its two launch slots, so launch k + 1
     runs while launch k drains) into two buffer sets, hit counts zeroed on
     each stream before its render; every set equals the one-stream render bit
     for bit (hit ids, distances, PPM bytes, per-pose hit counts), also at the
-    per-GPU size of an 8-GPU run (shard 0 of 8)."""
+    per-GPU size of an 8-GPU run (shard 0 of 8), and with RT_FLAG_SIDE_SLOT
+    (the smaller persistent grid of a multi-GPU rank) with a copy kernel on a
+    third stream beside each render, as bench.py's gather."""
     tris, s = proxy()
     cams = orbit(tris)
     R = rt.shard_height(H, shard_of, 0) if shard_of > 1 else H
@@ -116,23 +118,35 @@ def test_consecutive_launches_on_two_streams_equal_one_stream(shard_of):
                 torch.empty((F, R, W, 3), dtype=torch.uint8, device="cuda:0"),
                 torch.zeros(F, dtype=torch.int64, device="cuda:0"))
 
-    def render(b, st):
+    def render(b, st, side=False):
         with torch.cuda.stream(st):
             b[3].zero_()
             s.render_shard_device(0, cams, W, H, 0, shard_of, hit_id=b[0].data_ptr(), dist=b[1].data_ptr(),
-                                  rgb=b[2].data_ptr(), hit_count=b[3].data_ptr(), stream=st.cuda_stream)
+                                  rgb=b[2].data_ptr(), hit_count=b[3].data_ptr(), stream=st.cuda_stream,
+                                  side_slot=side)
 
     ref = bufs()
     render(ref, torch.cuda.current_stream())
     torch.cuda.synchronize()
     sets = [bufs(), bufs()]
+    copies = [torch.empty_like(sets[0][2]) for _ in range(2)]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    post = torch.cuda.Stream(priority=-1)
     for k in range(6):
-        render(sets[k % 2], streams[k % 2])
+        b = k % 2
+        streams[b].wait_stream(post)  # the copy of this set's previous frames is done
+        render(sets[b], streams[b], side_slot)
+        if side_slot:
+            post.wait_stream(streams[b])
+            with torch.cuda.stream(post):
+                copies[b].copy_(sets[b][2])
     torch.cuda.synchronize()
     for b in sets:
         for x, y in zip(b, ref):
             assert torch.equal(x, y)
+    if side_slot:
+        for c in copies:
+            assert torch.equal(c, ref[2])
     assert int(ref[3].sum()) > 0
 
 

@@ -12,7 +12,9 @@ N = 8) on a high-priority side stream.  Modes:
   blit   device-to-device copy (torch copy_: a copy KERNEL, which needs CU
          slots — as RCCL's gather kernels do)
   sdma   device-to-host copy into pinned memory (the copy ENGINE: no CU slots;
-         the one-GPU stand-in for a peer copy over xGMI)
+         but PCIe-bound at ~53 GB/s, so no stand-in for a peer copy over xGMI)
+  rccl   a one-rank RCCL gather through torch.distributed (RCCL's own
+         kernels, on its high-priority stream: do they find a slot?)
 
 For each mode: the step time over the timed steps, and per step the delay
 from the render's end to the copy's end (HIP events).  RT_PACKET_BLOCKS_PER_CU
@@ -63,6 +65,14 @@ def main():
         scene.render_shard_device(0, cams, W, H, 0, G, hit_id=ids[b].data_ptr(), dist=dists[b].data_ptr(),
                                   rgb=rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(), stream=streams[b].cuda_stream)
 
+    dist = None
+    if "rccl" in a.modes:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29611")
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, pg_options=opts)
     for mode in a.modes.split(","):
         shipped = [None] * NB
         delays = []
@@ -81,7 +91,10 @@ def main():
                 return
             side.wait_stream(streams[b])
             with torch.cuda.stream(side):
-                if mode == "blit":
+                if mode == "rccl":
+                    w = dist.gather(rgb[b], [dst_dev[b]], dst=0, async_op=True)
+                    w.wait()
+                elif mode == "blit":
                     dst_dev[b].copy_(rgb[b])
                 else:
                     dst_host[b].copy_(rgb[b], non_blocking=True)
@@ -109,6 +122,8 @@ def main():
                                                 "p10": round(sorted(delays)[len(delays) // 10], 4),
                                                 "p90": round(sorted(delays)[len(delays) * 9 // 10], 4)}
         print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

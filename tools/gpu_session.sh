@@ -107,8 +107,19 @@ for s in $STEPS; do
                python tools/pmc_valu.py --kernel ${PATHS_KERNEL:-queue} gpurun_out/pmcp_key.txt gpurun_out/pmc_valu_paths.json \
                    gpurun_out/sqp/sqp*_counter_collection.csv ;;
         xprobe) # exchange beside the render (tools/exchange_probe.py): all blocks, one block slot free per CU
-               run xprobe7 300 python tools/exchange_probe.py --shard-of 8 --steps 200 && \
-               RT_PACKET_BLOCKS_PER_CU=6 run xprobe6 300 python tools/exchange_probe.py --shard-of 8 --steps 200 ;;
+               run xprobe7 300 python tools/exchange_probe.py --shard-of 8 --steps 200 ${XPROBE_MODES:+--modes $XPROBE_MODES} && \
+               RT_PACKET_BLOCKS_PER_CU=6 run xprobe6 300 python tools/exchange_probe.py --shard-of 8 --steps 200 \
+                   ${XPROBE_MODES:+--modes $XPROBE_MODES} ;;
+        xtrace) # kernel trace of the probe's RCCL mode with one block slot per CU free
+               RT_PACKET_BLOCKS_PER_CU=6 run xtrace 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                   -d gpurun_out/xtrace -o x -- python tools/exchange_probe.py --shard-of 8 --steps 50 --modes rccl ;;
+        ship8) # rank 0's side of an 8-GPU step simulated on one GPU (bench.py RT_BENCH_SHIP_SIM=2), with the
+               # side slot (RT_FLAG_SIDE_SLOT, the default with an exchange) and without; then the render alone
+               for rep in 1 2; do
+               RT_BENCH_SHIP_SIM=2 run ship8_side$rep 300 python bench.py --no-cpu --no-dropin --steps 40 --shard-of 8 && \
+               RT_BENCH_SHIP_SIM=2 RT_BENCH_SIDE_SLOT=0 run ship8_full$rep 300 python bench.py --no-cpu --no-dropin \
+                   --steps 40 --shard-of 8 || exit 1; done
+               run shard8 300 python bench.py --no-cpu --no-dropin --steps 40 --shard-of 8 ;;
         ab)    # A/B over environment settings: AB_ENVS="A=1 B=2;A=3;..." (one bench per entry)
                i=0; IFS=';' read -ra cfgs <<< "${AB_ENVS:-}"
                for c in "${cfgs[@]}"; do i=$((i+1))

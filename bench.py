@@ -342,6 +342,18 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
                 sh_bytes += sh_n * 64 + sh_lit * 48
         alg_pose += sh_bytes / F
         alg_parts["occlusion"] = round(sh_bytes / F)
+    # The headline's convention, a record once per fetching wave instruction,
+    # applied to the per-lane walks too (the per-lane figure
+    # above is not comparable with the headline's): the lane walks' node
+    # steps and triangle records counted once per distinct record among the
+    # lanes of each wave step (render.hip wave_step_fetches), the fp64
+    # records, queues and outputs as above.  None if the counting pass did
+    # not fill the wave-distinct counters (a library without them).
+    alg_wave = None
+    if cs.get("lane_wave_nodes"):
+        lane_bytes = (cs["node_fetches"] * 96 + cs["tri_prefilter"] * 48 +
+                      (cs["shadow_lane_nodes"] * 96 + cs["shadow_lane_tris"] * 48 if shadow_kind != "binned" else 0))
+        alg_wave = alg_pose + (cs["lane_wave_nodes"] * 96 + cs["lane_wave_tris"] * 48 - lane_bytes) / F
     # W warm-up steps, then render-only steps until SETTLE_S of GPU work (main())
     for w in range(a.warmup):
         step(w, timing=True)
@@ -440,6 +452,11 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "frac_per_lane": round(achieved_pl / HBM_PEAK_GBS, 4),
+                         # every walk's records once per wave instruction (the
+                         # headline's convention; comparable with its frac)
+                         "frac_per_wave_instruction": (round(alg_wave / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
+                                                       if alg_wave and kernel_s > 0 else None),
+                         "alg_bytes_per_wave_instruction": round(alg_wave) if alg_wave else None,
                          # measured bytes past L2 (FETCH_SIZE x 2 + WRITE_SIZE): fabric
                          # requests, Infinity-Cache hits included (MI355X guide, HBM
                          # section) — an upper bound of HBM traffic, not HBM itself

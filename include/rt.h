@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* status codes */
 #define RT_OK 0
@@ -184,6 +184,10 @@ typedef struct {
     uint64_t timed_launches; /* RT_FLAG_TIMING launches since the last reset */
     double trace_ms;         /*   summed traversal-kernel time (HIP events
                                   recorded around it on the launch stream) */
+    uint64_t lane_wave_nodes;/* per-lane walks (paths, occlusion rays): node fetches
+                                counted once per wave instruction (lanes of one
+                                step loading the same node share the fetch) */
+    uint64_t lane_wave_tris; /*   and fp32 triangle records, the same way  */
 } rt_frame_stats_t;
 
 /* Host time of each stage of rt_scene_create (std::chrono, ms).  With the

@@ -88,7 +88,8 @@ class rt_frame_stats_t(C.Structure):
                 ("shadow_rays", C.c_uint64), ("shadow_occluded", C.c_uint64),
                 ("side_jobs_fused", C.c_uint64), ("side_jobs_kernel", C.c_uint64),
                 ("shadow_wave_nodes", C.c_uint64), ("shadow_wave_tris", C.c_uint64),
-                ("shadow_lane_nodes", C.c_uint64), ("shadow_lane_tris", C.c_uint64), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double)]
+                ("shadow_lane_nodes", C.c_uint64), ("shadow_lane_tris", C.c_uint64), ("timed_launches", C.c_uint64), ("trace_ms", C.c_double),
+                ("lane_wave_nodes", C.c_uint64), ("lane_wave_tris", C.c_uint64)]
 
 
 class rt_build_times_t(C.Structure):

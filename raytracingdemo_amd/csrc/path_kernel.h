@@ -321,6 +321,7 @@ __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFram
     w.tcull = round_up_f(tmax);
     bool occ = false;
     while (w.cur != RT_INVALID_REF) {
+        if constexpr (COUNT) wave_step_fetches(w.cur, lc);
         if (!(w.cur & RT_LEAF_BIT)) {
             w.visit_node(sc, st, lc);
             continue;
@@ -350,6 +351,8 @@ __device__ __forceinline__ bool lane_occluded(const RtDevScene& sc, const RtFram
     if (COUNT) {
         oc->nodes += lc.nodes;
         oc->pre += lc.pre;
+        oc->wnodes += lc.wnodes;
+        oc->wtris += lc.wtris;
     }
     return occ;
 }
@@ -495,6 +498,8 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
                     segs++;
                     if (COUNT) {
                         tot.nodes += lc.nodes;
+                        tot.wnodes += lc.wnodes;
+                        tot.wtris += lc.wtris;
                         tot.pre += lc.pre;
                         tot.tris += lc.tris;
                         tot.chain += lc.chain;
@@ -563,11 +568,15 @@ __global__ void __launch_bounds__(256) RT_PATHS_ATTR k_paths(RtDevScene sc, RtFr
             wave_add<20>(fp.counters + 25, sh_occ);
             if (COUNT) {
                 wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 30, shc.wnodes);
+                wave_add<28>(fp.counters + 31, shc.wtris);
                 wave_add<28>(fp.counters + 29, shc.pre);
             }
         }
         if (COUNT && fp.counters) {
             wave_add<24>(fp.counters + 1, tot.nodes);
+            wave_add<28>(fp.counters + 30, tot.wnodes);
+            wave_add<28>(fp.counters + 31, tot.wtris);
             wave_add<24>(fp.counters + 6, tot.pre);
             wave_add<24>(fp.counters + 2, tot.tris);
             wave_add<24>(fp.counters + 3, tot.chain);

@@ -547,6 +547,12 @@ constexpr uint32_t kQFromPass0 = 0x80000000u;
 #ifndef RT_QP_CLAIM
 #define RT_QP_CLAIM 1  // units claimed per atomic by k_q_primary
 #endif
+// Phase timing builds (never shipped; results are wrong): 1 = the primary
+// kernel stops after the walk, 2 = after the exact resolve (its tcull /
+// winner go to hit_id so the work stays live).
+#ifndef RT_QP_DIAG
+#define RT_QP_DIAG 0
+#endif
 template <int W, int S, bool COUNT, bool PACK, bool PRIM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ? RT_QP_WPE : RT_PATHS_WPE))) k_q_primary(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                                  PathQs qs, uint32_t frame, int bounces) {
@@ -617,6 +623,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
                 lane_walk<W, S, RT_PATHS_K, COUNT, W == 8 && RT_QNODES>(sc, q0, tsl, st, pcand, lc, tcull, nc, over);
             }
         }
+        if constexpr (RT_QP_DIAG == 1) {
+            if (valid && fp.hit_id)
+                fp.hit_id[((uint32_t)rv * (uint32_t)fp.W + (uint32_t)iv) * (uint32_t)spp + (uint32_t)s] =
+                    __float_as_uint(tcull) + (uint32_t)nc + (over ? 1u : 0u);
+            continue;
+        }
         bool fall = false;
         if (valid) {
             fall = over;
@@ -625,6 +637,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
                                             lc) != 0;
         }
         const uint32_t path = ((uint32_t)rv * (uint32_t)fp.W + (uint32_t)iv) * (uint32_t)spp + (uint32_t)s;
+        if constexpr (RT_QP_DIAG == 2) {
+            if (valid && fp.hit_id) fp.hit_id[path] = (uint32_t)win.tri + (fall ? 1u : 0u);
+            continue;
+        }
         if (fall) {  // the ray to the fall-back list: q[1] (free until segment 1) holds it
             RT_G double* p = q_entry(qs, 1, atomicAdd(qc_fb(qs, 0), 1u));
             p[0] = ray.ox;
@@ -721,6 +737,8 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
                 lane_walk<W, S, K, COUNT, W == 8 && RT_QNODES>(sc, q, tsl, st, cand, lc, tcull, nc, over);
                 if (COUNT) {
                     tot.nodes += lc.nodes;
+                    tot.wnodes += lc.wnodes;
+                    tot.wtris += lc.wtris;
                     tot.pre += lc.pre;
                 }
             }
@@ -761,11 +779,15 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
             wave_add<24>(fp.counters + 25, sh_occ);
             if (COUNT) {
                 wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 30, shc.wnodes);
+                wave_add<28>(fp.counters + 31, shc.wtris);
                 wave_add<28>(fp.counters + 29, shc.pre);
             }
         }
         if (COUNT) {
             wave_add<28>(fp.counters + 1, tot.nodes);
+            wave_add<28>(fp.counters + 30, tot.wnodes);
+            wave_add<28>(fp.counters + 31, tot.wtris);
             wave_add<28>(fp.counters + 6, tot.pre);
             wave_add<28>(fp.counters + 2, tot.tris);
             wave_add<28>(fp.counters + 3, tot.chain);
@@ -821,6 +843,8 @@ k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
         wave_add<24>(fp.counters + 25, occl);
         if (COUNT) {
             wave_add<28>(fp.counters + 28, shc.nodes);
+            wave_add<28>(fp.counters + 30, shc.wnodes);
+            wave_add<28>(fp.counters + 31, shc.wtris);
             wave_add<28>(fp.counters + 29, shc.pre);
         }
     }
@@ -898,11 +922,15 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
             wave_add<24>(fp.counters + 25, sh_occ);
             if (COUNT) {
                 wave_add<28>(fp.counters + 28, shc.nodes);
+                wave_add<28>(fp.counters + 30, shc.wnodes);
+                wave_add<28>(fp.counters + 31, shc.wtris);
                 wave_add<28>(fp.counters + 29, shc.pre);
             }
         }
         if (COUNT) {
             wave_add<28>(fp.counters + 1, tot.nodes);
+            wave_add<28>(fp.counters + 30, tot.wnodes);
+            wave_add<28>(fp.counters + 31, tot.wtris);
             wave_add<28>(fp.counters + 2, tot.tris);
             wave_add<28>(fp.counters + 3, tot.chain);
         }

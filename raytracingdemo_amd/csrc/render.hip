@@ -131,7 +131,33 @@ struct Win {
 // Per-lane traversal counters (COUNT builds).
 struct LaneCounts {
     uint32_t nodes = 0, tris = 0, chain = 0, chain_nodes = 0, pre = 0;
+    // per-lane walks: records fetched once per wave instruction (the lanes
+    // of one step that load the same node or triangle record share the
+    // fetch), added in the wave's first active lane only
+    uint32_t wnodes = 0, wtris = 0;
 };
+
+// COUNT builds: the wave-distinct node fetches and triangle records of one
+// step of the lanes' walks that are active here (cur: each lane's next node
+// or leaf ref).  Added to lc of the first active lane.
+__device__ __forceinline__ void wave_step_fetches(uint32_t cur, LaneCounts& lc) {
+    const uint64_t act = __ballot(1);
+    const bool node = !(cur & RT_LEAF_BIT);
+    uint64_t todo = act;
+    uint32_t wn = 0, wt = 0;
+    while (todo) {
+        const int l = (int)__builtin_ctzll(todo);
+        const uint32_t k = (uint32_t)__shfl((int)cur, l);
+        todo &= ~__ballot(cur == k);
+        if (k & RT_LEAF_BIT) wt += ((k >> 27) & 15u) + 1u;
+        else wn++;
+    }
+    (void)node;
+    if ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(act)) {
+        lc.wnodes += wn;
+        lc.wtris += wt;
+    }
+}
 
 // The exact per-lane traversal of one ray, the reference's closest-hit
 // semantics (stack_bvh.hpp:611-644) over the walk tree: ray_of() returns the
@@ -489,7 +515,10 @@ __device__ __forceinline__ void lane_walk(const RtDevScene& sc, const Ray32& q, 
                                           bool& over_out) {
     LaneWalk<W, S, K, COUNT, QN> w;
     w.begin(sc, q, tsl, st);
-    while (w.cur != RT_INVALID_REF) w.step(sc, st, cand, lc);
+    while (w.cur != RT_INVALID_REF) {
+        if constexpr (COUNT) wave_step_fetches(w.cur, lc);
+        w.step(sc, st, cand, lc);
+    }
     tcull_out = w.tcull;
     nc_out = w.nc;
     over_out = w.over;

@@ -77,7 +77,7 @@ size_t align_up(size_t x) {
 }
 
 // d_counters: RT_FLAG_COUNT counters (rt_frame_stats)
-constexpr size_t kCounterWords = 32;  // 18-23: RT_PROFILE builds (packet_kernel.h); 24-29: occlusion rays
+constexpr size_t kCounterWords = 32;  // 18-23: RT_PROFILE builds (packet_kernel.h); 24-29: occlusion rays; 30-31: per-lane walks, wave-distinct fetches
 #if defined(RT_PROFILE) && RT_PROFILE
 constexpr bool RT_PROFILE_BUILD = true;  // every timed launch writes the counters
 #else
@@ -1506,6 +1506,8 @@ int rt_frame_stats(rt_scene* s, int device, int reset, rt_frame_stats_t* out) {
         out->shadow_wave_tris = c[27];
         out->shadow_lane_nodes = c[28];
         out->shadow_lane_tris = c[29];
+        out->lane_wave_nodes = c[30];
+        out->lane_wave_tris = c[31];
         out->side_jobs_fused = r.jobs_fused;
         out->side_jobs_kernel = r.jobs_kernel;
         if (reset) r.jobs_fused = r.jobs_kernel = 0;

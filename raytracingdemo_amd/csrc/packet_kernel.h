@@ -217,9 +217,24 @@ struct PacketArgs {
     RtDevScene sc;
     RtFrameParams fp;
     RtLaunchAux aux;
+    // PATHS (queue_paths.h): the queued path tracer's workspace, the hash's
+    // frame number and the bounce segments per path
+    PathQs qs;
+    uint32_t frame;
+    int32_t bounces;
 };
 static_assert(sizeof(PacketArgs) % 4 == 0, "argument block is copied as words");
 typedef const __attribute__((address_space(3))) PacketArgs* args_p;
+
+// PATHS: the packed packet walk traces the primary segments of the queued
+// path tracer (config c5).  Defined in queue_paths.h: the sample's jittered
+// sub-pixel offset, and the primary vertex (outputs, first bounce appended,
+// radiance, or the fall-back list); returns 1 for a resolved hit.
+template <int W>
+__device__ void q_primary_offset(args_p A, int s, int i, int r, double& ox, double& oy);
+template <int W, bool COUNT>
+__device__ uint32_t q_primary_vertex(args_p A, int s, int i, int r, bool valid, uint32_t redo, const Best& out,
+                                     const Ray64& pre);
 
 __device__ __forceinline__ args_p launder(args_p p) {
     asm volatile("" : "+s"(p));
@@ -469,7 +484,7 @@ struct TileOut {
     uint32_t hits;  // fp.pack: on a pixel's first-sample lane, its samples hit
 };
 
-template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK>
+template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK, bool PATHS = false>
 __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, bool valid,
                                                 uint32_t* __restrict__ wstack, uint2* __restrict__ cand) {
     const int lane = threadIdx.x & 63;
@@ -484,7 +499,10 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     double kd[3];  // kKeepDir: the fp64 direction, kept for the resolve
     {
         const RtFrameParams fp = kload(&A->fp);
-        const RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f / fp.spp]), fp, f);  // this tile's frame
+        RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f / fp.spp]), fp, f);  // this tile's frame
+#if !defined(RT_QPV_DIAG) || RT_QPV_DIAG < 2
+        if constexpr (PATHS) q_primary_offset<W>(A, f, i, r, cam.ox, cam.oy);  // the path sample's jitter
+#endif
         // kFastInv: the fp32 reciprocals straight from the fp32 direction
         // (v_rcp_f32 + a Newton step: no fp64 divisions in the set-up)
         const Ray64 ray = gen_ray<!kFastInv>(fp, cam, i, rt_image_row(fp.row0, fp.row_stride, fp.band, r));
@@ -759,7 +777,16 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
             [&](uint32_t c) { return cand[c * 64 + lane]; }, ch, dropped, drop, out, sh, rc,
             kKeepDir ? &pre : nullptr);
         const bool hit_s = !redo && out.tri >= 0;
-        if (spp == 1) {
+        if constexpr (PATHS) {
+            // the path's primary vertex (queue_paths.h; the sample's
+            // outputs, its first bounce ray appended, or the fall-back list)
+            static_assert(PACK && kKeepDir, "path primaries: packed samples, the kept fp64 direction");
+#if defined(RT_QPV_DIAG) && RT_QPV_DIAG > 0
+            res.hits = out.tri >= 0;  // timing build: no path vertex (wrong results)
+#else
+            res.hits = q_primary_vertex<W, COUNT>(A, f - pose * spp, i, r, true, redo, out, pre);
+#endif
+        } else if (spp == 1) {
             if (redo) {
                 // k_fixup redoes the pixel with the exact per-lane path
                 redo_put(aux, ob | (redo == 2u ? kRedoPass1 : 0u));
@@ -837,14 +864,15 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                 atomicAdd(&fp.counters[17], (unsigned long long)u_win);
             }
             atomicAdd(&fp.counters[0], 1ull);
-            atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
+            // (PATHS: node_fetches are the per-lane bounce walks' counter)
+            if constexpr (!PATHS) atomicAdd(&fp.counters[1], (unsigned long long)n_nodes);
             atomicAdd(&fp.counters[2], (unsigned long long)rc.tris);
             atomicAdd(&fp.counters[3], (unsigned long long)rc.chain);
             if (hit_s) atomicAdd(&fp.counters[4], 1ull);
             atomicAdd(&fp.counters[5], (unsigned long long)rc.chain_nodes);
             atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
-            if (redo == 1) atomicAdd(&fp.counters[10], 1ull);
-            if (redo == 2) atomicAdd(&fp.counters[11], 1ull);
+            if (!PATHS && redo == 1) atomicAdd(&fp.counters[10], 1ull);
+            if (!PATHS && redo == 2) atomicAdd(&fp.counters[11], 1ull);
             if (spilled) atomicAdd(&fp.counters[13], 1ull);
             if (dropped) atomicAdd(&fp.counters[14], 1ull);
         }
@@ -1212,7 +1240,7 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
 
 // JOB: the launch carries a side de-interleave job (RtLaunchAux::job_*; its
 // own instantiation, so the kernels without one keep their registers).
-template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK = false, bool JOB = false>
+template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK = false, bool JOB = false, bool PATHS = false>
 __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_packet(PacketArgs args) {
     __shared__ uint32_t stacks[kPacketWaves][SP];
     __shared__ uint2 cands[kPacketWaves][K * 64];
@@ -1298,7 +1326,7 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             r = ty * 8 + (lane >> 3);
         }
         const TileOut o =
-            trace_packet<W, SP, K, COUNT, FUSED, PACK>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);
+            trace_packet<W, SP, K, COUNT, FUSED, PACK, PATHS>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);
         if constexpr (FUSED) {
             uint32_t h = (uint32_t)__builtin_popcountll(__ballot(o.hit));
             if constexpr (pack) {  // samples hit per pixel (<= 64) summed over the wave

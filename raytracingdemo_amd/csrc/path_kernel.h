@@ -173,6 +173,10 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
                     ChildRec ch[W];
 #pragma unroll
                     for (int c = 0; c < W; c++) ch[c] = load_child(nb + c);
+                    // all 8 words of every record loaded (4 s_load_dwordx16),
+                    // not the ~24 narrow loads of the words used
+#pragma unroll
+                    for (int c = 0; c < W; c++) pin_rec(ch[c]);
 #pragma unroll
                     for (int c = 0; c < W; c++) {
                         bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;

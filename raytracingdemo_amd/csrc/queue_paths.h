@@ -45,15 +45,26 @@
 #endif
 
 // Control words (u32, RT_QC_STRIDE apart): per segment b = 0 .. bounces,
-//   emit(b)  rays segment b appended to queue b & 1 (segment b + 1's input)
-//   pull(b)  pull cursor of segment b's kernel (primary: tile cursor)
-//   fb(b)    fall-back entries segment b listed
+//   emit(b, x)  rays segment b appended to partition x of queue b & 1
+//               (segment b + 1's input)
+//   pull(b, x)  pull cursor of segment b's kernel in partition x (k_q_primary:
+//               its tile cursor)
+//   fb(b)       fall-back entries segment b listed
+//   sh(b)       occlusion records segment b appended (queued shadows); its
+//               second word: the occlusion kernels' pull cursor
 #define RT_QC_STRIDE 16
-//   sh(b)    occlusion records segment b appended (queued shadows)
-__device__ __forceinline__ RT_G uint32_t* qc_emit(const PathQs& q, int b) { return q.ctl + (4 * b) * RT_QC_STRIDE; }
-__device__ __forceinline__ RT_G uint32_t* qc_pull(const PathQs& q, int b) { return q.ctl + (4 * b + 1) * RT_QC_STRIDE; }
-__device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) { return q.ctl + (4 * b + 2) * RT_QC_STRIDE; }
-__device__ __forceinline__ RT_G uint32_t* qc_sh(const PathQs& q, int b) { return q.ctl + (4 * b + 3) * RT_QC_STRIDE; }
+__device__ __forceinline__ RT_G uint32_t* qc_emit(const PathQs& q, int b, int x) {
+    return q.ctl + (RT_QC_LINES * b + x) * RT_QC_STRIDE;
+}
+__device__ __forceinline__ RT_G uint32_t* qc_pull(const PathQs& q, int b, int x) {
+    return q.ctl + (RT_QC_LINES * b + RT_QPARTS + x) * RT_QC_STRIDE;
+}
+__device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) {
+    return q.ctl + (RT_QC_LINES * b + 2 * RT_QPARTS) * RT_QC_STRIDE;
+}
+__device__ __forceinline__ RT_G uint32_t* qc_sh(const PathQs& q, int b) {
+    return q.ctl + (RT_QC_LINES * b + 2 * RT_QPARTS + 1) * RT_QC_STRIDE;
+}
 
 // Queue entry e of queue k: 10 doubles {o, d, L, path | pad}.
 constexpr int kQDoubles = 10;
@@ -75,19 +86,20 @@ __device__ __forceinline__ void q_load(const PathQs& q, int k, uint32_t e, Ray64
     path = (uint32_t)__double_as_longlong(p[9]);
 }
 
-// Appends each emitting lane's bounce ray (origin, direction, path) to queue
-// k with one atomic per wave (the compaction: lanes whose paths ended append
-// nothing) and returns the lane's entry; the radiance is written after the
-// occlusion test (q_light).  Every lane of the wave calls it.
-__device__ __forceinline__ uint32_t q_append(const PathQs& q, int k, RT_G uint32_t* cnt, bool emit, const Ray64& nr,
+// Appends each emitting lane's bounce ray (origin, direction, path) to
+// partition x of queue k (segment b's counter) with one atomic per wave (the
+// compaction: lanes whose paths ended append nothing) and returns the lane's
+// entry (an index into the whole queue); the radiance is written after the
+// occlusion test (q_light).  Every lane of the wave calls it, with one x.
+__device__ __forceinline__ uint32_t q_append(const PathQs& q, int k, int x, int b, bool emit, const Ray64& nr,
                                              uint32_t path) {
     const uint64_t em = __ballot(emit);
     if (em == 0) return 0;
     const int lane = (int)(threadIdx.x & 63);
     const int leader = __builtin_ctzll(em);
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__builtin_popcountll(em));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    if (lane == leader) base = atomicAdd(qc_emit(q, b, x), (uint32_t)__builtin_popcountll(em));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader) + (uint32_t)x * q.pcap;
     const uint32_t slot = base + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1ull));
     if (emit) {
         RT_G double* p = q_entry(q, k, slot);
@@ -100,6 +112,32 @@ __device__ __forceinline__ uint32_t q_append(const PathQs& q, int k, RT_G uint32
         p[9] = __longlong_as_double((long long)path);
     }
     return slot;
+}
+
+// q_append for one lane (the fall-back kernel: lanes of a wave append to
+// different partitions, ~1e-4 of the rays).
+__device__ __forceinline__ uint32_t q_append_lane(const PathQs& q, int k, int x, int b, bool emit, const Ray64& nr,
+                                                  uint32_t path) {
+    if (!emit) return 0;
+    const uint32_t slot = atomicAdd(qc_emit(q, b, x), 1u) + (uint32_t)x * q.pcap;
+    RT_G double* p = q_entry(q, k, slot);
+    p[0] = nr.ox;
+    p[1] = nr.oy;
+    p[2] = nr.oz;
+    p[3] = nr.dx;
+    p[4] = nr.dy;
+    p[5] = nr.dz;
+    p[9] = __longlong_as_double((long long)path);
+    return slot;
+}
+
+// The partition of a primary path (parts > 1: its tile's XCD queue,
+// k_trace_packet's tiles of ptile x ptile pixels dealt to queue t % parts).
+__device__ __forceinline__ int q_primary_part(const PathQs& q, const RtFrameParams& fp, uint32_t path) {
+    if (q.parts <= 1) return 0;
+    const uint32_t pix = path / (uint32_t)fp.spp;
+    const uint32_t i = pix % (uint32_t)fp.W, r = pix / (uint32_t)fp.W;
+    return (int)(((r / q.ptile) * q.ptiles_x + i / q.ptile) % q.parts);
 }
 
 // Sample index of a path -> its pixel's image coordinates and the hash seed.
@@ -384,6 +422,10 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
                     ChildRec ch[W];
 #pragma unroll
                     for (int c = 0; c < W; c++) ch[c] = load_child(nb + c);
+                    // all 8 words of every record loaded (4 s_load_dwordx16),
+                    // not the ~24 narrow loads of the words used
+#pragma unroll
+                    for (int c = 0; c < W; c++) pin_rec(ch[c]);
 #pragma unroll
                     for (int c = 0; c < W; c++) {
                         bx[c][0] = ch[c].lx; bx[c][1] = ch[c].hx; bx[c][2] = ch[c].ly;
@@ -489,7 +531,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_
     uint32_t occl = 0, cast = 0, w_nodes = 0, w_tris = 0;
     for (;;) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 1, 64u);  // (the pull line's second word)
+        if (lane == 0) base = atomicAdd(qc_sh(qs, b) + 1, 64u);  // (the record count's line, second word)
         base = (uint32_t)__shfl((int)base, 0);
         if (base >= n) break;
         const uint32_t e = base + (uint32_t)lane;
@@ -579,7 +621,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
         // RT_QP_CLAIM consecutive units per claim (one atomic on the shared
         // counter per claim, not per unit)
         int u0 = 0;
-        if (lane == 0) u0 = (int)atomicAdd(qc_pull(qs, 0), (uint32_t)RT_QP_CLAIM);
+        if (lane == 0) u0 = (int)atomicAdd(qc_pull(qs, 0, 0), (uint32_t)RT_QP_CLAIM);
         u0 = __shfl(u0, 0);
         if (u0 >= units) break;
         const int u1 = u0 + RT_QP_CLAIM < units ? u0 + RT_QP_CLAIM : units;
@@ -667,7 +709,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
             store_sample(fp, path, hb, shade_of(sc, win.tri));
             hit = win.tri >= 0;
         }
-        const uint32_t slot = q_append(qs, 0, qc_emit(qs, 0), emit, nr, path);
+        const uint32_t slot = q_append(qs, 0, 0, 0, emit, nr, path);  // (one partition: qs.parts = 1)
         if (valid && !fall) {
             bool qd;
             uint32_t dst;
@@ -683,6 +725,86 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PRIM ?
         }
         }
     }
+}
+
+// The packed packet walk (k_trace_packet<…, PATHS = true>, packet_kernel.h)
+// as the primary segment: sample s of pixel (i, r) takes the jittered
+// sub-pixel offset of k_q_primary — draws 0 and 1 of the path's hash.
+template <int W>
+__device__ void q_primary_offset(args_p A, int s, int i, int r, double& ox, double& oy) {
+    A = launder(A);
+    const int Wd = kword(&A->fp.W);
+    const int j = rt_image_row(kword(&A->fp.row0), kword(&A->fp.row_stride), kword(&A->fp.band), r);
+    const uint32_t seed = path_seed(kword(&A->frame), (uint32_t)j * (uint32_t)Wd + (uint32_t)i, (uint32_t)s);
+    ox = path_u(seed, 0);
+    oy = path_u(seed, 1);
+}
+
+// Its primary vertex, k_q_primary's epilogue operation for operation: the
+// sample's outputs, the first bounce ray appended to queue 0 (compacted, one
+// atomic per wave) with the vertex colour as its radiance, or — when the
+// exact resolve could not certify the lane's winner (redo: 1 a list
+// overflow, 2 a winner the reference tree cannot see) — the ray on segment
+// 0's fall-back list for k_q_fallback.  out: the exact winner with its hit
+// point fl(o + d t); pre: the fp64 ray (o, d).  Every lane of the wave that
+// traced a valid sample calls it (q_append is wave-wide).  Returns 1 for a
+// hit resolved here (the pose's hit count).
+template <int W, bool COUNT>
+__device__ uint32_t q_primary_vertex(args_p A, int s, int i, int r, bool valid, uint32_t redo, const Best& out,
+                                     const Ray64& pre) {
+    A = launder(A);
+    const PathQs qs = kload(&A->qs);
+    const int Wd = kword(&A->fp.W), spp = kword(&A->fp.spp);
+    const uint32_t path = ((uint32_t)r * (uint32_t)Wd + (uint32_t)i) * (uint32_t)spp + (uint32_t)s;
+    const bool fall = valid && redo != 0;
+    if (fall) {  // the ray to the fall-back list: q[1] (free until segment 1) holds it
+        RT_G double* p = q_entry(qs, 1, atomicAdd(qc_fb(qs, 0), 1u));
+        p[0] = pre.ox;
+        p[1] = pre.oy;
+        p[2] = pre.oz;
+        p[3] = pre.dx;
+        p[4] = pre.dy;
+        p[5] = pre.dz;
+        p[9] = __longlong_as_double((long long)(path | (redo == 1 ? kQFromPass0 : 0u)));
+    }
+    const bool done = valid && !fall;
+    bool emit = false;
+    Ray64 nr{};
+    const RtDevScene sc = kload(&launder(A)->sc);
+    if (done && out.tri >= 0) {  // q_bounce with the hit point the resolve computed
+        emit = 0 < kword(&A->bounces);
+        if (emit) {
+            const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)out.tri;
+            const int j = rt_image_row(kword(&A->fp.row0), kword(&A->fp.row_stride), kword(&A->fp.band), r);
+            const uint32_t seed = path_seed(kword(&A->frame), (uint32_t)j * (uint32_t)Wd + (uint32_t)i, (uint32_t)s);
+            bounce_dir(T[RT_T64_NORMAL], T[RT_T64_NORMAL + 1], T[RT_T64_NORMAL + 2], pre.dx, pre.dy, pre.dz,
+                       path_u(seed, 2u), path_u(seed, 3u), nr.dx, nr.dy, nr.dz);
+            nr.ox = out.px;
+            nr.oy = out.py;
+            nr.oz = out.pz;
+        }
+    }
+    if (done) store_sample(kload(&launder(A)->fp), path, out, shade_of(sc, out.tri));
+    // the partition of the tile's XCD queue (k_trace_packet: xq = block % RT_QUEUES)
+    const uint32_t slot = q_append(qs, 0, (int)(blockIdx.x % (uint32_t)qs.parts), 0, emit, nr, path);
+    if (done) {  // q_light of vertex 0: its colour always counts (no occlusion ray)
+        double L[3] = {0.0, 0.0, 0.0};
+        if (out.tri >= 0) {
+            const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)out.tri;
+            const double w = __builtin_ldexp(1.0, 0);
+            double c[3];
+            shade_at(frame_cam(kload(&launder(A)->fp), 0), out.px, out.py, out.pz, T[RT_T64_NORMAL],
+                     T[RT_T64_NORMAL + 1], T[RT_T64_NORMAL + 2], c);
+            L[0] = L[0] + w * c[0];
+            L[1] = L[1] + w * c[1];
+            L[2] = L[2] + w * c[2];
+        }
+        RT_G double* f = emit ? q_entry(qs, 0, slot) + 6 : qs.Lfin + 3 * (size_t)path;
+        f[0] = L[0];
+        f[1] = L[1];
+        f[2] = L[2];
+    }
+    return done && out.tri >= 0 ? 1u : 0u;
 }
 
 // Segment b (1 .. bounces) over queue (b - 1) & 1.  Fall-back entries: the
@@ -701,7 +823,12 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int qin = (b - 1) & 1, qout = b & 1;
-    const uint32_t n = *qc_emit(qs, b - 1);
+    // the wave's partition: its XCD's (blocks are dealt to the XCDs round-
+    // robin), then, once that is drained, the others in turn (their counters
+    // then see a few cross-XCD atomics at the segment's tail)
+    const int parts = (int)qs.parts;
+    int x = (int)(blockIdx.x % (uint32_t)parts), left = parts;
+    uint32_t n = *qc_emit(qs, b - 1, x);
     LaneStack<S> st;
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
@@ -710,11 +837,16 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
     LaneCounts tot;
     for (;;) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qc_pull(qs, b), 64u);
+        if (lane == 0) base = atomicAdd(qc_pull(qs, b, x), 64u);
         base = (uint32_t)__shfl((int)base, 0);
-        if (base >= n) break;
-        const uint32_t e = base + (uint32_t)lane;
-        const bool act = e < n;
+        if (base >= n) {
+            if (--left == 0) break;
+            x = x + 1 == parts ? 0 : x + 1;
+            n = *qc_emit(qs, b - 1, x);
+            continue;
+        }
+        const uint32_t e = (uint32_t)x * qs.pcap + base + (uint32_t)lane;
+        const bool act = base + (uint32_t)lane < n;
         bool emit = false, fall = false;
         Ray64 nr;
         Win win;
@@ -764,7 +896,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
                 q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
             }
         }
-        const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        const uint32_t slot = q_append(qs, qout, x, b, emit, nr, path);
         bool qd = false;
         uint32_t dst = 0;
         if (act && !fall)
@@ -815,7 +947,7 @@ k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
     LaneCounts shc;
     for (;;) {
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qc_pull(qs, b) + 1, 64u);
+        if (lane == 0) base = atomicAdd(qc_sh(qs, b) + 1, 64u);  // (the record count's line, second word)
         base = (uint32_t)__shfl((int)base, 0);
         if (base >= n) break;
         const uint32_t e = base + (uint32_t)lane;
@@ -907,7 +1039,9 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
                 hit = win.tri >= 0;
             }
         }
-        const uint32_t slot = q_append(qs, qout, qc_emit(qs, b), emit, nr, path);
+        // (into the partition the ray came from: its capacity covers it)
+        const int x = k >= n ? 0 : b == 0 ? q_primary_part(qs, fp, path) : (int)(e / qs.pcap);
+        const uint32_t slot = q_append_lane(qs, qout, x, b, emit, nr, path);
         if (b == 0) wave_add<1>(fp.hit_count, hit);
         bool qd = false;
         uint32_t dst = 0;

@@ -1393,9 +1393,35 @@ int queued_shadow_mode(const RtDevScene& sc, bool shadow, uint64_t paths) {
     return 1;
 }
 
-hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
+// Packed primary segments of the queued pipeline through the packet kernel
+// (RT_QP_PACKET=0: k_q_primary's wave walk; read per call): every sample of
+// a pose fits one launch (spp <= RT_MAX_BATCH) and the launch state is there.
+bool packet_primaries(const RtFrameParams& fp, const RtLaunchAux& aux) {
+    const char* e = getenv("RT_QP_PACKET");
+    if (e && e[0] == '0') return false;
+    // (the packed tile is (8 / n) x (8 / n) pixels of spp = n x n samples)
+    const bool square = fp.spp == 4 || fp.spp == 16;
+    return square && fp.spp <= RT_MAX_BATCH && aux.tile_ctr && aux.pool && aux.pgrid > 0;
+}
+
+hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs_,
                           uint32_t frame, int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev) {
     if (fp.W <= 0 || fp.nrows <= 0) return hipSuccess;
+    // one partition, or RT_QPARTS when the packet kernel deals the primaries
+    // (its tiles' XCD queues: PathQs)
+    PathQs qs = qs_;
+    qs.parts = 1;
+    qs.pcap = qs.cap;
+    qs.ptile = qs.ptiles_x = 1;
+    const bool qpacket = sc.width == 8 && fp.pack && paths_primary_wave(sc) && packet_primaries(fp, aux);
+    if (qpacket) {
+        const RtQParts p = rt_qparts(fp.W, fp.nrows, fp.spp);
+        if (p.entries > qs.cap) return hipErrorInvalidValue;
+        qs.parts = RT_QPARTS;
+        qs.pcap = p.pcap;
+        qs.ptile = p.ptile;
+        qs.ptiles_x = p.ptiles_x;
+    }
     const uint64_t paths = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)fp.spp;
     if (fp.nframes != 1 || fp.spp < 1 || bounces < 0 || bounces > 64 || !aux.spill || aux.grid <= 0 || !qs.ctl ||
         paths > qs.cap || aux.spill_cap + RT_Q_STACK < sc.stack_bound || aux.spill_cap + kPathStack < sc.stack_bound ||
@@ -1421,7 +1447,28 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
             launch_q_segments<4>(sc, fp, aux, qs, frame, bounces, sh, false, s);
             break;
         case 8:
-            if (fp.pack && paths_primary_wave(sc)) {
+            if (qpacket) {
+                // the packed packet walk (k_trace_packet<…, PATHS>): the
+                // headline kernel's walk and resolve, the path's primary
+                // vertex as its epilogue (queue_paths.h q_primary_vertex);
+                // one pose of spp sample frames, its work-queue block zeroed
+                // here and left zeroed by the kernel's exit (packet_exit)
+                RtFrameParams fq = fp;
+                fq.nframes = fp.spp;
+                fq.spp_n = fp.spp == 16 ? 4 : 2;
+                RtLaunchAux aq = aux;
+                aq.self_fix = 1;
+                aq.job_src = nullptr;
+                e = hipMemsetAsync(aux.tile_ctr, 0, RT_QUEUE_WORDS * sizeof(uint32_t), s);
+                if (e != hipSuccess) return e;
+                const dim3 qgrid((unsigned)aux.pgrid), qblk(64 * kPacketWaves);
+                if (count)
+                    hipLaunchKernelGGL((k_trace_packet<8, kPacketStack, kCandidates, true, true, true, false, true>), qgrid,
+                                       qblk, 0, s, PacketArgs{sc, fq, aq, qs, frame, bounces});
+                else
+                    hipLaunchKernelGGL((k_trace_packet<8, kPacketStack, kCandidates, false, true, true, false, true>),
+                                       qgrid, qblk, 0, s, PacketArgs{sc, fq, aq, qs, frame, bounces});
+            } else if (fp.pack && paths_primary_wave(sc)) {
                 if (count)
                     hipLaunchKernelGGL((k_q_primary<8, 1, true, true, true>), pgrid, blk, 0, s, sc, fp, aux, qs, frame, bounces);
                 else

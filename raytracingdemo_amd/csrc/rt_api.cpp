@@ -1339,7 +1339,9 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             // the queued workspace (256 B per path: 34 GB for a c5 pose);
             // when the library chose the queue itself and the workspace
             // cannot be had, the megakernel renders the same bits with none
-            const uint64_t P = (uint64_t)cam->width * (uint64_t)nrows * (uint64_t)spp;
+            uint64_t P = (uint64_t)cam->width * (uint64_t)nrows * (uint64_t)spp;
+            if (spp == 4 || spp == 16)  // (room for the partitioned layout of the packet primaries)
+                P = std::max(P, rt_qparts(cam->width, nrows, spp).entries);
             try {
                 qs = ensure_pq(*r, P);
             } catch (const rt::Error&) {

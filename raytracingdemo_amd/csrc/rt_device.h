@@ -262,6 +262,14 @@ struct PathQs {
     RT_G uint32_t* fb;     // fall-back lists, [2][cap]: queue slots for the exact per-lane traversal
     RT_G uint32_t* ctl;    // control words (queue_paths.h qc_*), zeroed per pose
     uint32_t cap;          // paths (entries per queue)
+    // Each queue is `parts` partitions of `pcap` entries (parts * pcap <=
+    // cap), each with its own append and pull counters: partition x holds
+    // the rays of the primary tiles of XCD queue x and everything they
+    // bounce into, so no counter is shared by the whole chip (one word takes
+    // ~88 atomics per us: 2.07 M primary tiles on one counter alone took
+    // 23.7 ms per pose).  parts = 1: one queue (k_q_primary's primaries).
+    uint32_t parts, pcap;
+    uint32_t ptile, ptiles_x;  // parts > 1: the primary tiles' edge in pixels and tiles per row
     // occlusion-ray queue (queued shadows): records {p (3 doubles), tri | dst}
     // as the segment kernel appends them ([0]) and binned by their direction
     // from the light ([1]); per-block bin counts of the binning passes
@@ -269,7 +277,26 @@ struct PathQs {
     RT_G uint32_t* bhist;  // [bins][sh_blocks]
     uint32_t sh_blocks;
 };
-#define RT_QC_WORDS(bounces) (4 * ((bounces) + 1) * 16)
+#define RT_QPARTS RT_QUEUES
+#define RT_QC_LINES (2 * RT_QPARTS + 2)
+#define RT_QC_WORDS(bounces) (RT_QC_LINES * ((bounces) + 1) * 16)
+// The partitioned layout of a pose of W x nrows pixels at spp = n x n samples
+// (n = 2 or 4): the packed primary tiles (8 / n pixels square, 64 samples)
+// dealt round-robin to the RT_QPARTS partitions, each with room for its
+// tiles' samples; `entries` = the queue length it needs (>= the paths).
+struct RtQParts {
+    uint32_t pcap, ptile, ptiles_x;
+    uint64_t entries;
+};
+static inline RT_HD RtQParts rt_qparts(int W, int nrows, int spp) {
+    RtQParts p{};
+    p.ptile = spp == 16 ? 2u : 4u;
+    p.ptiles_x = ((uint32_t)W + p.ptile - 1) / p.ptile;
+    const uint64_t T = (uint64_t)p.ptiles_x * (((uint32_t)nrows + p.ptile - 1) / p.ptile);
+    p.pcap = (uint32_t)((T + RT_QPARTS - 1) / RT_QPARTS * 64);
+    p.entries = (uint64_t)p.pcap * RT_QPARTS;
+    return p;
+}
 // occlusion-ray order: a cube map around the light, 512 x 512 cells per face
 // in Morton order (21-bit keys), counting-sorted in two passes of RT_SH_BITS
 // bits (RT_SH_BINS bins, per-block counts of RT_SH_BLOCKS blocks)

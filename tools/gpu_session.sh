@@ -120,10 +120,10 @@ for s in $STEPS; do
                RT_BENCH_SHIP_SIM=2 RT_BENCH_SIDE_SLOT=0 run ship8_full$rep 300 python bench.py --no-cpu --no-dropin \
                    --steps 40 --shard-of 8 || exit 1; done
                run shard8 300 python bench.py --no-cpu --no-dropin --steps 40 --shard-of 8 ;;
-        qpdiag) # k_q_primary phase timing: the shipped kernel, then the walk only and walk + resolve builds
+        qpdiag) # path-primary phase timing: the shipped kernel, then timing builds QPDIAG_VARIANTS
                run qpd_base 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/qpd_base -o qp \
                    -- python bench.py --paths --steps 2 --warmup 1 --no-cpu || exit 1
-               for v in qpdiag1 qpdiag2; do
+               for v in ${QPDIAG_VARIANTS:-qpdiag1 qpdiag2}; do
                    RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_$v.so run qpd_$v 300 rocprofv3 --kernel-trace \
                        --stats --output-format csv -d gpurun_out/qpd_$v -o qp -- python bench.py --paths --steps 2 \
                        --warmup 1 --no-cpu || exit 1; done ;;

@@ -89,7 +89,8 @@ def parse():
     p.add_argument("--bounces", type=int, default=4, help="paths: secondary bounces per sample")
     p.add_argument("--pipeline", default=os.environ.get("RT_PATHS", "auto"), choices=["auto", "queue", "mega"],
                    help="paths: the queued tracer (compacted per-segment queues) or the megakernel (sets RT_PATHS "
-                        "for the library); auto: the library's default (queued with occlusion rays, else mega)")
+                        "for the library); auto: the library's default (queued with occlusion rays or packet primaries "
+                        "(8-wide tree, spp 4 or 16), else mega)")
     p.add_argument("--no-shadow", action="store_true",
                    help="paths: no occlusion rays toward the head-light at the bounce vertices (RT_FLAG_SHADOW)")
     p.add_argument("--scene", default="sponza", choices=["sponza", "armadillo"],
@@ -266,17 +267,18 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
     shadow = not a.no_shadow
     if a.pipeline == "auto":  # the library's default (rt_api.cpp path_pipe)
         os.environ.pop("RT_PATHS", None)
-        a.pipeline = "queue" if shadow else "mega"
+        a.pipeline = "queue" if shadow or (S in (4, 16) and a.k == 8) else "mega"
     else:
         os.environ["RT_PATHS"] = a.pipeline  # (read by the library per call)
     queued = a.pipeline == "queue"
     # occlusion-ray mode (render.hip queued_shadow_mode): per lane where the
-    # vertex is shaded (the megakernel; the queued pipeline's default), or
-    # queued: from records per lane (RT_SHADOW_RAYS=rec) or sorted and walked
-    # by the wave (RT_SHADOW_RAYS=bin)
+    # vertex is shaded (the megakernel; the queued pipeline with
+    # RT_SHADOW_RAYS=lane), or queued: from records per lane
+    # (RT_SHADOW_RAYS=rec) or sorted and walked by the wave (the queued
+    # pipeline's default)
     sh_env = os.environ.get("RT_SHADOW_RAYS", "")[:1]
     shadow_kind = None if not shadow else ("records" if queued and sh_env == "r" else
-                                           "binned" if queued and sh_env == "b" else "inline")
+                                           "inline" if not queued or sh_env == "l" else "binned")
     path = rt.CameraPath(rt.scene_center(tris), 36)
     rows = rows_per_rank(H, world, band=1)  # the paths kernel takes single interleaved rows
     my_rows = len(shard_rows(rank, world, H, band=1))

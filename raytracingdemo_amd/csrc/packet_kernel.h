@@ -1256,8 +1256,9 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     // tile scheduling: one queue per XCD (blocks are dealt to the 8 XCDs
-    // round-robin, so block b's XCD is b % 8): queue x hands out tiles
-    // x, x + 8, x + 16, ...; every queue is drained by the blocks b = x mod 8.
+    // round-robin, so block b's XCD is b % 8): slot s of queue x is tile
+    // queue_tile(x, s) — runs of RT_TILE_RUN consecutive tiles, every 8th
+    // run; every queue is drained by the blocks b = x mod 8.
     const uint32_t xq = blockIdx.x % RT_QUEUES;
     bool first = true;
     // one atomic claims `claim` consecutive slots of the queue: 2 when there
@@ -1283,30 +1284,31 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
         const int tiles_f = tiles_x * ((nrows + ts - 1) / ts);  // tiles per frame (pose when packed)
         const int tiles = tiles_f * (pack ? kword(&A->fp.nframes) / spp : kword(&A->fp.nframes));
         claim = tiles >= 64 * (int)(gridDim.x * kPacketWaves) ? 2 : 1;
-        int t = 0;
+        int s = 0;
         bool claimed = false;
         if (pend >= 0) {  // the rest of the last claim
-            t = pend;
-            pend = (++pend_n < claim) ? pend + RT_QUEUES : -1;
+            s = pend;
+            pend = (++pend_n < claim) ? pend + 1 : -1;
         } else if (first) {
             // a wave's first tile is its own slot in the queue (no atomic: the
             // whole grid starting at once would serialise on the 8 counters
             // for ~10 us); the counter hands out the slots after the XCD's waves
             first = false;
-            t = (int)(xq + RT_QUEUES * ((blockIdx.x / RT_QUEUES) * kPacketWaves + wv));
+            s = (int)((blockIdx.x / RT_QUEUES) * kPacketWaves + wv);
         } else {
             claimed = true;
             if (lane == 0) {
                 const uint32_t nwq = kPacketWaves * ((gridDim.x + RT_QUEUES - 1 - xq) / RT_QUEUES);  // waves of queue xq
-                t = (int)(xq + RT_QUEUES * (nwq + (uint32_t)claim * atomicAdd(kload(&A->aux.tile_ctr) +
-                                                                                  xq * RT_QUEUE_STRIDE, 1u)));
+                s = (int)(nwq + (uint32_t)claim * atomicAdd(kload(&A->aux.tile_ctr) + xq * RT_QUEUE_STRIDE, 1u));
             }
         }
-        const int tile = __builtin_amdgcn_readlane(t, 0);  // wave-uniform: a uniform loop exit
-        if (claimed && claim > 1) {  // the claim's further slots follow, RT_QUEUES tiles apart
-            pend = tile + RT_QUEUES;
+        const int slot = __builtin_amdgcn_readlane(s, 0);  // wave-uniform: a uniform loop exit
+        if (claimed && claim > 1) {  // the claim's further slots
+            pend = slot + 1;
             pend_n = 1;
         }
+        // (increasing with the slot: the first tile past the end ends the queue)
+        const int tile = ((slot / RT_TILE_RUN) * RT_QUEUES + (int)xq) * RT_TILE_RUN + slot % RT_TILE_RUN;
         if (tile >= tiles) {
             if constexpr (JOB)
                 while (job) job = side_copy(A, lane, xq);  // the job's rows the tiles left

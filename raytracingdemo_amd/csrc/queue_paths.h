@@ -49,9 +49,10 @@
 //               (segment b + 1's input)
 //   pull(b, x)  pull cursor of segment b's kernel in partition x (k_q_primary:
 //               its tile cursor)
+//   sh(b, x)    occlusion records segment b appended to partition x of the
+//               record array (queued shadows)
+//   shpull(b,x) the occlusion kernels' pull cursor in part x of their input
 //   fb(b)       fall-back entries segment b listed
-//   sh(b)       occlusion records segment b appended (queued shadows); its
-//               second word: the occlusion kernels' pull cursor
 #define RT_QC_STRIDE 16
 __device__ __forceinline__ RT_G uint32_t* qc_emit(const PathQs& q, int b, int x) {
     return q.ctl + (RT_QC_LINES * b + x) * RT_QC_STRIDE;
@@ -59,11 +60,63 @@ __device__ __forceinline__ RT_G uint32_t* qc_emit(const PathQs& q, int b, int x)
 __device__ __forceinline__ RT_G uint32_t* qc_pull(const PathQs& q, int b, int x) {
     return q.ctl + (RT_QC_LINES * b + RT_QPARTS + x) * RT_QC_STRIDE;
 }
-__device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) {
-    return q.ctl + (RT_QC_LINES * b + 2 * RT_QPARTS) * RT_QC_STRIDE;
+__device__ __forceinline__ RT_G uint32_t* qc_sh(const PathQs& q, int b, int x) {
+    return q.ctl + (RT_QC_LINES * b + 2 * RT_QPARTS + x) * RT_QC_STRIDE;
 }
-__device__ __forceinline__ RT_G uint32_t* qc_sh(const PathQs& q, int b) {
-    return q.ctl + (RT_QC_LINES * b + 2 * RT_QPARTS + 1) * RT_QC_STRIDE;
+__device__ __forceinline__ RT_G uint32_t* qc_shpull(const PathQs& q, int b, int x) {
+    return q.ctl + (RT_QC_LINES * b + 3 * RT_QPARTS + x) * RT_QC_STRIDE;
+}
+__device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) {
+    return q.ctl + (RT_QC_LINES * b + 4 * RT_QPARTS) * RT_QC_STRIDE;
+}
+// Occlusion records of segment b: partition x holds entries [x pcap, x pcap +
+// *qc_sh(b, x)) of srec[0] as appended; sorted (binned mode) they are one
+// run of sh_total records.
+__device__ __forceinline__ uint32_t sh_total(const PathQs& q, int b) {
+    uint32_t n = 0;
+    for (int x = 0; x < (int)q.parts; x++) n += *qc_sh(q, b, x);
+    return n;
+}
+// Range [lo, hi) of part x of `parts` over an input of records: partitioned
+// (the appended records: partition x) or one run of n (sorted: its x-th
+// slice).
+__device__ __forceinline__ void sh_part(const PathQs& q, int b, int x, bool sorted, uint32_t n, uint32_t& lo,
+                                        uint32_t& hi) {
+    if (sorted) {
+        lo = (uint32_t)((uint64_t)n * (uint32_t)x / q.parts);
+        hi = (uint32_t)((uint64_t)n * (uint32_t)(x + 1) / q.parts);
+    } else {
+        lo = (uint32_t)x * q.pcap;
+        hi = lo + *qc_sh(q, b, x);
+    }
+}
+// A wave's next 64 records of an occlusion kernel's input: from its part x
+// (its XCD's: blocks are dealt round-robin), then the others in turn; false
+// when every part is drained.  e0: the first record of the 64, hi: the end of
+// its part.
+struct ShPull {
+    int x, left;
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ void sh_pull_begin(const PathQs& q, int b, bool sorted, uint32_t n, ShPull& p) {
+    p.x = (int)(blockIdx.x % q.parts);
+    p.left = (int)q.parts;
+    sh_part(q, b, p.x, sorted, n, p.lo, p.hi);
+}
+__device__ __forceinline__ bool sh_pull(const PathQs& q, int b, bool sorted, uint32_t n, ShPull& p, uint32_t& e0) {
+    const int lane = (int)(threadIdx.x & 63);
+    for (;;) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(qc_shpull(q, b, p.x), 64u);
+        base = (uint32_t)__shfl((int)base, 0);
+        if (p.lo + base < p.hi) {
+            e0 = p.lo + base;
+            return true;
+        }
+        if (--p.left == 0) return false;
+        p.x = p.x + 1 == (int)q.parts ? 0 : p.x + 1;
+        sh_part(q, b, p.x, sorted, n, p.lo, p.hi);
+    }
 }
 
 // Queue entry e of queue k: 10 doubles {o, d, L, path | pad}.
@@ -132,12 +185,13 @@ __device__ __forceinline__ uint32_t q_append_lane(const PathQs& q, int k, int x,
 }
 
 // The partition of a primary path (parts > 1: its tile's XCD queue,
-// k_trace_packet's tiles of ptile x ptile pixels dealt to queue t % parts).
+// k_trace_packet's tiles of ptile x ptile pixels dealt to queue
+// (t / RT_TILE_RUN) % parts).
 __device__ __forceinline__ int q_primary_part(const PathQs& q, const RtFrameParams& fp, uint32_t path) {
     if (q.parts <= 1) return 0;
     const uint32_t pix = path / (uint32_t)fp.spp;
     const uint32_t i = pix % (uint32_t)fp.W, r = pix / (uint32_t)fp.W;
-    return (int)(((r / q.ptile) * q.ptiles_x + i / q.ptile) % q.parts);
+    return (int)((((r / q.ptile) * q.ptiles_x + i / q.ptile) / RT_TILE_RUN) % q.parts);
 }
 
 // Sample index of a path -> its pixel's image coordinates and the hash seed.
@@ -225,19 +279,31 @@ __device__ __forceinline__ RT_G double* q_dst(const PathQs& qs, uint32_t dst) {
     return qs.Lfin + 3 * (size_t)dst;
 }
 
-// Appends the lanes' occlusion records {p, tri, dst} to srec[0] (one atomic
-// per wave); every lane of the wave calls it.
-__device__ __forceinline__ void q_shadow_append(const PathQs& qs, int b, bool queue, double px, double py, double pz,
-                                                int32_t tri, uint32_t dst) {
+// Appends the lanes' occlusion records {p, tri, dst} to partition x of
+// srec[0] (the partition of the segment's input ray: its capacity covers
+// them; one atomic per wave); every lane of the wave calls it, with one x.
+__device__ __forceinline__ void q_shadow_append(const PathQs& qs, int b, int x, bool queue, double px, double py,
+                                                double pz, int32_t tri, uint32_t dst) {
     const uint64_t em = __ballot(queue);
     if (em == 0) return;
     const int lane = (int)(threadIdx.x & 63);
     const int leader = __builtin_ctzll(em);
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(qc_sh(qs, b), (uint32_t)__builtin_popcountll(em));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    if (lane == leader) base = atomicAdd(qc_sh(qs, b, x), (uint32_t)__builtin_popcountll(em));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader) + (uint32_t)x * qs.pcap;
     if (!queue) return;
     RT_G double* r = qs.srec[0] + 4 * (size_t)(base + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1ull)));
+    r[0] = px;
+    r[1] = py;
+    r[2] = pz;
+    r[3] = __longlong_as_double((long long)(((uint64_t)dst << 32) | (uint32_t)tri));
+}
+// ... for one lane (the fall-back kernel's lanes append to their own rays'
+// partitions).
+__device__ __forceinline__ void q_shadow_append_lane(const PathQs& qs, int b, int x, bool queue, double px,
+                                                     double py, double pz, int32_t tri, uint32_t dst) {
+    if (!queue) return;
+    RT_G double* r = qs.srec[0] + 4 * (size_t)(atomicAdd(qc_sh(qs, b, x), 1u) + (uint32_t)x * qs.pcap);
     r[0] = px;
     r[1] = py;
     r[2] = pz;
@@ -283,8 +349,18 @@ __device__ __forceinline__ uint32_t sh_key(const RtFrameCam& cam, double px, dou
 // is the LDS atomics', so a pass is stable only up to a block's range).  Two
 // passes (low digit, then high) order the records by key up to that fuzz:
 // neighbouring records are rays of nearly the same direction from the light.
-// Block k of RT_SH_BLOCKS takes records [k n / NB, (k+1) n / NB).
-__device__ __forceinline__ void sh_range(uint32_t n, uint32_t k, uint32_t& lo, uint32_t& hi) {
+// Block k of RT_SH_BLOCKS takes records [k n / NB, (k+1) n / NB) of the
+// sorted run (src 1), or its share of partition k % parts of the appended
+// records (src 0: RT_SH_BLOCKS / parts blocks per partition).
+__device__ __forceinline__ void sh_range(const PathQs& qs, int b, int src, uint32_t k, uint32_t& lo, uint32_t& hi) {
+    if (src == 0) {
+        const uint32_t x = k % qs.parts, j = k / qs.parts, nb = RT_SH_BLOCKS / qs.parts;
+        const uint32_t n = *qc_sh(qs, b, (int)x);
+        lo = x * qs.pcap + (uint32_t)((uint64_t)n * j / nb);
+        hi = x * qs.pcap + (uint32_t)((uint64_t)n * (j + 1) / nb);
+        return;
+    }
+    const uint32_t n = sh_total(qs, b);
     lo = (uint32_t)((uint64_t)n * k / RT_SH_BLOCKS);
     hi = (uint32_t)((uint64_t)n * (k + 1) / RT_SH_BLOCKS);
 }
@@ -294,7 +370,7 @@ __global__ void __launch_bounds__(1024) k_sh_hist(RtFrameParams fp, PathQs qs, i
     __syncthreads();
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t lo, hi;
-    sh_range(*qc_sh(qs, b), blockIdx.x, lo, hi);
+    sh_range(qs, b, src, blockIdx.x, lo, hi);
     for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
         const RT_G double* r = qs.srec[src] + 4 * (size_t)e;
         atomicAdd(&h[(sh_key(cam, r[0], r[1], r[2]) >> shift) & (RT_SH_BINS - 1)], 1u);
@@ -340,7 +416,7 @@ __global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs
     __syncthreads();
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t lo, hi;
-    sh_range(*qc_sh(qs, b), blockIdx.x, lo, hi);
+    sh_range(qs, b, src, blockIdx.x, lo, hi);
     for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
         const RT_G double* r = qs.srec[src] + 4 * (size_t)e;
         const double x = r[0], y = r[1], z = r[2], w = r[3];
@@ -521,25 +597,24 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
 #define RT_SH_WPE 6  // waves per SIMD of k_sh_walk
 #endif
 template <int W, bool COUNT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_WPE))) k_sh_walk(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_WPE))) k_sh_walk(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b, int src) {
     __shared__ uint32_t wst[4][128];  // one 128-entry node stack per wave
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const uint32_t n = *qc_sh(qs, b);
+    const uint32_t n = sh_total(qs, b);
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t* wstack = wst[tid >> 6];
     uint32_t occl = 0, cast = 0, w_nodes = 0, w_tris = 0;
-    for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qc_sh(qs, b) + 1, 64u);  // (the record count's line, second word)
-        base = (uint32_t)__shfl((int)base, 0);
-        if (base >= n) break;
-        const uint32_t e = base + (uint32_t)lane;
-        const bool act = e < n;
+    ShPull pl;
+    sh_pull_begin(qs, b, true, n, pl);
+    uint32_t e0;
+    while (sh_pull(qs, b, true, n, pl, e0)) {
+        const uint32_t e = e0 + (uint32_t)lane;
+        const bool act = e < pl.hi;
         double px = 0.0, py = 0.0, pz = 0.0;
         uint64_t td = 0;
         if (act) {
-            const RT_G double* r = qs.srec[0] + 4 * (size_t)e;  // (sorted: srec[0] -> [1] -> [0])
+            const RT_G double* r = qs.srec[src] + 4 * (size_t)e;  // (sorted: srec[0] -> [1] (-> [0]))
             px = r[0];
             py = r[1];
             pz = r[2];
@@ -902,7 +977,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         if (act && !fall)
             q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
                               sh_cast, sh_occ, qd, dst, &shc);
-        if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
+        if constexpr (SH >= 2) q_shadow_append(qs, b, x, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         wave_add<24>(fp.counters, segs);
@@ -939,19 +1014,17 @@ k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
     __shared__ uint2 lds[S][256];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const uint32_t n = *qc_sh(qs, b);
     LaneStack<S> st;
     st.attach(lds, aux, tid);
     const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t occl = 0, cast = 0;
     LaneCounts shc;
-    for (;;) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(qc_sh(qs, b) + 1, 64u);  // (the record count's line, second word)
-        base = (uint32_t)__shfl((int)base, 0);
-        if (base >= n) break;
-        const uint32_t e = base + (uint32_t)lane;
-        if (e >= n) continue;
+    ShPull pl;
+    sh_pull_begin(qs, b, false, 0, pl);
+    uint32_t e0;
+    while (sh_pull(qs, b, false, 0, pl, e0)) {
+        const uint32_t e = e0 + (uint32_t)lane;
+        if (e >= pl.hi) continue;
         const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
         const double px = r[0], py = r[1], pz = r[2];
         const bool occ = lane_occluded<W, S, W == 8 && RT_QNODES, COUNT>(sc, cam, px, py, pz, st, &shc);
@@ -1048,7 +1121,7 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
         if (k < n)
             q_light<W, S, SH, COUNT>(sc, qs, cam, b, b == 0 ? nullptr : q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit,
                               qout, slot, path, st, sh_cast, sh_occ, qd, dst, &shc);
-        if constexpr (SH >= 2) q_shadow_append(qs, b, qd, px, py, pz, win.tri, dst);
+        if constexpr (SH >= 2) q_shadow_append_lane(qs, b, x, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         if (SH == 1) {

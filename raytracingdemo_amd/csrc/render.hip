@@ -1340,13 +1340,17 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
     if constexpr (SH == 2) {
         // the segment's occlusion records: binned by direction from the light,
         // then walked 64 at a time by the wave-cooperative any-hit walk
-        for (int pass = 0; pass < 2; pass++) {  // low digit 0 -> 1, high digit 1 -> 0
-            hipLaunchKernelGGL(k_sh_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, pass * RT_SH_BITS);
+        // (RT_SH_PASSES=1, read per call: the high digit alone, 0 -> 1)
+        const char* ps = getenv("RT_SH_PASSES");
+        const int passes = ps && ps[0] == '1' ? 1 : 2;
+        for (int pass = 0; pass < passes; pass++) {  // low digit 0 -> 1, high digit 1 -> 0
+            const int shift = (passes - 1 - pass == 0 ? 1 : 0) * RT_SH_BITS;
+            hipLaunchKernelGGL(k_sh_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, shift);
             hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
-            hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, pass * RT_SH_BITS);
+            hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, shift);
         }
         static const dim3 wgrid = occupancy_grid(k_sh_walk<W, COUNT>);
-        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), wgrid, blk, 0, s, sc, fp, aux, qs, b);
+        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), wgrid, blk, 0, s, sc, fp, aux, qs, b, passes & 1);
     }
 }
 // sh: 0 no occlusion rays, 1 per lane in the segment kernel, 2 queued and binned
@@ -1376,11 +1380,12 @@ void launch_q_segments(const RtDevScene& sc, const RtFrameParams& fp, const RtLa
 }
 
 // Occlusion rays of the queued pipeline (RT_SHADOW_RAYS, read per call):
-// walked per lane inside the segment kernel where the vertex is shaded
-// (default, "lane"); "rec": queued as records, walked per lane in emission
-// order by k_sh_lane; "bin": queued, sorted by direction from the light and
-// walked by the wave (k_sh_walk; its wave stack holds kPacketStack entries,
-// deeper trees stay per lane).  Config c5: 241 / 242 / 266 ms per pose.
+// "bin" (default): queued, sorted by direction from the light and walked by
+// the wave (k_sh_walk; its wave stack holds kPacketStack entries, deeper
+// trees stay per lane); "lane": walked per lane inside the segment kernel
+// where the vertex is shaded; "rec": queued as records, walked per lane in
+// emission order by k_sh_lane.  Config c5 with partitioned counters: 201.0 /
+// 220.5 / 216.7 ms per pose (round 4, one counter per queue: 266 / 233 / 237).
 // A queued record names its destination in one word (q_light: bit 31, the
 // queue in bit 30, the slot in bits 0-29), so pools of 2^30 paths or more
 // stay per lane too.
@@ -1389,8 +1394,8 @@ int queued_shadow_mode(const RtDevScene& sc, bool shadow, uint64_t paths) {
     const char* e = getenv("RT_SHADOW_RAYS");
     if (paths >= (1ull << 30)) return 1;
     if (e && e[0] == 'r') return 3;
-    if (e && e[0] == 'b') return sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
-    return 1;
+    if (e && e[0] == 'l') return 1;
+    return sc.stack_bound > (uint32_t)kPacketStack ? 1 : 2;
 }
 
 // Packed primary segments of the queued pipeline through the packet kernel
@@ -1430,7 +1435,8 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     hipError_t e = hipMemsetAsync(qs.ctl, 0, RT_QC_WORDS(bounces) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     const bool count = fp.counters != nullptr;
-    const int sh = queued_shadow_mode(sc, shadow, paths);
+    // (a queued record's destination names a queue slot: < parts * pcap)
+    const int sh = queued_shadow_mode(sc, shadow, std::max(paths, (uint64_t)qs.parts * qs.pcap));
     if (sh == 2 && (!qs.srec[0] || !qs.srec[1] || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
     // the wave-walked primary kernel uses no per-lane stack (no spill

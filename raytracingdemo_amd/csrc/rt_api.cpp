@@ -517,20 +517,21 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
 // Path pipeline (RT_PATHS, read per call: tests switch it in-process):
 // "queue" — the queued tracer (queue_paths.h: compacted segment queues, lean
 // per-segment kernels); "mega" — the megakernel (path_kernel.h k_paths).
-// Unset: the faster of the two on config c5 — the queued tracer with
-// occlusion rays (234 vs 250 ms per pose), the megakernel without (156 vs
-// 161).  (The round-2 wavefront tracer, 1.45x slower than
-// either, was removed in round 5.)
+// Unset: the faster of the two — the queued tracer with occlusion rays
+// (config c5: 201 vs 250 ms per pose), and without them wherever its primary
+// segments go through the packet kernel (an 8-wide tree, spp 4 or 16: c5
+// 143.9 vs 157.0 ms), else the megakernel.  (The round-2
+// wavefront tracer, 1.45x slower than either, was removed in round 5.)
 enum class PathPipe { mega, queue };
 bool path_pipe_forced() {
     const char* e = std::getenv("RT_PATHS");
     return e && (e[0] == 'q' || e[0] == 'm');
 }
-PathPipe path_pipe(bool shadow) {
+PathPipe path_pipe(bool shadow, int width, int spp) {
     const char* e = std::getenv("RT_PATHS");
     if (e && e[0] == 'q') return PathPipe::queue;
     if (e && e[0] == 'm') return PathPipe::mega;
-    return shadow ? PathPipe::queue : PathPipe::mega;
+    return shadow || (width == 8 && (spp == 4 || spp == 16)) ? PathPipe::queue : PathPipe::mega;
 }
 
 void check_camera(const rt_scene* s, const rt_camera* c) {
@@ -1333,7 +1334,7 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
             tev = r->tev[r->tev_used++].data();
         }
         hipError_t e;
-        PathPipe pipe = path_pipe((flags & RT_FLAG_SHADOW) != 0);
+        PathPipe pipe = path_pipe((flags & RT_FLAG_SHADOW) != 0, (int)r->dev.width, spp);
         PathQs qs{};
         if (pipe == PathPipe::queue) {
             // the queued workspace (256 B per path: 34 GB for a c5 pose);

@@ -278,12 +278,22 @@ struct PathQs {
     uint32_t sh_blocks;
 };
 #define RT_QPARTS RT_QUEUES
-#define RT_QC_LINES (2 * RT_QPARTS + 2)
+// k_trace_packet deals its tiles to the XCD queues in runs of RT_TILE_RUN
+// consecutive tiles (tile t to queue (t / RUN) % RT_QUEUES).  Tuning knob:
+// runs of 4 (a run's 8-pixel tile rows = 96 B of rgb, three whole 32-B
+// sectors from one XCD) measured 1.49 GB of writes per headline launch
+// against 1.38 with runs of 1, and 1.69 with cached (not non-temporal)
+// outputs, at the same 4.16-4.21 ms.
+#ifndef RT_TILE_RUN
+#define RT_TILE_RUN 1
+#endif
+#define RT_QC_LINES (4 * RT_QPARTS + 1)
 #define RT_QC_WORDS(bounces) (RT_QC_LINES * ((bounces) + 1) * 16)
 // The partitioned layout of a pose of W x nrows pixels at spp = n x n samples
 // (n = 2 or 4): the packed primary tiles (8 / n pixels square, 64 samples)
-// dealt round-robin to the RT_QPARTS partitions, each with room for its
-// tiles' samples; `entries` = the queue length it needs (>= the paths).
+// dealt in runs of RT_TILE_RUN round-robin to the RT_QPARTS partitions, each
+// with room for its tiles' samples; `entries` = the queue length it needs
+// (>= the paths).
 struct RtQParts {
     uint32_t pcap, ptile, ptiles_x;
     uint64_t entries;
@@ -293,7 +303,8 @@ static inline RT_HD RtQParts rt_qparts(int W, int nrows, int spp) {
     p.ptile = spp == 16 ? 2u : 4u;
     p.ptiles_x = ((uint32_t)W + p.ptile - 1) / p.ptile;
     const uint64_t T = (uint64_t)p.ptiles_x * (((uint32_t)nrows + p.ptile - 1) / p.ptile);
-    p.pcap = (uint32_t)((T + RT_QPARTS - 1) / RT_QPARTS * 64);
+    const uint64_t runs = (T + RT_TILE_RUN - 1) / RT_TILE_RUN;
+    p.pcap = (uint32_t)((runs + RT_QPARTS - 1) / RT_QPARTS * RT_TILE_RUN * 64);
     p.entries = (uint64_t)p.pcap * RT_QPARTS;
     return p;
 }

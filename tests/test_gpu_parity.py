@@ -570,7 +570,7 @@ def test_paths_shadow_sponza_proxy_band(oracle):
 @pytest.mark.parametrize("model,spp,bounces,shadow", [("stanford-bunny.obj", 16, 4, "bin"),
                                                       ("suzanne.obj", 3, 3, "bin"), ("suzanne.obj", 3, 3, "lane"),
                                                       ("stanford-bunny.obj", 16, 4, "lane"),
-                                                      ("teapot.obj", 4, 3, "rec"),
+                                                      ("teapot.obj", 4, 3, "rec"), ("teapot.obj", 4, 3, "bin"),
                                                       ("teapot.obj", 4, 2, None), ("stanford-bunny.obj", 1, 0, None)])
 def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, shadow, monkeypatch):
     """The queued pipeline (RT_PATHS=queue, queue_paths.h: the primary segments
@@ -578,10 +578,11 @@ def test_paths_queue_matches_megakernel_and_oracle(oracle, model, spp, bounces, 
     a fall-back list for the exact per-lane traversal, and the pixel sums)
     renders the same bits as the megakernel and the oracle: packed (spp 16, 4)
     and one-sample (spp 3, 1) primary tiles, occlusion rays (RT_SHADOW_RAYS=
-    lane, the default: per lane in the segment kernel; bin: queued, sorted by
-    direction from the light and walked by the wave-cooperative any-hit walk;
+    bin, the default: queued, sorted by direction from the light and walked by
+    the wave-cooperative any-hit walk; lane: per lane in the segment kernel;
     rec: from queued records, per lane), a strided shard, and the counts of
-    segments and occlusion rays."""
+    segments and occlusion rays.  Packed spp 16 and 4 take the packet kernel's
+    primaries and the 8-way partitioned queues."""
     if shadow:
         monkeypatch.setenv("RT_SHADOW_RAYS", shadow)
     shadow = shadow is not None

@@ -223,7 +223,11 @@ def test_pmc_traffic_sums_the_queued_pipeline_per_pose(tmp_path):
     names = ["k_q_primary<8, 1, true, true, true>(", "k_q_segment<8, 8, 4, true, 1>(", "k_q_accum(",  # counting pose
              "k_q_primary<8, 1, false, true, true>(", "k_q_segment<8, 8, 4, false, 1>(", "k_sh_scatter(", "k_q_accum(",
              "k_trace_packet<8, 128, 8, false, true, false, false>(",  # not the pipeline's
-             "k_q_primary<8, 1, false, true, true>(", "k_q_segment<8, 8, 4, false, 1>(", "k_q_accum("]
+             "k_q_primary<8, 1, false, true, true>(", "k_q_segment<8, 8, 4, false, 1>(", "k_q_accum(",
+             # packet-kernel primaries: the counting one skipped, the timed one starts a pose
+             "k_trace_packet<8, 128, 8, true, true, true, false, true>(",
+             "k_trace_packet<8, 128, 8, false, true, true, false, true>(", "k_q_segment<8, 8, 5, false, 2>(",
+             "k_sh_walk<8, false>("]
     for d, n in enumerate(names):
         rows.append({"Dispatch_Id": str(d + 1), "Kernel_Name": "void (anonymous namespace)::" + n + "RtDevScene)",
                      "Counter_Name": "FETCH_SIZE", "Counter_Value": str(10.0 * (d + 1))})
@@ -233,9 +237,10 @@ def test_pmc_traffic_sums_the_queued_pipeline_per_pose(tmp_path):
         w.writeheader()
         w.writerows(rows)
     poses = pmc_traffic.per_pose(str(path))
-    assert sorted(poses) == [0, 1]
+    assert sorted(poses) == [0, 1, 2]
     assert poses[0]["FETCH_SIZE"] == 40 + 50 + 60 + 70
     assert poses[1]["FETCH_SIZE"] == 90 + 100 + 110
+    assert poses[2]["FETCH_SIZE"] == 130 + 140 + 150
     assert pmc_traffic.queue_counting("k_sh_lane<8, 8, true>(") and not pmc_traffic.queue_counting("k_sh_lane<8, 8, false>(")
 
 

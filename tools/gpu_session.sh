@@ -167,6 +167,15 @@ for s in $STEPS; do
                        python -c "import json; l=[x for x in open('gpurun_out/ovl${i}_s$sh.log') if x.startswith('{')][-1]; d=json.loads(l); print('RESULT', 'shard-of $sh', '$o', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'], d['settle_steps'])" || true
                    done
                done ;;
+        wvar)  # per variant library (and the shipped one): the headline's WRITE_SIZE per launch, then its bench
+               for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
+                   n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}
+                   RT_LIB=${v:+$PWD/$v} run wv_$n 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/wv_$n -o w \
+                       -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin || exit 1
+                   python -c "import csv,statistics,re; v=[float(r['Counter_Value']) for r in csv.DictReader(open('gpurun_out/wv_$n/w_counter_collection.csv')) if 'k_trace_packet<' in r['Kernel_Name'] and not re.search(r'k_trace_packet<\d+, \d+, \d+, true', r['Kernel_Name'])]; print('WRITE', '$n', len(v), round(statistics.mean(v)*1024/1e9, 4), 'GB/launch')"
+                   RT_LIB=${v:+$PWD/$v} run wb_$n 300 python bench.py --no-cpu --no-dropin --steps 20 || exit 1
+                   python -c "import json; l=[x for x in open('gpurun_out/wb_$n.log') if x.startswith('{')][-1]; d=json.loads(l); print('BENCH', '$n', d['value'], d['roofline']['kernel_ms_avg'])"
+               done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -20,7 +20,8 @@ upper bound for a kernel with scalar reads).  WRITE_SIZE is taken as is.
 
 Usage: tools/pmc_traffic.py FETCH_CSV WRITE_CSV KEY_FILE OUT_JSON [KERNEL [WALK_CSV]]
 (KERNEL: k_trace_packet, the default, k_paths for config c5's megakernel, or
-"queue" for the queued path tracer: every k_q_* / k_sh_* dispatch of a pose,
+"queue" for the queued path tracer: every k_q_* / k_sh_* dispatch of a pose
+and its primary segments' packet kernel (k_trace_packet<..., PATHS = true>),
 summed, per pose)
 """
 import collections
@@ -38,23 +39,33 @@ def counting(name):
     return bool(m and m.group(1) == "true")
 
 
-QUEUE = re.compile(r"k_q_|k_sh_")
+# the packet kernel's path-primary instantiation: k_trace_packet<W, SP, K,
+# COUNT, FUSED, PACK, JOB, PATHS = true>
+PACKET_PATHS = re.compile(r"k_trace_packet<\d+, \d+, \d+, (true|false), \w+, \w+, \w+, true>")
+QUEUE = re.compile(r"k_q_|k_sh_|" + PACKET_PATHS.pattern)
 
 
 def queue_counting(name):
     """The queued pipeline's COUNT instantiations (queue_paths.h):
     k_q_primary<W, S, COUNT, ..>, k_q_segment<W, S, K, COUNT, ..>,
-    k_q_fallback<W, S, COUNT, ..>, k_sh_walk<W, COUNT>, k_sh_lane<W, S, COUNT>."""
+    k_q_fallback<W, S, COUNT, ..>, k_sh_walk<W, COUNT>, k_sh_lane<W, S, COUNT>,
+    and the packet kernel's path primaries."""
     m = (re.search(r"k_q_primary<\d+, \d+, (true|false)", name) or re.search(r"k_q_segment<\d+, \d+, \d+, (true|false)", name)
          or re.search(r"k_q_fallback<\d+, \d+, (true|false)", name) or re.search(r"k_sh_walk<\d+, (true|false)", name)
-         or re.search(r"k_sh_lane<\d+, \d+, (true|false)", name))
+         or re.search(r"k_sh_lane<\d+, \d+, (true|false)", name) or PACKET_PATHS.search(name))
     return bool(m and m.group(1) == "true")
+
+
+def pose_start(name):
+    """A pose's first kernel: its primary segments (k_q_primary or the packet
+    kernel's path primaries), not the counting instantiation."""
+    return ("k_q_primary<" in name or bool(PACKET_PATHS.search(name))) and not queue_counting(name)
 
 
 def per_pose(path):
     """KERNEL "queue": the queued path tracer's kernels summed per pose.  The
     counting pose (first) is skipped: every dispatch before the first
-    non-counting k_q_primary; a pose starts at each non-counting k_q_primary."""
+    non-counting primary-segment kernel; a pose starts at each (pose_start)."""
     rows = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for r in csv.DictReader(open(path)):
@@ -67,7 +78,7 @@ def per_pose(path):
     pose = -1
     for d in sorted(rows):
         n = names[d]
-        if "k_q_primary<" in n and not queue_counting(n):
+        if pose_start(n):
             pose += 1
         if pose < 0 or queue_counting(n):
             continue

@@ -70,7 +70,7 @@ __device__ __forceinline__ RT_G uint32_t* qc_fb(const PathQs& q, int b) {
     return q.ctl + (RT_QC_LINES * b + 4 * RT_QPARTS) * RT_QC_STRIDE;
 }
 // Occlusion records of segment b: partition x holds entries [x pcap, x pcap +
-// *qc_sh(b, x)) of srec[0] as appended; sorted (binned mode) they are one
+// *qc_sh(b, x)) of srec as appended; sorted (binned mode) their pairs are one
 // run of sh_total records.
 __device__ __forceinline__ uint32_t sh_total(const PathQs& q, int b) {
     uint32_t n = 0;
@@ -279,37 +279,6 @@ __device__ __forceinline__ RT_G double* q_dst(const PathQs& qs, uint32_t dst) {
     return qs.Lfin + 3 * (size_t)dst;
 }
 
-// Appends the lanes' occlusion records {p, tri, dst} to partition x of
-// srec[0] (the partition of the segment's input ray: its capacity covers
-// them; one atomic per wave); every lane of the wave calls it, with one x.
-__device__ __forceinline__ void q_shadow_append(const PathQs& qs, int b, int x, bool queue, double px, double py,
-                                                double pz, int32_t tri, uint32_t dst) {
-    const uint64_t em = __ballot(queue);
-    if (em == 0) return;
-    const int lane = (int)(threadIdx.x & 63);
-    const int leader = __builtin_ctzll(em);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(qc_sh(qs, b, x), (uint32_t)__builtin_popcountll(em));
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader) + (uint32_t)x * qs.pcap;
-    if (!queue) return;
-    RT_G double* r = qs.srec[0] + 4 * (size_t)(base + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1ull)));
-    r[0] = px;
-    r[1] = py;
-    r[2] = pz;
-    r[3] = __longlong_as_double((long long)(((uint64_t)dst << 32) | (uint32_t)tri));
-}
-// ... for one lane (the fall-back kernel's lanes append to their own rays'
-// partitions).
-__device__ __forceinline__ void q_shadow_append_lane(const PathQs& qs, int b, int x, bool queue, double px,
-                                                     double py, double pz, int32_t tri, uint32_t dst) {
-    if (!queue) return;
-    RT_G double* r = qs.srec[0] + 4 * (size_t)(atomicAdd(qc_sh(qs, b, x), 1u) + (uint32_t)x * qs.pcap);
-    r[0] = px;
-    r[1] = py;
-    r[2] = pz;
-    r[3] = __longlong_as_double((long long)(((uint64_t)dst << 32) | (uint32_t)tri));
-}
-
 // Sort key of an occlusion ray: the cube-map cell of its direction from the
 // light — face (3 bits) over the Morton code of the cell (u, v) on the face
 // (RT_SH_CELLS^2 cells, 0.18 degrees).  Only the order of the occlusion pass
@@ -343,17 +312,55 @@ __device__ __forceinline__ uint32_t sh_key(const RtFrameCam& cam, double px, dou
     return (face << 18) | morton9((uint32_t)iu) | (morton9((uint32_t)iv) << 1);
 }
 
+// Occlusion record k {p, tri, dst} and its sort key.
+__device__ __forceinline__ void q_shadow_store(const PathQs& qs, const RtFrameCam& cam, uint32_t k, double px,
+                                               double py, double pz, int32_t tri, uint32_t dst) {
+    RT_G double* r = qs.srec + 4 * (size_t)k;
+    r[0] = px;
+    r[1] = py;
+    r[2] = pz;
+    r[3] = __longlong_as_double((long long)(((uint64_t)dst << 32) | (uint32_t)tri));
+    qs.skey[k] = sh_key(cam, px, py, pz);
+}
+// Appends the lanes' occlusion records to partition x of srec (the partition
+// of the segment's input ray: its capacity covers them; one atomic per wave);
+// every lane of the wave calls it, with one x.
+__device__ __forceinline__ void q_shadow_append(const PathQs& qs, const RtFrameCam& cam, int b, int x, bool queue,
+                                                double px, double py, double pz, int32_t tri, uint32_t dst) {
+    const uint64_t em = __ballot(queue);
+    if (em == 0) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __builtin_ctzll(em);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(qc_sh(qs, b, x), (uint32_t)__builtin_popcountll(em));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader) + (uint32_t)x * qs.pcap;
+    if (!queue) return;
+    q_shadow_store(qs, cam, base + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1ull)), px, py, pz, tri,
+                   dst);
+}
+// ... for one lane (the fall-back kernel's lanes append to their own rays'
+// partitions).
+__device__ __forceinline__ void q_shadow_append_lane(const PathQs& qs, const RtFrameCam& cam, int b, int x,
+                                                     bool queue, double px, double py, double pz, int32_t tri,
+                                                     uint32_t dst) {
+    if (!queue) return;
+    q_shadow_store(qs, cam, atomicAdd(qc_sh(qs, b, x), 1u) + (uint32_t)x * qs.pcap, px, py, pz, tri, dst);
+}
+
 // Counting-sort pass over segment b's occlusion records, digit (key >> shift)
-// mod RT_SH_BINS, from srec[src] to srec[1 - src]: per-block LDS histograms,
-// one scan, then each block scatters its records (their order inside a block
-// is the LDS atomics', so a pass is stable only up to a block's range).  Two
-// passes (low digit, then high) order the records by key up to that fuzz:
-// neighbouring records are rays of nearly the same direction from the light.
-// Block k of RT_SH_BLOCKS takes records [k n / NB, (k+1) n / NB) of the
-// sorted run (src 1), or its share of partition k % parts of the appended
-// records (src 0: RT_SH_BLOCKS / parts blocks per partition).
-__device__ __forceinline__ void sh_range(const PathQs& qs, int b, int src, uint32_t k, uint32_t& lo, uint32_t& hi) {
-    if (src == 0) {
+// mod 2^BITS: pass 0 reads the appended records' keys (skey) and writes
+// (key, record) pairs to spair[0], pass 1 reorders spair[0] into spair[1];
+// per-block LDS histograms, one scan, then each block scatters its pairs
+// (their order inside a block is the LDS atomics', so a pass is stable only
+// up to a block's range).  Two passes (low digit, then high) order the
+// records by key up to that fuzz: neighbouring pairs are rays of nearly the
+// same direction from the light.  Only 4-8 B move per record and pass; the
+// occlusion walk gathers the 32-B records through the pairs.
+// Block k of RT_SH_BLOCKS takes its share of partition k % parts of the
+// appended records (pass 0: RT_SH_BLOCKS / parts blocks per partition), or
+// pairs [k n / NB, (k+1) n / NB) of the sorted run (pass 1).
+__device__ __forceinline__ void sh_range(const PathQs& qs, int b, int pass, uint32_t k, uint32_t& lo, uint32_t& hi) {
+    if (pass == 0) {
         const uint32_t x = k % qs.parts, j = k / qs.parts, nb = RT_SH_BLOCKS / qs.parts;
         const uint32_t n = *qc_sh(qs, b, (int)x);
         lo = x * qs.pcap + (uint32_t)((uint64_t)n * j / nb);
@@ -364,24 +371,32 @@ __device__ __forceinline__ void sh_range(const PathQs& qs, int b, int src, uint3
     lo = (uint32_t)((uint64_t)n * k / RT_SH_BLOCKS);
     hi = (uint32_t)((uint64_t)n * (k + 1) / RT_SH_BLOCKS);
 }
-__global__ void __launch_bounds__(1024) k_sh_hist(RtFrameParams fp, PathQs qs, int b, int src, int shift) {
-    __shared__ uint32_t h[RT_SH_BINS];
-    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) h[i] = 0;
+// Sorted pairs {key, record} of pass p.
+__device__ __forceinline__ RT_G uint2* sh_pairs(const PathQs& qs, int p) {
+    return reinterpret_cast<RT_G uint2*>(qs.spair[p]);
+}
+// The pass's input element e: its key and record.
+__device__ __forceinline__ uint2 sh_input(const PathQs& qs, int pass, uint32_t e) {
+    return pass == 0 ? make_uint2(qs.skey[e], e) : sh_pairs(qs, 0)[e];
+}
+template <int BITS>
+__global__ void __launch_bounds__(1024) k_sh_hist(PathQs qs, int b, int pass, int shift) {
+    constexpr uint32_t BINS = 1u << BITS;
+    __shared__ uint32_t h[BINS];
+    for (uint32_t i = threadIdx.x; i < BINS; i += 1024) h[i] = 0;
     __syncthreads();
-    const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t lo, hi;
-    sh_range(qs, b, src, blockIdx.x, lo, hi);
-    for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
-        const RT_G double* r = qs.srec[src] + 4 * (size_t)e;
-        atomicAdd(&h[(sh_key(cam, r[0], r[1], r[2]) >> shift) & (RT_SH_BINS - 1)], 1u);
-    }
+    sh_range(qs, b, pass, blockIdx.x, lo, hi);
+    for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024)
+        atomicAdd(&h[(sh_input(qs, pass, e).x >> shift) & (BINS - 1)], 1u);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x] = h[i];
+    for (uint32_t i = threadIdx.x; i < BINS; i += 1024) qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x] = h[i];
 }
 // Exclusive scan of bhist in place, bin-major (one block: each thread scans a
 // contiguous run, then the runs' totals are scanned in LDS).
+template <int BITS>
 __global__ void __launch_bounds__(1024) k_sh_scan(PathQs qs) {
-    constexpr uint32_t N = RT_SH_BINS * RT_SH_BLOCKS, R = N / 1024;
+    constexpr uint32_t N = (1u << BITS) * RT_SH_BLOCKS, R = N / 1024;
     static_assert(N % 1024 == 0 && R % 4 == 0, "scan runs of whole uint4s");
     __shared__ uint32_t part[1024];
     RT_G uint4* run = reinterpret_cast<RT_G uint4*>(qs.bhist + (size_t)threadIdx.x * R);
@@ -410,22 +425,18 @@ __global__ void __launch_bounds__(1024) k_sh_scan(PathQs qs) {
         run[k] = v;
     }
 }
-__global__ void __launch_bounds__(1024) k_sh_scatter(RtFrameParams fp, PathQs qs, int b, int src, int shift) {
-    __shared__ uint32_t cur[RT_SH_BINS];
-    for (uint32_t i = threadIdx.x; i < RT_SH_BINS; i += 1024) cur[i] = qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x];
+template <int BITS>
+__global__ void __launch_bounds__(1024) k_sh_scatter(PathQs qs, int b, int pass, int shift) {
+    constexpr uint32_t BINS = 1u << BITS;
+    __shared__ uint32_t cur[BINS];
+    for (uint32_t i = threadIdx.x; i < BINS; i += 1024) cur[i] = qs.bhist[(size_t)i * RT_SH_BLOCKS + blockIdx.x];
     __syncthreads();
-    const RtFrameCam cam = frame_cam(fp, 0);
     uint32_t lo, hi;
-    sh_range(qs, b, src, blockIdx.x, lo, hi);
+    sh_range(qs, b, pass, blockIdx.x, lo, hi);
+    RT_G uint2* const out = sh_pairs(qs, pass);
     for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
-        const RT_G double* r = qs.srec[src] + 4 * (size_t)e;
-        const double x = r[0], y = r[1], z = r[2], w = r[3];
-        const uint32_t d = (sh_key(cam, x, y, z) >> shift) & (RT_SH_BINS - 1);
-        RT_G double* o = qs.srec[1 - src] + 4 * (size_t)atomicAdd(&cur[d], 1u);
-        o[0] = x;
-        o[1] = y;
-        o[2] = z;
-        o[3] = w;
+        const uint2 v = sh_input(qs, pass, e);
+        out[atomicAdd(&cur[(v.x >> shift) & (BINS - 1)], 1u)] = v;
     }
 }
 
@@ -614,7 +625,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_
         double px = 0.0, py = 0.0, pz = 0.0;
         uint64_t td = 0;
         if (act) {
-            const RT_G double* r = qs.srec[src] + 4 * (size_t)e;  // (sorted: srec[0] -> [1] (-> [0]))
+            const RT_G double* r = qs.srec + 4 * (size_t)sh_pairs(qs, src)[e].y;  // (the sorted pairs' record)
             px = r[0];
             py = r[1];
             pz = r[2];
@@ -977,7 +988,7 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
         if (act && !fall)
             q_light<W, S, SH, COUNT>(sc, qs, cam, b, q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit, qout, slot, path, st,
                               sh_cast, sh_occ, qd, dst, &shc);
-        if constexpr (SH >= 2) q_shadow_append(qs, b, x, qd, px, py, pz, win.tri, dst);
+        if constexpr (SH >= 2) q_shadow_append(qs, cam, b, x, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         wave_add<24>(fp.counters, segs);
@@ -1025,7 +1036,7 @@ k_sh_lane(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b) {
     while (sh_pull(qs, b, false, 0, pl, e0)) {
         const uint32_t e = e0 + (uint32_t)lane;
         if (e >= pl.hi) continue;
-        const RT_G double* r = qs.srec[0] + 4 * (size_t)e;
+        const RT_G double* r = qs.srec + 4 * (size_t)e;
         const double px = r[0], py = r[1], pz = r[2];
         const bool occ = lane_occluded<W, S, W == 8 && RT_QNODES, COUNT>(sc, cam, px, py, pz, st, &shc);
         cast++;
@@ -1121,7 +1132,7 @@ __global__ void __launch_bounds__(256) k_q_fallback(RtDevScene sc, RtFrameParams
         if (k < n)
             q_light<W, S, SH, COUNT>(sc, qs, cam, b, b == 0 ? nullptr : q_entry(qs, qin, e) + 6, win.tri, px, py, pz, emit,
                               qout, slot, path, st, sh_cast, sh_occ, qd, dst, &shc);
-        if constexpr (SH >= 2) q_shadow_append_lane(qs, b, x, qd, px, py, pz, win.tri, dst);
+        if constexpr (SH >= 2) q_shadow_append_lane(qs, cam, b, x, qd, px, py, pz, win.tri, dst);
     }
     if (fp.counters) {
         if (SH == 1) {

@@ -1340,17 +1340,24 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
     if constexpr (SH == 2) {
         // the segment's occlusion records: binned by direction from the light,
         // then walked 64 at a time by the wave-cooperative any-hit walk
-        // (RT_SH_PASSES=1, read per call: the high digit alone, 0 -> 1)
+        // (RT_SH_PASSES=1, read per call: one pass over the top RT_SH_BITS1
+        // bits of the key, 0 -> 1)
         const char* ps = getenv("RT_SH_PASSES");
         const int passes = ps && ps[0] == '1' ? 1 : 2;
-        for (int pass = 0; pass < passes; pass++) {  // low digit 0 -> 1, high digit 1 -> 0
-            const int shift = (passes - 1 - pass == 0 ? 1 : 0) * RT_SH_BITS;
-            hipLaunchKernelGGL(k_sh_hist, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, shift);
-            hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, qs);
-            hipLaunchKernelGGL(k_sh_scatter, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, fp, qs, b, pass, shift);
+        if (passes == 1) {
+            constexpr int shift = RT_SH_KEY_BITS - RT_SH_BITS1;
+            hipLaunchKernelGGL(k_sh_hist<RT_SH_BITS1>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, 0, shift);
+            hipLaunchKernelGGL(k_sh_scan<RT_SH_BITS1>, dim3(1), dim3(1024), 0, s, qs);
+            hipLaunchKernelGGL(k_sh_scatter<RT_SH_BITS1>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, 0, shift);
+        }
+        for (int pass = 0; pass < passes && passes == 2; pass++) {  // low digit -> spair[0], high -> spair[1]
+            const int shift = pass * RT_SH_BITS;
+            hipLaunchKernelGGL(k_sh_hist<RT_SH_BITS>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, pass, shift);
+            hipLaunchKernelGGL(k_sh_scan<RT_SH_BITS>, dim3(1), dim3(1024), 0, s, qs);
+            hipLaunchKernelGGL(k_sh_scatter<RT_SH_BITS>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, pass, shift);
         }
         static const dim3 wgrid = occupancy_grid(k_sh_walk<W, COUNT>);
-        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), wgrid, blk, 0, s, sc, fp, aux, qs, b, passes & 1);
+        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), wgrid, blk, 0, s, sc, fp, aux, qs, b, passes - 1);
     }
 }
 // sh: 0 no occlusion rays, 1 per lane in the segment kernel, 2 queued and binned
@@ -1437,7 +1444,8 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     const bool count = fp.counters != nullptr;
     // (a queued record's destination names a queue slot: < parts * pcap)
     const int sh = queued_shadow_mode(sc, shadow, std::max(paths, (uint64_t)qs.parts * qs.pcap));
-    if (sh == 2 && (!qs.srec[0] || !qs.srec[1] || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
+    if (sh == 2 && (!qs.srec || !qs.skey || !qs.spair[0] || !qs.spair[1] || !qs.bhist || aux.pgrid <= 0))
+        return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
     // the wave-walked primary kernel uses no per-lane stack (no spill
     // columns): its own occupancy's grid

@@ -493,7 +493,7 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
         r.d_pq = nullptr;
         r.pq_cap = 0;
         HIP_TRY(hipMalloc(&r.d_pq, P * kPqBytesPerPath + RT_QC_WORDS(64) * sizeof(uint32_t) +
-                                       (uint64_t)RT_SH_BINS * RT_SH_BLOCKS * sizeof(uint32_t) + 2048));
+                                       (uint64_t)RT_SH_HBINS * RT_SH_BLOCKS * sizeof(uint32_t) + 2048));
         r.pq_cap = P;
     }
     uint8_t* base = static_cast<uint8_t*>(r.d_pq);
@@ -503,8 +503,11 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
     qs.q[1] = reinterpret_cast<double*>(base + c * 80);
     qs.Lfin = reinterpret_cast<double*>(base + c * 160);
     qs.fb = reinterpret_cast<uint32_t*>(base + c * 184);
-    qs.srec[0] = reinterpret_cast<double*>(base + align_up<char>(c * 192));
-    qs.srec[1] = reinterpret_cast<double*>(base + align_up<char>(c * 192) + c * 32);
+    qs.srec = reinterpret_cast<double*>(base + align_up<char>(c * 192));
+    // (the second 32 B per path: two arrays of sort pairs and the keys)
+    qs.spair[0] = reinterpret_cast<uint64_t*>(base + align_up<char>(c * 192) + c * 32);
+    qs.spair[1] = reinterpret_cast<uint64_t*>(base + align_up<char>(c * 192) + c * 40);
+    qs.skey = reinterpret_cast<uint32_t*>(base + align_up<char>(c * 192) + c * 48);
     const uint64_t o_ctl = align_up<char>(align_up<char>(c * 192) + c * 64);
     qs.ctl = reinterpret_cast<uint32_t*>(base + o_ctl);
     const uint64_t o_bh = align_up<char>(o_ctl + RT_QC_WORDS(64) * sizeof(uint32_t));

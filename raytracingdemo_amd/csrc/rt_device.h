@@ -271,9 +271,14 @@ struct PathQs {
     uint32_t parts, pcap;
     uint32_t ptile, ptiles_x;  // parts > 1: the primary tiles' edge in pixels and tiles per row
     // occlusion-ray queue (queued shadows): records {p (3 doubles), tri | dst}
-    // as the segment kernel appends them ([0]) and binned by their direction
-    // from the light ([1]); per-block bin counts of the binning passes
-    RT_G double* srec[2];
+    // as the segment kernel appends them, each with its sort key (skey: the
+    // direction from the light, queue_paths.h sh_key); the binning passes
+    // order (key, record) pairs (spair[0] after the low digit, spair[1] after
+    // the high one) with per-block bin counts bhist, and the occlusion walk
+    // reads the records through the sorted pairs
+    RT_G double* srec;
+    RT_G uint32_t* skey;
+    RT_G uint64_t* spair[2];  // {key, record} as two u32 (uint2 on the device)
     RT_G uint32_t* bhist;  // [bins][sh_blocks]
     uint32_t sh_blocks;
 };
@@ -310,9 +315,14 @@ static inline RT_HD RtQParts rt_qparts(int W, int nrows, int spp) {
 }
 // occlusion-ray order: a cube map around the light, 512 x 512 cells per face
 // in Morton order (21-bit keys), counting-sorted in two passes of RT_SH_BITS
-// bits (RT_SH_BINS bins, per-block counts of RT_SH_BLOCKS blocks)
+// bits, or in one pass of the top RT_SH_BITS1 bits (per-block counts of
+// RT_SH_BLOCKS blocks; RT_SH_HBINS: the larger digit's bins)
 #define RT_SH_CELLS 512
+#define RT_SH_KEY_BITS 21
 #define RT_SH_BITS 11
-#define RT_SH_BINS (1 << RT_SH_BITS)
+#ifndef RT_SH_BITS1
+#define RT_SH_BITS1 13
+#endif
+#define RT_SH_HBINS (1 << (RT_SH_BITS > RT_SH_BITS1 ? RT_SH_BITS : RT_SH_BITS1))
 #define RT_SH_BLOCKS 256
 

@@ -901,6 +901,12 @@ __device__ uint32_t q_primary_vertex(args_p A, int s, int i, int r, bool valid, 
 #else
 #define RT_Q_ATTR
 #endif
+// Phase timing builds of the segment kernel (never shipped; results are
+// wrong, and later segments see empty queues): 1 = each ray stops after its
+// walk, 2 = after the exact resolve.
+#ifndef RT_QS_DIAG
+#define RT_QS_DIAG 0
+#endif
 template <int W, int S, int K, bool COUNT, int SH>
 __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux,
                                                              PathQs qs, uint32_t frame, int b, int bounces) {
@@ -960,6 +966,10 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
                     tot.pre += lc.pre;
                 }
             }
+            if constexpr (RT_QS_DIAG == 1) {  // phase timing: the walk alone
+                qs.Lfin[3 * (size_t)e] = (double)tcull + nc + (over ? 1.0 : 0.0);
+                continue;
+            }
             Ray64 ray;
             double L[3];
             q_load(qs, qin, e, ray, L, path);  // (the entry again: L1 / L2)
@@ -976,6 +986,10 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
                 }
             }
             segs++;
+            if constexpr (RT_QS_DIAG == 2) {  // phase timing: the walk and the exact resolve
+                qs.Lfin[3 * (size_t)e] = win.t + win.tri + (fall ? 1.0 : 0.0);
+                continue;
+            }
             if (fall) {
                 qs.fb[qin * (size_t)qs.cap + atomicAdd(qc_fb(qs, b), 1u)] = fe;
             } else if (win.tri >= 0) {

@@ -605,7 +605,7 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
 // vertex the light sees adds 0.5^b of its colour to its destination's
 // radiance (the segment kernel wrote the radiance before this vertex there).
 #ifndef RT_SH_WPE
-#define RT_SH_WPE 6  // waves per SIMD of k_sh_walk
+#define RT_SH_WPE 5  // waves per SIMD of k_sh_walk (96 VGPRs): c5 190.3 / 190.4 vs 193.9 / 193.8 ms per pose at 6, 4: 189.9 / 190.4
 #endif
 template <int W, bool COUNT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SH_WPE))) k_sh_walk(RtDevScene sc, RtFrameParams fp, RtLaunchAux aux, PathQs qs, int b, int src) {

@@ -331,15 +331,15 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         # wave (256-B nodes, 48-B triangle records once per wave), else per
         # lane (96-B quantised nodes, 48-B fp32 records per lane) — plus, for
         # queued records, each 32-B record's trips (binned: the record and
-        # its 4-B key written; the 2 sort passes move (key, record) pairs:
-        # histogram reads of 4 and 8 B, scatters of 4 -> 8 and 8 -> 8 B; the
-        # walk reads its pair and gathers the record = 116 B; per-lane
-        # records kernel: written and read) and the lit ones' radiance read
-        # and written (48 B)
+        # its 4-B key written; the 3 sort passes of 7 bits move (key, record)
+        # pairs: histogram reads of 4, 8 and 8 B, scatters of 4 -> 8, 8 -> 8
+        # and 8 -> 8 B; the walk reads its pair and gathers the record = 140
+        # B; per-lane records kernel: written and read) and the lit ones'
+        # radiance read and written (48 B)
         sh_n = cs["shadow_rays"]
         sh_lit = sh_n - cs["shadow_occluded"]
         if shadow_kind == "binned":
-            sh_bytes = sh_n * 116 + sh_lit * 48 + cs["shadow_wave_nodes"] * 256 + cs["shadow_wave_tris"] * 48
+            sh_bytes = sh_n * 140 + sh_lit * 48 + cs["shadow_wave_nodes"] * 256 + cs["shadow_wave_tris"] * 48
         else:
             sh_bytes = cs["shadow_lane_nodes"] * 96 + cs["shadow_lane_tris"] * 48
             if shadow_kind == "records":
@@ -476,8 +476,8 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
                          "bytes": "per-lane node steps x 96 (quantised) + wave node steps x 256 and wave triangle "
                                   "records x 48 (primary segments walked by the wave) + pre-filter x 48 + fp64 tests "
                                   "x 72 + chain checks x 52 + segments x 56 + 3 per pixel; queued: + 160 per bounce "
-                                  "ray and 48 per sample (queues, final radiance); occlusion rays: binned: 116 per "
-                                  "ray (record + key written, key/record pairs through the 2-pass sort, record read) + 48 per lit one + wave node steps x 256 + "
+                                  "ray and 48 per sample (queues, final radiance); occlusion rays: binned: 140 per "
+                                  "ray (record + key written, key/record pairs through the 3-pass sort, record read) + 48 per lit one + wave node steps x 256 + "
                                   "wave triangle records x 48; per lane: node steps x 96 + triangle records x 48 "
                                   "(+ 64 per record and 48 per lit one from queued records)",
                          "convention": "a record once per fetching wave instruction: the wave walks' (primary, "

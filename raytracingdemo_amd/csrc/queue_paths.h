@@ -349,10 +349,11 @@ __device__ __forceinline__ void q_shadow_append_lane(const PathQs& qs, const RtF
 
 // Counting-sort pass over segment b's occlusion records, digit (key >> shift)
 // mod 2^BITS: pass 0 reads the appended records' keys (skey) and writes
-// (key, record) pairs to spair[0], pass 1 reorders spair[0] into spair[1];
+// (key, record) pairs to spair[0], pass p > 0 reorders spair[(p - 1) & 1]
+// into spair[p & 1];
 // per-block LDS histograms, one scan, then each block scatters its pairs
 // (their order inside a block is the LDS atomics', so a pass is stable only
-// up to a block's range).  Two passes (low digit, then high) order the
+// up to a block's range).  The passes (lowest digit first) order the
 // records by key up to that fuzz: neighbouring pairs are rays of nearly the
 // same direction from the light.  Only 4-8 B move per record and pass; the
 // occlusion walk gathers the 32-B records through the pairs.
@@ -377,7 +378,7 @@ __device__ __forceinline__ RT_G uint2* sh_pairs(const PathQs& qs, int p) {
 }
 // The pass's input element e: its key and record.
 __device__ __forceinline__ uint2 sh_input(const PathQs& qs, int pass, uint32_t e) {
-    return pass == 0 ? make_uint2(qs.skey[e], e) : sh_pairs(qs, 0)[e];
+    return pass == 0 ? make_uint2(qs.skey[e], e) : sh_pairs(qs, (pass - 1) & 1)[e];
 }
 template <int BITS>
 __global__ void __launch_bounds__(1024) k_sh_hist(PathQs qs, int b, int pass, int shift) {
@@ -433,7 +434,7 @@ __global__ void __launch_bounds__(1024) k_sh_scatter(PathQs qs, int b, int pass,
     __syncthreads();
     uint32_t lo, hi;
     sh_range(qs, b, pass, blockIdx.x, lo, hi);
-    RT_G uint2* const out = sh_pairs(qs, pass);
+    RT_G uint2* const out = sh_pairs(qs, pass & 1);
     for (uint32_t e = lo + threadIdx.x; e < hi; e += 1024) {
         const uint2 v = sh_input(qs, pass, e);
         out[atomicAdd(&cur[(v.x >> shift) & (BINS - 1)], 1u)] = v;

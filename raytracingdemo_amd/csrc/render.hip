@@ -1349,24 +1349,17 @@ void launch_q_segment(const RtDevScene& sc, const RtFrameParams& fp, const RtLau
     if constexpr (SH == 2) {
         // the segment's occlusion records: binned by direction from the light,
         // then walked 64 at a time by the wave-cooperative any-hit walk
-        // (RT_SH_PASSES=1, read per call: one pass over the top RT_SH_BITS1
-        // bits of the key, 0 -> 1)
-        const char* ps = getenv("RT_SH_PASSES");
-        const int passes = ps && ps[0] == '1' ? 1 : 2;
-        if (passes == 1) {
-            constexpr int shift = RT_SH_KEY_BITS - RT_SH_BITS1;
-            hipLaunchKernelGGL(k_sh_hist<RT_SH_BITS1>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, 0, shift);
-            hipLaunchKernelGGL(k_sh_scan<RT_SH_BITS1>, dim3(1), dim3(1024), 0, s, qs);
-            hipLaunchKernelGGL(k_sh_scatter<RT_SH_BITS1>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, 0, shift);
-        }
-        for (int pass = 0; pass < passes && passes == 2; pass++) {  // low digit -> spair[0], high -> spair[1]
+        // (RT_SH_BITS bits per pass, lowest digit first; ping-pong between
+        // the two pair arrays)
+        constexpr int passes = (RT_SH_KEY_BITS + RT_SH_BITS - 1) / RT_SH_BITS;
+        for (int pass = 0; pass < passes; pass++) {
             const int shift = pass * RT_SH_BITS;
             hipLaunchKernelGGL(k_sh_hist<RT_SH_BITS>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, pass, shift);
             hipLaunchKernelGGL(k_sh_scan<RT_SH_BITS>, dim3(1), dim3(1024), 0, s, qs);
             hipLaunchKernelGGL(k_sh_scatter<RT_SH_BITS>, dim3(RT_SH_BLOCKS), dim3(1024), 0, s, qs, b, pass, shift);
         }
         static const dim3 wgrid = occupancy_grid(k_sh_walk<W, COUNT>);
-        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), wgrid, blk, 0, s, sc, fp, aux, qs, b, passes - 1);
+        hipLaunchKernelGGL((k_sh_walk<W, COUNT>), wgrid, blk, 0, s, sc, fp, aux, qs, b, (passes - 1) & 1);
     }
 }
 // sh: 0 no occlusion rays, 1 per lane in the segment kernel, 2 queued and binned

@@ -314,15 +314,13 @@ static inline RT_HD RtQParts rt_qparts(int W, int nrows, int spp) {
     return p;
 }
 // occlusion-ray order: a cube map around the light, 512 x 512 cells per face
-// in Morton order (21-bit keys), counting-sorted in two passes of RT_SH_BITS
-// bits, or in one pass of the top RT_SH_BITS1 bits (per-block counts of
-// RT_SH_BLOCKS blocks; RT_SH_HBINS: the larger digit's bins)
+// in Morton order (21-bit keys), counting-sorted in passes of RT_SH_BITS
+// bits (per-block counts of RT_SH_BLOCKS blocks; RT_SH_HBINS bins)
 #define RT_SH_CELLS 512
 #define RT_SH_KEY_BITS 21
-#define RT_SH_BITS 11
-#ifndef RT_SH_BITS1
-#define RT_SH_BITS1 13
+#ifndef RT_SH_BITS
+#define RT_SH_BITS 7
 #endif
-#define RT_SH_HBINS (1 << (RT_SH_BITS > RT_SH_BITS1 ? RT_SH_BITS : RT_SH_BITS1))
+#define RT_SH_HBINS (1 << RT_SH_BITS)
 #define RT_SH_BLOCKS 256
 

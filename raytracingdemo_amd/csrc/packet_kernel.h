@@ -224,6 +224,10 @@ struct PacketArgs {
     int32_t bounces;
 };
 static_assert(sizeof(PacketArgs) % 4 == 0, "argument block is copied as words");
+// Measured (round 5): 16 B more of PathQs (4,336-B block) made
+// launches under rocprofv3 stall for 0.3-2 s with no waves resident (the
+// dispatch waiting, not the kernel); the round-4 size and below run clean.
+static_assert(sizeof(PacketArgs) <= 4320, "kernel argument block grew past the measured-clean size");
 typedef const __attribute__((address_space(3))) PacketArgs* args_p;
 
 // PATHS: the packed packet walk traces the primary segments of the queued
@@ -1150,16 +1154,8 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // Step 2 out of line, so the kernel body's registers stay as they are
 // (inlined, the per-lane exact path raised the fused kernel's spills from
 // 36 B to 4 KB of scratch per lane).
-#ifndef RT_REDO_INLINE
-#define RT_REDO_INLINE 0
-#endif
 template <int W, int K, bool COUNT>
-#if RT_REDO_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-void packet_redo(args_p A, uint2* ring, int lane) {
+__device__ __noinline__ void packet_redo(args_p A, uint2* ring, int lane) {
     // (a call's arguments arrive in VGPRs: the argument block's address made
     // uniform again)
     A = (args_p)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)A);
@@ -1200,17 +1196,8 @@ void packet_redo(args_p A, uint2* ring, int lane) {
             const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: pose * npix + pixel
             const int p = (int)(ob / npix);
             const uint32_t o = ob - (uint32_t)p * npix;
-            // (per lane: the lanes may hold pixels of different poses, so not kload's uniform copy)
-            RtPose pose;
-            {
-                const __attribute__((address_space(3))) uint32_t* src =
-                    (const __attribute__((address_space(3))) uint32_t*)&launder(A)->fp.pose[p];
-                uint32_t* dst = reinterpret_cast<uint32_t*>(&pose);
-#pragma unroll
-                for (unsigned w = 0; w < sizeof(RtPose) / 4; w++) dst[w] = src[w];
-            }
             trace_pixel<W, K, COUNT>(sc, fp, p, (int)(o % (uint32_t)fp.W), (int)(o / (uint32_t)fp.W), st,
-                                     (v & kRedoPass1) ? 1 : 0, true, &pose);
+                                     (v & kRedoPass1) ? 1 : 0, true);
         }
     }
 }
@@ -1223,9 +1210,7 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
     // (a cheap check first: the call only when entries are waiting)
     uint32_t pending = 0;
     if (lane == 0) pending = atomicAdd(ctr + RT_REDO_COUNT, 0u) > atomicAdd(ctr + RT_REDO_CLAIM, 0u);
-#ifndef RT_EXIT_NOREDO
     if (uni(pending)) packet_redo<W, K, COUNT>(A, ring, lane);
-#endif
     uint32_t tk = 0;
     if (lane == 0) tk = atomicAdd(ctr + RT_EXIT_COUNT, 1u) + 1u;
     if (uni(tk) != gridDim.x * (uint32_t)kPacketWaves) return;

@@ -320,7 +320,7 @@ __device__ __forceinline__ void q_shadow_store(const PathQs& qs, const RtFrameCa
     r[1] = py;
     r[2] = pz;
     r[3] = __longlong_as_double((long long)(((uint64_t)dst << 32) | (uint32_t)tri));
-    qs.skey[k] = sh_key(cam, px, py, pz);
+    rt_q_skey(qs)[k] = sh_key(cam, px, py, pz);
 }
 // Appends the lanes' occlusion records to partition x of srec (the partition
 // of the segment's input ray: its capacity covers them; one atomic per wave);
@@ -374,11 +374,11 @@ __device__ __forceinline__ void sh_range(const PathQs& qs, int b, int pass, uint
 }
 // Sorted pairs {key, record} of pass p.
 __device__ __forceinline__ RT_G uint2* sh_pairs(const PathQs& qs, int p) {
-    return reinterpret_cast<RT_G uint2*>(qs.spair[p]);
+    return reinterpret_cast<RT_G uint2*>(rt_q_spair(qs, p));
 }
 // The pass's input element e: its key and record.
 __device__ __forceinline__ uint2 sh_input(const PathQs& qs, int pass, uint32_t e) {
-    return pass == 0 ? make_uint2(qs.skey[e], e) : sh_pairs(qs, (pass - 1) & 1)[e];
+    return pass == 0 ? make_uint2(rt_q_skey(qs)[e], e) : sh_pairs(qs, (pass - 1) & 1)[e];
 }
 template <int BITS>
 __global__ void __launch_bounds__(1024) k_sh_hist(PathQs qs, int b, int pass, int shift) {

@@ -594,20 +594,12 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
     return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 1, lc);
 }
 
-// The camera of frame f: from fp's pose table, or — pose given — from that
-// pose (the packet kernel's exit path: indexing a private copy of fp's
-// 36-pose table by a run-time frame would put the whole table in scratch).
-__device__ __forceinline__ RtFrameCam frame_cam_at(const RtFrameParams& fp, int f, const RtPose* pose) {
-    return pose ? frame_cam_of(*pose, fp, f) : frame_cam(fp, f);
-}
-
 // Exact per-lane traversal of the primary ray of pixel (i, r) of frame f.
 template <int W, int S, bool COUNT, int C>
 __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
-                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false,
-                                            const RtPose* pose = nullptr) {
+                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
     const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
-    const RtFrameCam cam = frame_cam_at(fp, f, pose);
+    const RtFrameCam cam = frame_cam(fp, f);
     auto ray_of = [&]() { return gen_ray(fp, cam, opaque(i), j); };
     LaneCounts lc;
     const Win best = trace_core<W, S, COUNT>(sc, ray_of, cam.pad, st, pass0, lc);
@@ -668,18 +660,17 @@ __device__ __forceinline__ void wave_add_keyed(RT_G unsigned long long* base, in
 // lanes of a wave may hold pixels of different poses).
 template <int W, int S, bool COUNT, int C>
 __device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameParams& fp, int p, int i, int r,
-                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false,
-                                            const RtPose* pose = nullptr) {
+                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
     const size_t po = out_index(fp, p, (size_t)r * fp.W + i);
     double acc[3] = {0.0, 0.0, 0.0};
     uint32_t hits = 0;
     for (int k = 0; k < fp.spp; k++) {
         const int f = p * fp.spp + k;
-        const Best b = trace_exact<W, S, COUNT>(sc, fp, f, i, r, st, pass0, fixup, pose);
+        const Best b = trace_exact<W, S, COUNT>(sc, fp, f, i, r, st, pass0, fixup);
         const Shade sh = shade_of(sc, b.tri);
         store_sample(fp, po * (size_t)fp.spp + k, b, sh);
         double c[3];
-        shade_color(frame_cam_at(fp, f, pose), b, sh, c);
+        shade_color(frame_cam(fp, f), b, sh, c);
         acc[0] = acc[0] + c[0];
         acc[1] = acc[1] + c[1];
         acc[2] = acc[2] + c[2];
@@ -1446,8 +1437,7 @@ hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const R
     const bool count = fp.counters != nullptr;
     // (a queued record's destination names a queue slot: < parts * pcap)
     const int sh = queued_shadow_mode(sc, shadow, std::max(paths, (uint64_t)qs.parts * qs.pcap));
-    if (sh == 2 && (!qs.srec || !qs.skey || !qs.spair[0] || !qs.spair[1] || !qs.bhist || aux.pgrid <= 0))
-        return hipErrorInvalidValue;
+    if (sh == 2 && (!qs.srec || !qs.bhist || aux.pgrid <= 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)aux.grid), blk(256), agrid((unsigned)((fp.W * (uint64_t)fp.nrows + 255) / 256));
     // the wave-walked primary kernel uses no per-lane stack (no spill
     // columns): its own occupancy's grid

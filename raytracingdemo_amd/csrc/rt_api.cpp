@@ -503,11 +503,9 @@ PathQs ensure_pq(Replica& r, uint64_t P) {
     qs.q[1] = reinterpret_cast<double*>(base + c * 80);
     qs.Lfin = reinterpret_cast<double*>(base + c * 160);
     qs.fb = reinterpret_cast<uint32_t*>(base + c * 184);
+    // (and behind the records, 32 B per path: two arrays of sort pairs and
+    // the keys, rt_device.h rt_q_spair / rt_q_skey)
     qs.srec = reinterpret_cast<double*>(base + align_up<char>(c * 192));
-    // (the second 32 B per path: two arrays of sort pairs and the keys)
-    qs.spair[0] = reinterpret_cast<uint64_t*>(base + align_up<char>(c * 192) + c * 32);
-    qs.spair[1] = reinterpret_cast<uint64_t*>(base + align_up<char>(c * 192) + c * 40);
-    qs.skey = reinterpret_cast<uint32_t*>(base + align_up<char>(c * 192) + c * 48);
     const uint64_t o_ctl = align_up<char>(align_up<char>(c * 192) + c * 64);
     qs.ctl = reinterpret_cast<uint32_t*>(base + o_ctl);
     const uint64_t o_bh = align_up<char>(o_ctl + RT_QC_WORDS(64) * sizeof(uint32_t));

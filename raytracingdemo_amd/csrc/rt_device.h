@@ -276,12 +276,21 @@ struct PathQs {
     // order (key, record) pairs (spair[0] after the low digit, spair[1] after
     // the high one) with per-block bin counts bhist, and the occlusion walk
     // reads the records through the sorted pairs
+    // (one base pointer: srec's records, then per record slot the two pair
+    // arrays and the keys — rt_q_spair / rt_q_skey; the argument block of the
+    // packet kernel, which carries PathQs, keeps its size)
     RT_G double* srec;
-    RT_G uint32_t* skey;
-    RT_G uint64_t* spair[2];  // {key, record} as two u32 (uint2 on the device)
     RT_G uint32_t* bhist;  // [bins][sh_blocks]
     uint32_t sh_blocks;
 };
+// The sort arrays behind the occlusion records (cap record slots): pairs
+// {key, record} (two u32) after pass p at spair(p & 1), the keys at skey.
+static inline RT_HD RT_G uint64_t* rt_q_spair(const PathQs& q, int k) {
+    return reinterpret_cast<RT_G uint64_t*>(reinterpret_cast<RT_G char*>(q.srec) + (uint64_t)q.cap * (32u + 8u * (uint32_t)k));
+}
+static inline RT_HD RT_G uint32_t* rt_q_skey(const PathQs& q) {
+    return reinterpret_cast<RT_G uint32_t*>(reinterpret_cast<RT_G char*>(q.srec) + (uint64_t)q.cap * 48u);
+}
 #define RT_QPARTS RT_QUEUES
 // k_trace_packet deals its tiles to the XCD queues in runs of RT_TILE_RUN
 // consecutive tiles (tile t to queue (t / RUN) % RT_QUEUES).  Tuning knob:

@@ -213,6 +213,12 @@ __device__ __forceinline__ int compact_candidates(uint2* __restrict__ cand, int 
 // scene constants alive across the walk (the walk needs the SGPRs for the
 // child records of a whole node in flight) nor re-read the kernarg segment
 // (host-coherent memory, far slower) per tile.
+// Unpacked tiles: RT_TILE_W x (64 / RT_TILE_W) pixels of one frame per wave
+// (tuning knob; 8 x 8 by default).
+#ifndef RT_TILE_W
+#define RT_TILE_W 8
+#endif
+static_assert(RT_TILE_W >= 1 && RT_TILE_W <= 64 && (RT_TILE_W & (RT_TILE_W - 1)) == 0, "tile width: a power of two");
 struct PacketArgs {
     RtDevScene sc;
     RtFrameParams fp;
@@ -1283,9 +1289,10 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
         // (ts = 8 / n), else 8 x 8 pixels of one sample frame
         constexpr bool pack = FUSED && PACK;  // (launched only when fp.pack)
         const int spp = kword(&A->fp.spp);
-        const int ts = pack ? 8 / kword(&A->fp.spp_n) : 8;
+        const int ts = pack ? 8 / kword(&A->fp.spp_n) : RT_TILE_W;
+        const int th = pack ? ts : 64 / RT_TILE_W;
         const int tiles_x = (W_ + ts - 1) / ts;
-        const int tiles_f = tiles_x * ((nrows + ts - 1) / ts);  // tiles per frame (pose when packed)
+        const int tiles_f = tiles_x * ((nrows + th - 1) / th);  // tiles per frame (pose when packed)
         const int tiles = tiles_f * (pack ? kword(&A->fp.nframes) / spp : kword(&A->fp.nframes));
         claim = tiles >= 64 * (int)(gridDim.x * kPacketWaves) ? 2 : 1;
         int s = 0;
@@ -1328,8 +1335,8 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             i = tx * ts + pl % ts;
             r = ty * ts + pl / ts;
         } else {
-            i = tx * 8 + (lane & 7);
-            r = ty * 8 + (lane >> 3);
+            i = tx * RT_TILE_W + (lane & (RT_TILE_W - 1));
+            r = ty * (64 / RT_TILE_W) + lane / RT_TILE_W;
         }
         const TileOut o =
             trace_packet<W, SP, K, COUNT, FUSED, PACK, PATHS>(A, f, i, r, i < W_ && r < nrows, stacks[wv], cands[wv]);

@@ -331,7 +331,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         # wave (256-B nodes, 48-B triangle records once per wave), else per
         # lane (96-B quantised nodes, 48-B fp32 records per lane) — plus, for
         # queued records, each 32-B record's trips (binned: the record and
-        # its 4-B key written; the 3 sort passes of 7 bits move (key, record)
+        # its 4-B key written; the 3 sort passes of 7 bits (19-bit keys) move (key, record)
         # pairs: histogram reads of 4, 8 and 8 B, scatters of 4 -> 8, 8 -> 8
         # and 8 -> 8 B; the walk reads its pair and gathers the record = 140
         # B; per-lane records kernel: written and read) and the lit ones'

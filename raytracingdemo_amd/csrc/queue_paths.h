@@ -281,9 +281,9 @@ __device__ __forceinline__ RT_G double* q_dst(const PathQs& qs, uint32_t dst) {
 
 // Sort key of an occlusion ray: the cube-map cell of its direction from the
 // light — face (3 bits) over the Morton code of the cell (u, v) on the face
-// (RT_SH_CELLS^2 cells, 0.18 degrees).  Only the order of the occlusion pass
+// (RT_SH_CELLS^2 cells, 0.35 degrees).  Only the order of the occlusion pass
 // depends on it, never a result.
-__device__ __forceinline__ uint32_t morton9(uint32_t x) {  // 9 bits spread to the even bits
+__device__ __forceinline__ uint32_t morton_spread(uint32_t x) {  // up to 16 bits spread to the even bits
     x = (x | (x << 8)) & 0x00FF00FFu;
     x = (x | (x << 4)) & 0x0F0F0F0Fu;
     x = (x | (x << 2)) & 0x33333333u;
@@ -309,7 +309,7 @@ __device__ __forceinline__ uint32_t sh_key(const RtFrameCam& cam, double px, dou
     int iu = (int)((u + m) * s), iv = (int)((v + m) * s);
     iu = iu < 0 ? 0 : iu >= RT_SH_CELLS ? RT_SH_CELLS - 1 : iu;
     iv = iv < 0 ? 0 : iv >= RT_SH_CELLS ? RT_SH_CELLS - 1 : iv;
-    return (face << 18) | morton9((uint32_t)iu) | (morton9((uint32_t)iv) << 1);
+    return (face << (2 * RT_SH_CELL_BITS)) | morton_spread((uint32_t)iu) | (morton_spread((uint32_t)iv) << 1);
 }
 
 // Occlusion record k {p, tri, dst} and its sort key.

@@ -322,11 +322,14 @@ static inline RT_HD RtQParts rt_qparts(int W, int nrows, int spp) {
     p.entries = (uint64_t)p.pcap * RT_QPARTS;
     return p;
 }
-// occlusion-ray order: a cube map around the light, 512 x 512 cells per face
-// in Morton order (21-bit keys), counting-sorted in passes of RT_SH_BITS
+// occlusion-ray order: a cube map around the light, 2^RT_SH_CELL_BITS squared
+// cells per face in Morton order (19-bit keys), counting-sorted in passes of RT_SH_BITS
 // bits (per-block counts of RT_SH_BLOCKS blocks; RT_SH_HBINS bins)
-#define RT_SH_CELLS 512
-#define RT_SH_KEY_BITS 21
+#ifndef RT_SH_CELL_BITS
+#define RT_SH_CELL_BITS 8  // 256 x 256 cells per face: c5 187.1 / 187.3 vs 189.2 / 189.4 ms per pose at 512^2, 190.7 at 128^2
+#endif
+#define RT_SH_CELLS (1 << RT_SH_CELL_BITS)
+#define RT_SH_KEY_BITS (3 + 2 * RT_SH_CELL_BITS)
 #ifndef RT_SH_BITS
 #define RT_SH_BITS 7
 #endif

@@ -873,9 +873,10 @@ def main():
     # start event fires when its stream reaches it), so spans overlap and
     # their mean exceeds the time each launch actually holds the GPU.  The
     # roofline then takes the wall time per launch of the timed region
-    # (launches back to back, k_fixup and gaps included: an upper bound; the
-    # rocprofv3 median span agrees) and reports the mean span
-    # beside it.
+    # (launches back to back, gaps included: an upper bound; in a rocprofv3
+    # kernel trace it is the union of the timed launches' busy intervals per
+    # launch, `tools/launch_ends.py`, not their own start-to-end durations,
+    # which overlap) and reports the mean span beside it.
     span_s = avg_kernel_s
     overlapped = not a.no_overlap and ks["timed_launches"] > 1
     if overlapped:

@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--out")
+    ap.add_argument("--timed", type=int, default=30, help="traversal launches of the timed region (bench.py --steps)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows)
@@ -47,6 +48,23 @@ def main():
                          f"{tail:8.4f} q{q} {names}")
     lines.append(f"# launches {len(tails)}; tail after the traversal kernel: max {max(tails):.4f} ms, "
                  f"median {statistics.median(tails):.4f} ms")
+    # Launches on two streams overlap (launch k + 1's waves start on the CUs
+    # launch k's tail frees), so a kernel's own start-to-end duration exceeds
+    # the time per launch; the union of the last `timed` traversal launches'
+    # busy intervals, per launch, is the figure bench.py's roofline divides by.
+    trav = sorted((e[0], e[1]) for e in ev if "k_trace_packet<" in e[2] and ", false, true" in e[2]
+                  and not re.search(r"k_trace_packet<\d+, \d+, \d+, true", e[2]))[-a.timed:]
+    if trav:
+        busy, (cs, ce) = 0, trav[0]
+        for s0, e0 in trav[1:]:
+            if s0 > ce:
+                busy, cs, ce = busy + ce - cs, s0, e0
+            else:
+                ce = max(ce, e0)
+        busy += ce - cs
+        durs = sorted((e0 - s0) / 1e6 for s0, e0 in trav)
+        lines.append(f"# last {len(trav)} traversal launches: busy union {busy / 1e6 / len(trav):.4f} ms per launch, "
+                     f"own duration median {statistics.median(durs):.4f} ms (overlapped)")
     text = "\n".join(lines) + "\n"
     if a.out:
         open(a.out, "w").write(text)

@@ -292,7 +292,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         for f in range(F):
             scene.render_paths_device(local, pos, d, W, H, rank, world, my_rows, frame=k % 36, spp=S, bounces=B,
                                       rgb=rgb.data_ptr(), hit_count=cnt.data_ptr(), stream=stream.cuda_stream,
-                                      timing=timing, count=count, shadow=shadow)
+                                      timing=timing, count=count, shadow=shadow, counts_store=True)
 
     def step(k, timing=False, count=False):
         render(k, timing=timing, count=count)
@@ -392,7 +392,11 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu:
-            cpu = paths_cpu_baseline(tris, a, path, W, H, S, B, shadow)
+            # (the rows the CPU leg renders come from the last timed pose and
+            # are compared with that pose's timed colours)
+            k_last = (a.steps - 1) % 36
+            cpu = paths_cpu_baseline(tris, a, path, W, H, S, B, shadow, pose=k_last,
+                                     gpu_rgb=rgb[0].reshape(H, W, 3).cpu().numpy())
         key = (f"{label}|{W}x{H}|{a.algo}-{a.k}|paths|spp{S}|b{B}|n{world}" + ("|shadow" if shadow else "")
                + f"|{a.pipeline}")
         if a.key_out:
@@ -405,7 +409,12 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
                 traffic = round(float(pm["hbm_bytes_per_launch"]))
         except (OSError, ValueError, KeyError):
             pass
-        achieved = alg_pose / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        # frac counts bytes as the headline's does — a record once per
+        # fetching wave instruction (alg_wave); the lane
+        # walks counted per lane stay beside it (frac_lane_walks_per_lane)
+        alg_frac = alg_wave if alg_wave else alg_pose
+        achieved = alg_frac / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        achieved_lw = alg_pose / kernel_s / 1e9 if kernel_s > 0 else 0.0
         # the per-lane convention beside it: the primary segments' wave-walk
         # records counted once per lane (64) instead of once per wave; every
         # other walk here is per lane in both
@@ -455,11 +464,14 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
             "kernel_ms_avg": round(ks["trace_ms"] / max(ks["timed_launches"], 1), 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac_convention": ("per wave instruction (the headline's): every walk's records once per "
+                                             "fetching wave instruction" if alg_wave else
+                                             "lane walks per lane (no wave-distinct counters in this library)"),
+                         # the per-lane bounce and occlusion walks' records per lane
+                         # (round 4-5's frac), and every walk per lane
+                         "frac_lane_walks_per_lane": round(achieved_lw / HBM_PEAK_GBS, 4),
+                         "alg_bytes_lane_walks_per_lane": round(alg_pose),
                          "frac_per_lane": round(achieved_pl / HBM_PEAK_GBS, 4),
-                         # every walk's records once per wave instruction (the
-                         # headline's convention; comparable with its frac)
-                         "frac_per_wave_instruction": (round(alg_wave / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
-                                                       if alg_wave and kernel_s > 0 else None),
                          "alg_bytes_per_wave_instruction": round(alg_wave) if alg_wave else None,
                          # measured bytes past L2 (FETCH_SIZE x 2 + WRITE_SIZE): fabric
                          # requests, Infinity-Cache hits included (MI355X guide, HBM
@@ -469,7 +481,7 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
                          "traffic_counts": TRAFFIC_COUNTS,
                          "kernel": ("queued pipeline (k_q_primary, k_q_segment, k_q_fallback, k_sh_*, k_q_accum; "
                                     "HIP events around the pose)" if queued else "k_paths"),
-                         "alg_bytes_per_launch": round(alg_pose), "alg_bytes_parts": alg_parts,
+                         "alg_bytes_per_launch": round(alg_frac), "alg_bytes_parts": alg_parts,
                          "per_segment": {k: round(cs[c] / max(cs["rays"], 1), 3) for k, c in
                                          (("node_fetches", "node_fetches"), ("tri_prefilter", "tri_prefilter"),
                                           ("tri_tests_fp64", "tri_tests"), ("chain_checks", "chain_checks"))},
@@ -492,35 +504,49 @@ def run_paths(a, scene, tris, label, world, rank, local, dev, coll, rehearse, ra
         dist.destroy_process_group()
 
 
-def paths_cpu_baseline(tris, a, path, W, H, S, B, shadow=True):
+def paths_cpu_baseline(tris, a, path, W, H, S, B, shadow=True, pose=0, gpu_rgb=None):
     """The oracle's path tracer (the reference has none: kind "port") on host
-    cores over whole rows of the same pose until ~cpu_seconds."""
+    cores over whole rows of the same pose (the last timed one, frame = pose)
+    until ~cpu_seconds.  gpu_rgb: that pose's timed colours [H, W, 3]; every
+    row the oracle renders is compared with them (verified_timed_rows)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     host = host_cores()
     threads = int(os.environ.get("RT_CPU_THREADS", host["usable"]))
     b = pyoracle.Oracle().bvh(tris, a.algo, a.k)
-    pos, d = path.circular_path(0)
+    pos, d = path.circular_path(pose)
+    check = {"pose": pose, "rows": 0, "row_list": [], "pixels": 0, "rgb_diff": 0}
 
-    def leg(nthreads, budget_s):
+    def leg(nthreads, budget_s, verify):
         rows, spent, j = 0, 0.0, 0
         n = max(1, nthreads // 4)  # whole rows per call, spread over the image
         while spent < budget_s and rows < H:
+            m = min(n, H - j)
             t0 = time.perf_counter()
-            b.render_paths(pos, d, W, H, 0, S, B, row0=j, nrows=min(n, H - j), threads=nthreads, shadow=shadow)
+            o = b.render_paths(pos, d, W, H, pose, S, B, row0=j, nrows=m, threads=nthreads, shadow=shadow)
             spent += time.perf_counter() - t0
-            rows += min(n, H - j)
+            if verify and gpu_rgb is not None:  # (outside the timed CPU work)
+                check["rows"] += m
+                check["row_list"].append([j, m])
+                check["pixels"] += m * W
+                check["rgb_diff"] += int(np.count_nonzero(np.any(o["rgb"] != gpu_rgb[j:j + m].reshape(-1, 3),
+                                                                 axis=1)))
+            rows += m
             j = (j + 97 * n) % (H - n)
         return rows, spent
 
-    rows, spent = leg(threads, a.cpu_seconds)
-    rows1, spent1 = leg(1, a.cpu_seconds / 3)
+    rows, spent = leg(threads, a.cpu_seconds, True)
+    rows1, spent1 = leg(1, a.cpu_seconds / 3, False)
     rate = lambda r, s: round(r * W * S * (1 + B) / s / 1e6, 4)
     return {"value": rate(rows, spent), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{rows} rows of {W} px x {S} spp x (1 + {B}) segments, pose 0 ({spent:.1f} s)",
+            "sample": f"{rows} rows of {W} px x {S} spp x (1 + {B}) segments, pose {pose} ({spent:.1f} s)",
+            **({"verified_timed_rows": dict(check, equal=check["rgb_diff"] == 0 and check["rows"] > 0,
+                                            compared="PPM bytes of the timed pose (the timed call writes colours "
+                                                     "and the hit count only)")}
+               if gpu_rgb is not None else {}),
             "all_cores": {"value": rate(rows, spent), "cores": threads},
             "one_core": {"value": rate(rows1, spent1), "cores": 1,
-                         "sample": f"{rows1} rows of {W} px, pose 0 ({spent1:.1f} s)"},
+                         "sample": f"{rows1} rows of {W} px, pose {pose} ({spent1:.1f} s)"},
             "host": host,
             "note": "nominal rays (W x H x spp x (1 + bounces)) per second, as the GPU line; the reference has "
                     "no path tracer, so the oracle's restatement of this build's model is timed"}
@@ -682,6 +708,7 @@ def main():
     side_slot = (world > 1 or ship_sim > 0) and os.environ.get("RT_BENCH_SIDE_SLOT", "1") != "0"
     pending = [False] * NB
     mode = a.mode
+    zero_fill = os.environ.get("RT_BENCH_ZERO_FILL") == "1"
 
     def render(b, timing=False, count=False):
         # the whole camera orbit in one batched call (the library launches up
@@ -694,13 +721,17 @@ def main():
         with torch.cuda.stream(sb):
             if shipped[b] is not None:
                 sb.wait_event(shipped[b])  # set b's previous gather has read it
-            cnt[b].zero_()
             # the library's multi-GPU partition (rt_render_shard_device: bands of
-            # 8 rows interleaved over the ranks)
+            # 8 rows interleaved over the ranks); the render stores the per-pose
+            # hit counts (RT_FLAG_COUNTS_STORE), so no zero fill precedes it —
+            # one would wait behind the other stream's persistent grid for
+            # ~3 ms and gate this render's start
+            if zero_fill:  # (RT_BENCH_ZERO_FILL=1: round 5's fill + adding call, for A/B runs)
+                cnt[b].zero_()
             scene.render_shard_device(local, cams, W, H, srank, sworld, hit_id=r_ids[b].data_ptr(),
                                       dist=dists[b].data_ptr(), rgb=r_rgb[b].data_ptr(), hit_count=cnt[b].data_ptr(),
                                       stream=sb.cuda_stream, mode=mode, timing=timing, count=count, spp=S, job=job,
-                                      side_slot=side_slot)
+                                      side_slot=side_slot, counts_store=not zero_fill)
             if padded:
                 ids[b][:, :my_rows] = r_ids[b]
                 rgb[b][:, :my_rows] = r_rgb[b]
@@ -945,7 +976,13 @@ def main():
                        **({"side_slot": True} if side_slot else {}),
                        "parallelism": f"8-row image bands interleaved x{world}" +
                                       (" + RCCL gather of rgb (overlapped)" if world > 1 else ""),
-                       **({"gather_verified": verified} if world > 1 else {}),
+                       **({"gather_verified": verified,
+                           # what the timed gather ships (SURVEY 8(e) names hit id + dist + rgb)
+                           "timed_gather_payload": "rgb frames + per-pose hit counts (RCCL gather to rank 0 and "
+                                                   "de-interleave, overlapped with the next render); hit ids and "
+                                                   "distances stay on the ranks in the timed region and are gathered "
+                                                   "after it, for gather_verified (DESIGN.md §8)"}
+                          if world > 1 else {}),
                        # rank 0's de-interleave of the gathered frames: done by the
                        # traversal kernel of a render (rt_render_shard_device_job) or
                        # by its own kernel, over the timed steps

@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* status codes */
 #define RT_OK 0
@@ -95,6 +95,14 @@ extern "C" {
                              the previous step's frames — runs beside the
                              render instead of after it (one-process-per-GPU
                              drivers)                         */
+#define RT_FLAG_COUNTS_STORE 16u /* batch / shard / paths renders: hit_count[f]
+                             is SET to the call's count instead of being added
+                             to, so the caller need not zero it before every
+                             render (runTest's per-frame shadeScreen return,
+                             main.cpp:260-262).  The fused packet kernel
+                             stores the counts from its last wave; where a
+                             pipeline cannot, the library zeroes the counters
+                             on the stream first (same result).             */
 
 #define RT_MISS 0xFFFFFFFFu
 

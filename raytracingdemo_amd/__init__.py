@@ -242,11 +242,12 @@ class Scene:
 
     def render_batch_device(self, device: int, cams, W: int, H: int, row0: int, row_stride: int, nrows: int,
                             hit_id=0, dist=0, hit_pos=0, rgb=0, hit_count=0, stream=0, mode: str = "exact",
-                            count: bool = False, timing: bool = False, spp: int = 1):
+                            count: bool = False, timing: bool = False, spp: int = 1, counts_store: bool = False):
         """Asynchronous shard render of several poses ``cams`` = [(pos, dir), ...]
         (runTest's camera loop, src/main.cpp:234-281) into device pointers: pose
         f's outputs start f * W * nrows pixels in (per-sample outputs: times spp),
-        its hit counter is hit_count[f].  spp = n*n stratified samples per pixel
+        its hit counter is hit_count[f] (added to; counts_store: set,
+        RT_FLAG_COUNTS_STORE).  spp = n*n stratified samples per pixel
         (include/rt.h rt_render_batch_spp_device)."""
         n = len(cams)
         arr = (N.rt_camera * max(n, 1))(*[_camera(p, d, W, H) for p, d in cams])
@@ -256,11 +257,13 @@ class Scene:
                                                    int(row_stride), int(nrows), C.byref(o),
                                                    C.c_void_p(stream or None),
                                                    (N.RT_FLAG_COUNT if count else 0) |
-                                                   (N.RT_FLAG_TIMING if timing else 0)))
+                                                   (N.RT_FLAG_TIMING if timing else 0) |
+                                                   (N.RT_FLAG_COUNTS_STORE if counts_store else 0)))
 
     def render_shard_device(self, device: int, cams, W: int, H: int, shard: int, nshards: int, hit_id=0, dist=0,
                             hit_pos=0, rgb=0, hit_count=0, stream=0, mode: str = "exact", count: bool = False,
-                            timing: bool = False, spp: int = 1, job: dict | None = None, side_slot: bool = False):
+                            timing: bool = False, spp: int = 1, job: dict | None = None, side_slot: bool = False,
+                            counts_store: bool = False):
         """Shard `shard` of `nshards` of every pose (bands of 8 rows interleaved,
         include/rt.h rt_render_shard_device) into device pointers: pose f's
         outputs start f * W * shard_height(H, nshards, shard) pixels in.
@@ -268,13 +271,14 @@ class Scene:
         section_offset, shards, frames, height, width, elem_bytes, frame_rows,
         frames_out) carried out on the side by this render's kernel
         (rt_render_shard_device_job).  side_slot: RT_FLAG_SIDE_SLOT (one
-        workgroup slot per CU left free for a collective on another stream)."""
+        workgroup slot per CU left free for a collective on another stream);
+        counts_store: RT_FLAG_COUNTS_STORE (hit_count[f] set, not added to)."""
         n = len(cams)
         arr = (N.rt_camera * max(n, 1))(*[_camera(p, d, W, H) for p, d in cams])
         o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
         m = N.RT_MODE_FP64 if mode in ("fp64", "literal") else N.RT_MODE_EXACT
         fl = ((N.RT_FLAG_COUNT if count else 0) | (N.RT_FLAG_TIMING if timing else 0) |
-              (N.RT_FLAG_SIDE_SLOT if side_slot else 0))
+              (N.RT_FLAG_SIDE_SLOT if side_slot else 0) | (N.RT_FLAG_COUNTS_STORE if counts_store else 0))
         if job is None:
             N.check(N.lib().rt_render_shard_device(self._h, int(device), arr, n, int(spp), m, int(shard),
                                                    int(nshards), C.byref(o), C.c_void_p(stream or None), fl))
@@ -285,7 +289,8 @@ class Scene:
                                                        C.c_void_p(stream or None), fl))
 
     def render_batch_multi(self, cams, W: int, H: int, hit_id=0, dist=0, hit_pos=0, rgb=0, hit_count=0, stream=0,
-                           mode: str = "exact", count: bool = False, timing: bool = False, spp: int = 1):
+                           mode: str = "exact", count: bool = False, timing: bool = False, spp: int = 1,
+                           counts_store: bool = False):
         """Full frames of every pose in ``cams`` over all uploaded devices (rows
         interleaved, RCCL gather to the first device, de-interleaved there) into
         device pointers on the first device (include/rt.h rt_render_batch_multi)."""
@@ -294,24 +299,26 @@ class Scene:
         o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
         m = N.RT_MODE_FP64 if mode in ("fp64", "literal") else N.RT_MODE_EXACT
         N.check(N.lib().rt_render_batch_multi(self._h, arr, n, int(spp), m, C.byref(o), C.c_void_p(stream or None),
-                                              (N.RT_FLAG_COUNT if count else 0) | (N.RT_FLAG_TIMING if timing else 0)))
+                                              (N.RT_FLAG_COUNT if count else 0) | (N.RT_FLAG_TIMING if timing else 0) |
+                                              (N.RT_FLAG_COUNTS_STORE if counts_store else 0)))
 
     def render_paths_device(self, device: int, pos, d, W: int, H: int, row0: int, row_stride: int, nrows: int,
                             frame: int = 0, spp: int = 16, bounces: int = 4, hit_id=0, dist=0, hit_pos=0, rgb=0,
                             hit_count=0, stream=0, timing: bool = False, count: bool = False,
-                            shadow: bool = False):
+                            shadow: bool = False, counts_store: bool = False):
         """Diffuse path tracing of one pose into device pointers (include/rt.h
         rt_render_paths_device): rgb per pixel, primary-segment outputs per sample;
         count: add the ray segments traced to frame_stats()["rays"]; shadow: an
         occlusion ray toward the head-light from every bounce vertex
-        (RT_FLAG_SHADOW)."""
+        (RT_FLAG_SHADOW); counts_store: hit_count set, not added to."""
         o = N.rt_device_out(hit_id or None, dist or None, hit_pos or None, rgb or None, hit_count or None)
         cam = _camera(pos, d, W, H)
         N.check(N.lib().rt_render_paths_device(self._h, int(device), C.byref(cam), int(frame), int(spp), int(bounces),
                                                int(row0), int(row_stride), int(nrows), C.byref(o),
                                                C.c_void_p(stream or None),
                                                (N.RT_FLAG_TIMING if timing else 0) | (N.RT_FLAG_COUNT if count else 0) |
-                                               (N.RT_FLAG_SHADOW if shadow else 0)))
+                                               (N.RT_FLAG_SHADOW if shadow else 0) |
+                                               (N.RT_FLAG_COUNTS_STORE if counts_store else 0)))
 
     def frame_stats(self, device: int = 0, reset: bool = True) -> dict:
         s = N.rt_frame_stats_t()

@@ -29,6 +29,7 @@ RT_FLAG_COUNT = 1
 RT_FLAG_TIMING = 2
 RT_FLAG_SHADOW = 4
 RT_FLAG_SIDE_SLOT = 8
+RT_FLAG_COUNTS_STORE = 16
 RT_MISS = 0xFFFFFFFF
 
 # Every symbol include/rt.h declares (checked by tests/test_abi.py).

@@ -274,14 +274,31 @@ __device__ __forceinline__ T kword(const __attribute__((address_space(3))) T* p)
 // negative direction and the lo plane otherwise — exactly what the per-axis
 // min/max of the general test (OCT = -1) selects, since t(lo) <= t(hi) for a
 // positive reciprocal and t(hi) <= t(lo) for a negative one.
+//
+// RT_PK_SLAB (default): the two planes of an axis in one v_pk_fma_f32 — the
+// record's {lo, hi} pair is an aligned SGPR pair, the reciprocal goes to both
+// halves and the offsets are the {lo, hi} pair nox — so a child costs 3
+// packed fmas instead of 6 (each half rounds once, as fmaf: the same bits).
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 1
+#endif
 template <int W, int OCT>
 __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32& q, const f2 nox, const f2 noy,
                                            const f2 noz, float tcull, uint64_t (&hm)[W]) {
+    const f2 ix2{q.ix, q.ix}, iy2{q.iy, q.iy}, iz2{q.iz, q.iz};
 #pragma unroll
     for (int c = 0; c < W; c++) {
-        const float tlx = __builtin_fmaf(bx[c][0], q.ix, nox.x), thx = __builtin_fmaf(bx[c][1], q.ix, nox.y);
-        const float tly = __builtin_fmaf(bx[c][2], q.iy, noy.x), thy = __builtin_fmaf(bx[c][3], q.iy, noy.y);
-        const float tlz = __builtin_fmaf(bx[c][4], q.iz, noz.x), thz = __builtin_fmaf(bx[c][5], q.iz, noz.y);
+        float tlx, thx, tly, thy, tlz, thz;
+        if constexpr (RT_PK_SLAB != 0) {
+            const f2 tx = __builtin_elementwise_fma(f2{bx[c][0], bx[c][1]}, ix2, nox);
+            const f2 ty = __builtin_elementwise_fma(f2{bx[c][2], bx[c][3]}, iy2, noy);
+            const f2 tz = __builtin_elementwise_fma(f2{bx[c][4], bx[c][5]}, iz2, noz);
+            tlx = tx.x; thx = tx.y; tly = ty.x; thy = ty.y; tlz = tz.x; thz = tz.y;
+        } else {
+            tlx = __builtin_fmaf(bx[c][0], q.ix, nox.x); thx = __builtin_fmaf(bx[c][1], q.ix, nox.y);
+            tly = __builtin_fmaf(bx[c][2], q.iy, noy.x); thy = __builtin_fmaf(bx[c][3], q.iy, noy.y);
+            tlz = __builtin_fmaf(bx[c][4], q.iz, noz.x); thz = __builtin_fmaf(bx[c][5], q.iz, noz.y);
+        }
         float t0, t1;
         if constexpr (OCT < 0) {
             t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fmaxf(fminf(tlz, thz), 0.f));
@@ -1161,7 +1178,15 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // (inlined, the per-lane exact path raised the fused kernel's spills from
 // 36 B to 4 KB of scratch per lane).
 template <int W, int K, bool COUNT>
-__device__ __noinline__ void packet_redo(args_p A, uint2* ring, int lane) {
+#ifndef RT_REDO_INLINE
+#define RT_REDO_INLINE 0
+#endif
+#if RT_REDO_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void packet_redo(args_p A, uint2* ring, int lane) {
     // (a call's arguments arrive in VGPRs: the argument block's address made
     // uniform again)
     A = (args_p)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)A);
@@ -1191,19 +1216,42 @@ __device__ __noinline__ void packet_redo(args_p A, uint2* ring, int lane) {
         lo = uni(lo);
         hi = uni(hi);
         if (lo >= hi) break;
+        uint32_t v = kRedoEmpty;
         if ((uint32_t)lane < hi - lo) {
-            uint32_t v;
-            // (the append's count came first: its entry lands within a round trip)
-            while ((v = atomicExch(aux.redo + lo + (uint32_t)lane, kRedoEmpty)) == kRedoEmpty)
+            // (the append's count came first: its entry lands within a round
+            // trip; a spin past 2^22 sleeps means the all-kRedoEmpty
+            // invariant is broken: the lane gives the entry up and the launch
+            // reports it to the host, which fails the next call on the slot —
+            // rt_api.cpp launch — instead of hanging the GPU)
+            uint32_t spins = 0;
+            while ((v = atomicExch(aux.redo + lo + (uint32_t)lane, kRedoEmpty)) == kRedoEmpty) {
                 __builtin_amdgcn_s_sleep(2);
+                if (++spins == (1u << 22)) break;
+            }
+            if (v == kRedoEmpty) (void)atomicOr(ctr + RT_EXIT_ERROR, 1u);
+        }
+        if (v != kRedoEmpty) {
             const RtDevScene sc = kload(&A->sc);
-            const RtFrameParams fp = kload(&A->fp);
+            const RtFrameParams fp = kload(&A->fp);  // (its pose array is never indexed here)
             const uint32_t npix = (uint32_t)fp.W * (uint32_t)fp.nrows;
             const uint32_t ob = v & ~kRedoPass1;  // pixel of the batch: pose * npix + pixel
             const int p = (int)(ob / npix);
             const uint32_t o = ob - (uint32_t)p * npix;
-            trace_pixel<W, K, COUNT>(sc, fp, p, (int)(o % (uint32_t)fp.W), (int)(o / (uint32_t)fp.W), st,
-                                     (v & kRedoPass1) ? 1 : 0, true);
+            // the lane's pose, read out of the LDS argument block by the lane
+            // itself (lanes may hold different poses)
+            RtPose pose;
+            {
+                const __attribute__((address_space(3))) uint32_t* src =
+                    (const __attribute__((address_space(3))) uint32_t*)&A->fp.pose[p];
+                uint32_t* dst = reinterpret_cast<uint32_t*>(&pose);
+#pragma unroll
+                for (unsigned w = 0; w < sizeof(RtPose) / 4; w++) dst[w] = src[w];
+            }
+            const uint32_t hits = trace_pixel_at<W, K, COUNT>(sc, fp, pose, p, (int)(o % (uint32_t)fp.W),
+                                                              (int)(o / (uint32_t)fp.W), st,
+                                                              (v & kRedoPass1) ? 1 : 0, true);
+            // into the pose's partials, which the last wave folds (or stores)
+            if (hits) atomicAdd(ctr + RT_HIT_BASE + (p * RT_HIT_SLOTS + lane) * RT_QUEUE_STRIDE, hits);
         }
     }
 }
@@ -1216,14 +1264,37 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
     // (a cheap check first: the call only when entries are waiting)
     uint32_t pending = 0;
     if (lane == 0) pending = atomicAdd(ctr + RT_REDO_COUNT, 0u) > atomicAdd(ctr + RT_REDO_CLAIM, 0u);
+    // (RT_NO_REDO=1: a measurement build without the redo call — and its
+    // callee frame in the private segment; wrong results if any pixel needs
+    // a redo, never shipped)
+#if !defined(RT_NO_REDO) || !RT_NO_REDO
     if (uni(pending)) packet_redo<W, K, COUNT>(A, ring, lane);
+#else
+    (void)pending;
+#endif
+    // The exit ticket is a release (agent scope: the wave's partial adds,
+    // including the redo path's, are performed before it) and the last wave
+    // acquires before it reads the partials (HIP memory model: relaxed
+    // atomics alone would not order the partials of another XCD's wave
+    // before its ticket).  RT_EXIT_FENCE=0: relaxed, the waits only.
     uint32_t tk = 0;
+#if !defined(RT_EXIT_FENCE) || RT_EXIT_FENCE
+    if (lane == 0)
+        tk = __hip_atomic_fetch_add(ctr + RT_EXIT_COUNT, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) tk = atomicAdd(ctr + RT_EXIT_COUNT, 1u) + 1u;
+#endif
     if (uni(tk) != gridDim.x * (uint32_t)kPacketWaves) return;
-    // the last wave: per pose, the 64 spread partials (one per lane) summed
+#if !defined(RT_EXIT_FENCE) || RT_EXIT_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+    // the last wave: per pose, the 64 spread partials (one per lane) summed,
+    // then added to the caller's counter or (RT_SELF_STORE) stored in it
     A = launder(A);
     const int poses = kword(&A->fp.nframes) / kword(&A->fp.spp);
     RT_G unsigned long long* const hc = kload(&A->fp.hit_count);
+    const bool store = (kword(&A->aux.self_fix) & RT_SELF_STORE) != 0;
     uint32_t part[RT_MAX_BATCH];
 #pragma unroll
     for (int m = 0; m < RT_MAX_BATCH; m++)
@@ -1232,16 +1303,21 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
     for (int m = 0; m < RT_MAX_BATCH; m++) {
         if (m >= poses) break;
         const uint32_t s = wave_sum_u32(part[m]);
-        if (lane == 0 && hc && s) atomicAdd(hc + m, (unsigned long long)s);
+        if (lane == 0 && hc) {
+            if (store) __hip_atomic_store(hc + m, (unsigned long long)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (s) atomicAdd(hc + m, (unsigned long long)s);
+        }
     }
     if (lane < RT_QUEUES) {
         (void)atomicExch(ctr + lane * RT_QUEUE_STRIDE, 0u);
         (void)atomicExch(ctr + RT_COPY_BASE + lane * RT_QUEUE_STRIDE, 0u);
     }
     if (lane == 0) {
+        // the redo count to the host (RT_SEEN_ERROR: an entry was given up)
         const uint32_t n = atomicExch(ctr + RT_REDO_COUNT, 0u);
+        const uint32_t err = atomicExch(ctr + RT_EXIT_ERROR, 0u);
         uint32_t* const seen = kload(&A->aux.redo_seen);
-        if (seen) __hip_atomic_store(seen, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (seen) __hip_atomic_store(seen, n | (err ? RT_SEEN_ERROR : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         (void)atomicExch(ctr + RT_POOL_COUNT, 0u);
         (void)atomicExch(ctr + RT_REDO_CLAIM, 0u);
         (void)atomicExch(ctr + RT_EXIT_COUNT, 0u);

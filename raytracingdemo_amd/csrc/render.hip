@@ -594,12 +594,12 @@ __device__ __forceinline__ Win trace_deferred(const RtDevScene& sc, RayFn&& ray_
     return trace_core<W, S, COUNT>(sc, ray_of, pad, st, 1, lc);
 }
 
-// Exact per-lane traversal of the primary ray of pixel (i, r) of frame f.
+// Exact per-lane traversal of the primary ray of pixel (i, r) of the sample
+// frame whose camera is `cam`.
 template <int W, int S, bool COUNT, int C>
-__device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
-                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
+__device__ __forceinline__ Best trace_exact_cam(const RtDevScene& sc, const RtFrameParams& fp, const RtFrameCam& cam,
+                                                int i, int r, LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
     const int j = rt_image_row(fp.row0, fp.row_stride, fp.band, r);
-    const RtFrameCam cam = frame_cam(fp, f);
     auto ray_of = [&]() { return gen_ray(fp, cam, opaque(i), j); };
     LaneCounts lc;
     const Win best = trace_core<W, S, COUNT>(sc, ray_of, cam.pad, st, pass0, lc);
@@ -624,6 +624,12 @@ __device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameP
         atomicAdd(&fp.counters[6], (unsigned long long)n_pre);
     }
     return out;
+}
+// ... of frame f of the launch.
+template <int W, int S, bool COUNT, int C>
+__device__ __forceinline__ Best trace_exact(const RtDevScene& sc, const RtFrameParams& fp, int f, int i, int r,
+                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
+    return trace_exact_cam<W, S, COUNT>(sc, fp, frame_cam(fp, f), i, r, st, pass0, fixup);
 }
 
 // Adds each active lane's v (< 2^BITS) to *p with one atomic per wave.
@@ -655,28 +661,39 @@ __device__ __forceinline__ void wave_add_keyed(RT_G unsigned long long* base, in
     }
 }
 
-// All spp samples of pixel (i, r) of pose p with the per-lane exact kernel:
-// per-sample outputs, the averaged colour and the pose's hit count (the
-// lanes of a wave may hold pixels of different poses).
+// All spp samples of pixel (i, r) of pose p, whose camera is `pose`, with the
+// per-lane exact kernel: per-sample outputs and the averaged colour; returns
+// the samples hit.  (The pose comes in by itself so that a caller holding
+// the launch parameters in registers never indexes their pose array with a
+// lane-varying p: that array would go to the private segment.)
 template <int W, int S, bool COUNT, int C>
-__device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameParams& fp, int p, int i, int r,
-                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
+__device__ __forceinline__ uint32_t trace_pixel_at(const RtDevScene& sc, const RtFrameParams& fp, const RtPose& pose,
+                                                   int p, int i, int r, LaneStack<S, C>& st, int pass0 = 0,
+                                                   bool fixup = false) {
     const size_t po = out_index(fp, p, (size_t)r * fp.W + i);
     double acc[3] = {0.0, 0.0, 0.0};
     uint32_t hits = 0;
     for (int k = 0; k < fp.spp; k++) {
-        const int f = p * fp.spp + k;
-        const Best b = trace_exact<W, S, COUNT>(sc, fp, f, i, r, st, pass0, fixup);
+        const RtFrameCam cam = frame_cam_of(pose, fp, p * fp.spp + k);
+        const Best b = trace_exact_cam<W, S, COUNT>(sc, fp, cam, i, r, st, pass0, fixup);
         const Shade sh = shade_of(sc, b.tri);
         store_sample(fp, po * (size_t)fp.spp + k, b, sh);
         double c[3];
-        shade_color(frame_cam(fp, f), b, sh, c);
+        shade_color(cam, b, sh, c);
         acc[0] = acc[0] + c[0];
         acc[1] = acc[1] + c[1];
         acc[2] = acc[2] + c[2];
         hits += b.tri >= 0;
     }
     store_rgb(fp, po, acc);
+    return hits;
+}
+// ... with the pose's hit count added (the lanes of a wave may hold pixels of
+// different poses).
+template <int W, int S, bool COUNT, int C>
+__device__ __forceinline__ void trace_pixel(const RtDevScene& sc, const RtFrameParams& fp, int p, int i, int r,
+                                            LaneStack<S, C>& st, int pass0 = 0, bool fixup = false) {
+    const uint32_t hits = trace_pixel_at<W, S, COUNT>(sc, fp, fp.pose[p], p, i, r, st, pass0, fixup);
     wave_add_keyed(fp.hit_count, p, hits);
 }
 
@@ -954,12 +971,25 @@ hipError_t launch_exact(const RtDevScene& sc, const RtFrameParams& fp, const RtL
     // the bookkeeping (packet_exit) and no k_fixup follows, so the launch
     // ends with its traversal kernel
     RtLaunchAux aux = aux_in;
-    const bool packet_r = W == 8 && fp.spp == 1 && !fp.pack && !aux_in.job_src && packet_rays() == 2;
-    aux.self_fix = aux_in.self_fix && !split_resolve(fp.spp) && (fp.spp == 1 || fp.pack) && !packet_r ? 1 : 0;
+    // The kernel of the launch, chosen once (every launch below follows it):
+    // the fused k_trace_packet<FUSED> of spp = 1 or of packed samples is the
+    // one that calls packet_exit; RT_SELF_FIX goes to that kernel only, so a
+    // kernel without packet_exit (split resolve, k_trace_packet_r, the
+    // per-lane kernel) always gets its trailing k_fixup.
+    const bool packet = use_packet(sc.stack_bound);
+    const bool packet_r = W == 8 && packet && fp.spp == 1 && !fp.pack && !aux_in.job_src && packet_rays() == 2;
+    const bool fused_exit = packet && !split_resolve(fp.spp) && (fp.spp == 1 || fp.pack) && !packet_r;
+    aux.self_fix = (aux_in.self_fix & RT_SELF_FIX) && fused_exit ? (aux_in.self_fix & (RT_SELF_FIX | RT_SELF_STORE)) : 0;
+    // RT_SELF_STORE asked for where the kernel cannot store the counts: zero
+    // them first (the launch's poses' counters, nothing else adds to them)
+    if ((aux_in.self_fix & RT_SELF_STORE) && !(aux.self_fix & RT_SELF_STORE) && fp.hit_count) {
+        const hipError_t e = hipMemsetAsync(fp.hit_count, 0, sizeof(unsigned long long) * (size_t)(fp.nframes / fp.spp), s);
+        if (e != hipSuccess) return e;
+    }
     // RT_FLAG_TIMING: two markers bracket the traversal kernel only (the
     // rest of the pipeline is timed as frame minus traversal by the caller)
     if (ev) (void)hipEventRecord(ev[0], s);
-    if (use_packet(sc.stack_bound)) {
+    if (packet) {
         // (aux.fgrid: the host saw this slot's redo list overflow, so a
         // retry of the whole launch is likely: the full grid)
         int fg = aux.fgrid > 0 ? aux.fgrid : kFixupGrid;
@@ -1110,6 +1140,7 @@ int exact_lds_stack() {
     int a = kLdsStack < kPathStack ? kLdsStack : kPathStack;
     return a < RT_Q_STACK ? a : RT_Q_STACK;
 }
+int packet_threads() { return 64 * kPacketWaves; }  // threads per packet workgroup (spill columns per block)
 int packet_candidates() { return RT_CAND_LDS; }  // candidate entries per pixel (spp > 1 lists; packet_exit's ring)
 bool packet_split(int spp, bool pack) { return needs_cand(spp, pack); }
 uint32_t params_bytes() { return (uint32_t)sizeof(RtFrameParams); }
@@ -1158,8 +1189,11 @@ hipError_t launch_trace_core(const RtDevScene& sc, const RtFrameParams& fp, cons
         const long tiles = (long)((fp.W + 7) / 8) * (long)((fp.nrows + 7) / 8);
         const dim3 grid((unsigned)((tiles + 3) / 4));
         if (literal_stack > 1024) return hipErrorInvalidValue;
-        if (ev) (void)hipEventRecord(ev[0], s);
         hipError_t e = hipSuccess;
+        if ((aux.self_fix & RT_SELF_STORE) && fp.hit_count)  // (the literal kernel adds: zeroed first)
+            e = hipMemsetAsync(fp.hit_count, 0, sizeof(unsigned long long) * (size_t)(fp.nframes / fp.spp), s);
+        if (e != hipSuccess) return e;
+        if (ev) (void)hipEventRecord(ev[0], s);
         for (int f = 0; f < fp.nframes / fp.spp && e == hipSuccess; f++) {
             const RtFrameParams f1 = single_pose(fp, f);
             e = literal_stack <= 64    ? launch_literal_s<64>(sc, f1, count, grid, s)
@@ -1215,14 +1249,14 @@ __global__ void __launch_bounds__(256) k_deinterleave(RtLaunchAux a) {
 }
 
 // Per-frame hit counts of the G shards (u64 [F] at cnt_off of each block) added
-// to the caller's counters.
+// to the caller's counters (store: written over them, RT_FLAG_COUNTS_STORE).
 __global__ void k_sum_counts(const uint8_t* __restrict__ gather, uint64_t block, uint64_t cnt_off, int G, int F,
-                             unsigned long long* __restrict__ out) {
+                             unsigned long long* __restrict__ out, int store) {
     const int f = (int)threadIdx.x;
     if (f >= F) return;
     unsigned long long t = 0;
     for (int g = 0; g < G; g++) t += reinterpret_cast<const unsigned long long*>(gather + g * block + cnt_off)[f];
-    out[f] += t;
+    out[f] = store ? t : out[f] + t;
 }
 
 hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_off, int G, int F, int H, int W,
@@ -1249,10 +1283,10 @@ hipError_t launch_job(const RtLaunchAux& a, hipStream_t s) {
 }
 
 hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_off, int G, int F,
-                             unsigned long long* out, hipStream_t s) {
+                             unsigned long long* out, bool store, hipStream_t s) {
     if (F <= 0 || F > 1024) return F <= 0 ? hipSuccess : hipErrorInvalidValue;
     hipLaunchKernelGGL(k_sum_counts, dim3(1), dim3(1024), 0, s, static_cast<const uint8_t*>(gather), block, cnt_off,
-                       G, F, out);
+                       G, F, out, store ? 1 : 0);
     return hipGetLastError();
 }
 

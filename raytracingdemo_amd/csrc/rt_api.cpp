@@ -32,6 +32,7 @@ hipError_t launch_paths(const RtDevScene& sc, const RtFrameParams& fp, const RtL
 hipError_t launch_paths_q(const RtDevScene& sc, const RtFrameParams& fp, const RtLaunchAux& aux, const PathQs& qs,
                           uint32_t frame, int bounces, bool shadow, hipStream_t s, const hipEvent_t* ev);
 int packet_candidates();
+int packet_threads();
 bool packet_takes_job(const RtDevScene& sc, const RtFrameParams& fp, int mode, bool count);
 bool packet_split(int spp, bool pack);
 uint32_t params_bytes();
@@ -39,7 +40,7 @@ int exact_lds_stack();
 hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_off, int G, int F, int H, int W,
                                int eb, void* dst, hipStream_t s);
 hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_off, int G, int F,
-                             unsigned long long* out, hipStream_t s);
+                             unsigned long long* out, bool store, hipStream_t s);
 hipError_t launch_job(const RtLaunchAux& a, hipStream_t s);
 }
 
@@ -403,8 +404,10 @@ void upload_one(rt_scene* s, int device) {
     const int S = rt::exact_lds_stack();
     r.spill_cap = f.stack_bound > (uint32_t)S ? f.stack_bound - (uint32_t)S : 1u;
     const uint32_t K = (uint32_t)rt::packet_candidates();  // packet_exit's LDS ring (render.hip)
+    // (packet_redo spills at lane blockIdx * packet_threads + threadIdx of a
+    // grid of pgrid * packet_threads lanes)
     r.spill_words = std::max((size_t)r.grid * 256 * r.spill_cap,
-                             (size_t)r.pgrid * 256 * (f.stack_bound > K ? f.stack_bound - K : 1u));
+                             (size_t)r.pgrid * (size_t)rt::packet_threads() * (f.stack_bound > K ? f.stack_bound - K : 1u));
     r.pool_chunks = kPoolChunks;
     if (const char* e = std::getenv("RT_POOL_CHUNKS")) {  // test hook: a small pool runs dry
         const long v = std::atol(e);
@@ -649,8 +652,10 @@ Slot& take_slot(Replica& r, hipStream_t st, bool shared) {
 }
 
 // Runs the pipeline and tracks whether its work-queue block is left zeroed.
+// store: RT_FLAG_COUNTS_STORE (the launch sets its poses' hit counts).
 void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
-            const hipEvent_t* tev, const rt_deinterleave_job* job = nullptr, bool side_slot = false);
+            const hipEvent_t* tev, const rt_deinterleave_job* job = nullptr, bool side_slot = false,
+            bool store = false);
 
 // A side de-interleave job (include/rt.h) in the launch's aux block.
 void set_job(RtLaunchAux& a, const rt_deinterleave_job* j) {
@@ -706,11 +711,17 @@ uint32_t literal_stack_bound(const rt_scene* s) {
 }
 
 void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int mode, bool count, hipStream_t st,
-            const hipEvent_t* tev, const rt_deinterleave_job* job, bool side_slot) {
+            const hipEvent_t* tev, const rt_deinterleave_job* job, bool side_slot, bool store) {
     bool fresh_after = false;
     // a slot whose last launch overflowed its redo list (the count k_fixup
     // reported, possibly from a launch still running: a sizing hint only)
     const uint32_t seen = __atomic_load_n(q.h_seen, __ATOMIC_RELAXED);
+    if (seen & RT_SEEN_ERROR) {
+        // a wave of an earlier launch on the slot gave a redo entry up
+        // (packet_kernel.h packet_redo): its pixel was not finished
+        __atomic_store_n(q.h_seen, 0u, __ATOMIC_RELAXED);
+        throw rt::Error{RT_ERR_RUNTIME, "redo list invariant broken: an earlier launch left a pixel unfinished"};
+    }
     const uint64_t lpix = (uint64_t)fp.W * (uint64_t)fp.nrows * (uint64_t)(fp.nframes / std::max(fp.spp, 1));
     if (seen > q.redo_cap && q.redo_cap < std::min(lpix, kRedoGrow))
         ensure_redo(q, std::min<uint64_t>(2ull * seen, lpix), kRedoGrow);
@@ -718,7 +729,7 @@ void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int
     a.redo_seen = q.h_seen;
     if (seen > a.redo_cap) a.fgrid = r.grid;
     // the packet kernel may end the launch itself: no retry is possible
-    a.self_fix = a.redo_cap >= lpix ? 1 : 0;
+    a.self_fix = (a.redo_cap >= lpix ? RT_SELF_FIX : 0) | (store ? RT_SELF_STORE : 0);
     // RT_FLAG_SIDE_SLOT: one workgroup slot per CU left to other streams
     if (side_slot && r.pgrid > r.cus) a.pgrid = r.pgrid - r.cus;
     set_job(a, job);
@@ -785,7 +796,7 @@ void render_batch_locked(rt_scene* s, Replica& rr, const rt_camera* cams, int nf
             tev = r->tev[r->tev_used++].data();
         }
         launch(s, *r, q, fp, mode, count, st, tev, f0 == 0 ? job : nullptr,  // (the job rides the first launch)
-               (flags & RT_FLAG_SIDE_SLOT) != 0);
+               (flags & RT_FLAG_SIDE_SLOT) != 0, (flags & RT_FLAG_COUNTS_STORE) != 0);
     }
 }
 
@@ -906,7 +917,6 @@ void render_group(rt_scene* s, const rt_camera* cams, int nframes, int spp, int 
         DevGuard dg(r.device);
         HIP_TRY(hipStreamWaitEvent(r.stream, gp.ev_in, 0));
         uint8_t* b = static_cast<uint8_t*>(gp.stage[g]);
-        HIP_TRY(hipMemsetAsync(b + L.cnt, 0, (size_t)nframes * 8, r.stream));
         rt_device_out so{};
         so.hit_id = out->hit_id ? reinterpret_cast<uint32_t*>(b + L.id) : nullptr;
         so.dist = out->dist ? reinterpret_cast<double*>(b + L.dist) : nullptr;
@@ -914,8 +924,12 @@ void render_group(rt_scene* s, const rt_camera* cams, int nframes, int spp, int 
         so.rgb = out->rgb ? b + L.rgb : nullptr;
         so.hit_count = reinterpret_cast<unsigned long long*>(b + L.cnt);
         const int nrows = rt_shard_rows(H, G, g);
-        if (nrows > 0)
-            render_batch_locked(s, r, cams, nframes, spp, mode, g, G, nrows, &so, r.stream, flags, RT_SHARD_BAND);
+        if (nrows > 0) {  // (the shard's counts stored into its block: no zeroing)
+            render_batch_locked(s, r, cams, nframes, spp, mode, g, G, nrows, &so, r.stream,
+                                flags | RT_FLAG_COUNTS_STORE, RT_SHARD_BAND);
+        } else {
+            HIP_TRY(hipMemsetAsync(b + L.cnt, 0, (size_t)nframes * 8, r.stream));
+        }
     }
     // gather to the first device: RCCL between distinct devices (one group of
     // ncclGather calls, each on its shard's stream), device copies otherwise
@@ -942,7 +956,8 @@ void render_group(rt_scene* s, const rt_camera* cams, int nframes, int spp, int 
         HIP_TRY(rt::launch_deinterleave(gp.gather, block, L.pos, G, nframes, H, W, 24 * ssz, out->pos, r0.stream));
     if (out->rgb) HIP_TRY(rt::launch_deinterleave(gp.gather, block, L.rgb, G, nframes, H, W, 3, out->rgb, r0.stream));
     if (out->hit_count)
-        HIP_TRY(rt::launch_sum_counts(gp.gather, block, L.cnt, G, nframes, out->hit_count, r0.stream));
+        HIP_TRY(rt::launch_sum_counts(gp.gather, block, L.cnt, G, nframes, out->hit_count,
+                                      (flags & RT_FLAG_COUNTS_STORE) != 0, r0.stream));
     HIP_TRY(hipEventRecord(gp.ev1, r0.stream));
     HIP_TRY(hipEventRecord(gp.ev_out, r0.stream));
     HIP_TRY(hipStreamWaitEvent(st0, gp.ev_out, 0));
@@ -1325,6 +1340,9 @@ int rt_render_paths_device(rt_scene* s, int device, const rt_camera* cam, int fr
         fp.hit_pos = out->pos;
         fp.rgb = out->rgb;
         fp.hit_count = out->hit_count;
+        // (the path kernels add their hits: a stored count is zeroed first)
+        if ((flags & RT_FLAG_COUNTS_STORE) && out->hit_count)
+            HIP_TRY(hipMemsetAsync(out->hit_count, 0, sizeof(unsigned long long), st));
         const hipEvent_t* tev = nullptr;
         if (flags & RT_FLAG_TIMING) {
             if (r->tev_used == r->tev.size()) {
@@ -1403,7 +1421,6 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
         d.pos = out->pos ? reinterpret_cast<double*>(base + o_pos) : nullptr;
         d.rgb = reinterpret_cast<uint8_t*>(base + o_rgb);  // always shaded (shadeScreen)
         d.hit_count = reinterpret_cast<unsigned long long*>(base + o_cnt);
-        HIP_TRY(hipMemsetAsync(d.hit_count, 0, 8, r.stream));
         RtFrameParams fp = frame_params(s, cam, 1, 0, 1, cam->height);
         fp.hit_id = d.hit_id;
         fp.dist = d.dist;
@@ -1415,7 +1432,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
             // every uploaded device renders its interleaved rows; the frame
             // is gathered and de-interleaved on the first device (the device
             // time is the group's, first device's stream: renders to gather)
-            render_group(s, cam, 1, 1, mode, &d, r.stream, 0);
+            render_group(s, cam, 1, 1, mode, &d, r.stream, RT_FLAG_COUNTS_STORE);
             e0 = s->grp.ev0;
             e1 = s->grp.ev1;
         } else {
@@ -1424,7 +1441,7 @@ int rt_render_frame(rt_scene* s, const rt_camera* cam, int mode, rt_frame_out* o
             Slot& q = take_slot(r, r.stream, split);
             ensure_redo(q, npx);
             HIP_TRY(hipEventRecord(r.ev0, r.stream));
-            launch(s, r, q, fp, mode, false, r.stream, nullptr);
+            launch(s, r, q, fp, mode, false, r.stream, nullptr, nullptr, false, true);  // (counts stored)
             HIP_TRY(hipEventRecord(r.ev1, r.stream));
         }
         if (out->hit_id) HIP_TRY(hipMemcpyAsync(out->hit_id, d.hit_id, npx * 4, hipMemcpyDeviceToHost, r.stream));

@@ -51,6 +51,12 @@
 // exit tickets (RtLaunchAux::self_fix: the launch ends without k_fixup)
 #define RT_REDO_CLAIM (RT_REDO_COUNT + 3 * RT_QUEUE_STRIDE)
 #define RT_EXIT_COUNT (RT_REDO_COUNT + 4 * RT_QUEUE_STRIDE)
+// nonzero: a wave of the packet kernel's own redo pass gave an entry up (the
+// list's all-empty invariant was broken); reported to the host through
+// RtLaunchAux::redo_seen as RT_SEEN_ERROR (launch pixels < 2^31, so the bit
+// is free)
+#define RT_EXIT_ERROR (RT_REDO_COUNT + 5 * RT_QUEUE_STRIDE)
+#define RT_SEEN_ERROR 0x80000000u
 // rows of the side de-interleave job (RtLaunchAux::job_*) claimed so far,
 // one counter per XCD queue (queue x takes rows x, x + RT_QUEUES, ...: a
 // counter shared by all XCDs would serialise on cross-XCD atomics)
@@ -169,6 +175,10 @@ struct RtDevScene {
                                   // word holds its child node's; bvh_build.cpp flatten)
 };
 
+// RtLaunchAux::self_fix bits
+#define RT_SELF_FIX 1
+#define RT_SELF_STORE 2
+
 // Per-launch resources of the persistent exact kernel.
 struct RtLaunchAux {
     RT_G uint32_t* tile_ctr;   // work-queue block (RT_QUEUE_WORDS words), zeroed before every launch
@@ -180,9 +190,10 @@ struct RtLaunchAux {
     uint32_t* redo_seen;  // host-mapped word: k_fixup reports the launch's redo count there (or null);
                           // the host grows the slot's list for its next launches from it
     int32_t fgrid;        // k_fixup blocks (0: the default kFixupGrid)
-    int32_t self_fix;     // 1: the fused packet kernel's own waves finish the redo list and the
-                          // bookkeeping (packet_exit), no k_fixup (redo_cap >= the launch's pixels;
-                          // spill sized for the packet grid)
+    int32_t self_fix;     // RT_SELF_FIX: the fused packet kernel's own waves finish the redo list
+                          // and the bookkeeping (packet_exit), no k_fixup (redo_cap >= the launch's
+                          // pixels; spill sized for the packet grid); | RT_SELF_STORE: its last wave
+                          // stores the per-pose hit counts instead of adding them (RT_FLAG_COUNTS_STORE)
     RT_G uint64_t* pool;       // candidate overflow pool: pool_chunks x RT_POOL_CHUNK entries
     uint32_t pool_chunks;
     int32_t pgrid;             // workgroups of the packet kernel (64 * kPacketWaves threads each)

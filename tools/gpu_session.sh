@@ -25,6 +25,9 @@ for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python __graft_entry__.py smoke ;;
         tests) run tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+        testk) # the GPU tests whose names match PYTEST_K
+               run testk 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+                   -p no:cacheprovider -k "${PYTEST_K:?}" ;;
         bench) run bench 600 python bench.py ;;
         quick) run bench_quick 300 python bench.py --no-cpu --steps 10 ;;
         frames) for f in 4 9 36; do run bench_f$f 300 python bench.py --no-cpu --no-dropin --steps 20 --frames $f || exit 1; done ;;
@@ -80,6 +83,15 @@ for s in $STEPS; do
                    for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_paths_${n#librtmi355x_}" 300 \
                           python bench.py --paths --no-cpu --steps 3 --warmup 1 || exit 1; done ;;
+        vab)   # A/B, interleaved: the shipped library and every variant, VAB_REPS rounds, 20 steps each
+               for rep in $(seq 1 ${VAB_REPS:-2}); do
+                   for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
+                       n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}
+                       RT_LIB=${v:+$PWD/$v} run "vab_${n}_$rep" 300 python bench.py --no-cpu --no-dropin --steps ${AB_STEPS:-20} \
+                           --shard-of ${AB_SHARD:-1} || exit 1
+                       python -c "import json; l=[x for x in open('gpurun_out/vab_${n}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']; print('RESULT', '$n', $rep, d['value'], d['ms_per_step'], r['kernel_ms_avg'], r['kernel_ms_span_avg'])" || true
+                   done
+               done ;;
         vshards) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}_s8" 300 \
                           python bench.py --no-cpu --no-dropin --steps 10 --shard-of 8 || exit 1; done ;;

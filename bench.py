@@ -602,14 +602,16 @@ def main():
     # are the reference's dynamic-scene metric (build + traversal,
     # scripts/bvh_analysis.py:62,543) next to the host walk-tree build
     t_build = time.perf_counter()
-    scene = rt.Scene(tris, a.algo, a.k, walk_device=local)
+    # (RT_BENCH_HOST_WALK=1: the walk tree built on the host, for A/B runs)
+    wdev = None if os.environ.get("RT_BENCH_HOST_WALK") == "1" else local
+    scene = rt.Scene(tris, a.algo, a.k, walk_device=wdev)
     t_upload = time.perf_counter()
     scene.upload([local])
     torch.cuda.synchronize(dev)
     t_ready = time.perf_counter()
     bt = scene.build_times()
     # a second build: the first one in a process also loads the build kernels
-    warm_scene = rt.Scene(tris, a.algo, a.k, walk_device=local)
+    warm_scene = rt.Scene(tris, a.algo, a.k, walk_device=wdev)
     warm = warm_scene.build_times()
     t_wu = time.perf_counter()
     warm_scene.upload([local])

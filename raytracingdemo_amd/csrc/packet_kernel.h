@@ -275,12 +275,16 @@ __device__ __forceinline__ T kword(const __attribute__((address_space(3))) T* p)
 // min/max of the general test (OCT = -1) selects, since t(lo) <= t(hi) for a
 // positive reciprocal and t(hi) <= t(lo) for a negative one.
 //
-// RT_PK_SLAB (default): the two planes of an axis in one v_pk_fma_f32 — the
-// record's {lo, hi} pair is an aligned SGPR pair, the reciprocal goes to both
-// halves and the offsets are the {lo, hi} pair nox — so a child costs 3
-// packed fmas instead of 6 (each half rounds once, as fmaf: the same bits).
+// RT_PK_SLAB=1 (a tuning build): the two planes of an axis in one
+// v_pk_fma_f32 — the record's {lo, hi} pair is an aligned SGPR pair, the
+// reciprocal goes to both halves and the offsets are the {lo, hi} pair nox —
+// so a child costs 3 packed fmas instead of 6 and a node step 65 VALU
+// instead of 89 (each half rounds once, as fmaf: the same bits).  Measured
+// slower (round 6, one box, three interleaved 20-step pairs): 17.15 / 17.52
+// / 17.19 vs 17.88 / 17.93 / 17.96 Grays/s (−3.5%); round 1's plane pairs
+// measured ±0.  Fewer VALU per node step do not shorten it.
 #ifndef RT_PK_SLAB
-#define RT_PK_SLAB 1
+#define RT_PK_SLAB 0
 #endif
 template <int W, int OCT>
 __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32& q, const f2 nox, const f2 noy,
@@ -1272,13 +1276,20 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
 #else
     (void)pending;
 #endif
-    // The exit ticket is a release (agent scope: the wave's partial adds,
-    // including the redo path's, are performed before it) and the last wave
-    // acquires before it reads the partials (HIP memory model: relaxed
-    // atomics alone would not order the partials of another XCD's wave
-    // before its ticket).  RT_EXIT_FENCE=0: relaxed, the waits only.
+    // Ordering of the partials before the exit ticket.  Every value the
+    // waves exchange here (hit partials, redo entries, claim and ticket
+    // counters) is written and read by device-scope atomic RMWs, which
+    // gfx950 performs at the memory side, past the XCDs' L2s; a wave's
+    // `s_waitcnt vmcnt(0)` before its ticket waits until its own atomics are
+    // performed, so the last ticket holder's atomicExch reads see them all.
+    // The HIP memory model would ask for a release ticket and an acquire in
+    // the last wave; at agent scope those compile to an L2 write-back per
+    // exiting wave (7,168 per launch) and an L2 invalidate, and measured
+    // (RT_EXIT_FENCE=1, round 6, one box, 20-step runs): 16.96 / 17.38 G in
+    // the good runs but 3.7 and 0.76 Grays/s in two of six — sporadic
+    // whole-launch stalls — against 17.08-17.14 in every run without them.
     uint32_t tk = 0;
-#if !defined(RT_EXIT_FENCE) || RT_EXIT_FENCE
+#if defined(RT_EXIT_FENCE) && RT_EXIT_FENCE
     if (lane == 0)
         tk = __hip_atomic_fetch_add(ctr + RT_EXIT_COUNT, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) + 1u;
 #else
@@ -1286,7 +1297,7 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
     if (lane == 0) tk = atomicAdd(ctr + RT_EXIT_COUNT, 1u) + 1u;
 #endif
     if (uni(tk) != gridDim.x * (uint32_t)kPacketWaves) return;
-#if !defined(RT_EXIT_FENCE) || RT_EXIT_FENCE
+#if defined(RT_EXIT_FENCE) && RT_EXIT_FENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
     // the last wave: per pose, the 64 spread partials (one per lane) summed,
@@ -1294,18 +1305,34 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
     A = launder(A);
     const int poses = kword(&A->fp.nframes) / kword(&A->fp.spp);
     RT_G unsigned long long* const hc = kload(&A->fp.hit_count);
+#if !defined(RT_STORE_COUNTS) || RT_STORE_COUNTS
     const bool store = (kword(&A->aux.self_fix) & RT_SELF_STORE) != 0;
-    uint32_t part[RT_MAX_BATCH];
+#else
+    const bool store = false;  // (bisection build: always add)
+#endif
+    // (poses in groups of 12, each group's exchanges in flight together:
+    // three round trips for 36 poses, 12 registers — an unrolled 36-entry
+    // array went to the private segment, 144 B per lane)
+#ifndef RT_FOLD_GROUP
+#define RT_FOLD_GROUP 12
+#endif
+    constexpr int kFold = RT_FOLD_GROUP;
+    for (int m0 = 0; m0 < poses; m0 += kFold) {
+        uint32_t part[kFold];
 #pragma unroll
-    for (int m = 0; m < RT_MAX_BATCH; m++)
-        part[m] = m < poses ? atomicExch(ctr + RT_HIT_BASE + (m * RT_HIT_SLOTS + lane) * RT_QUEUE_STRIDE, 0u) : 0u;
+        for (int k = 0; k < kFold; k++)
+            part[k] = m0 + k < poses
+                          ? atomicExch(ctr + RT_HIT_BASE + ((m0 + k) * RT_HIT_SLOTS + lane) * RT_QUEUE_STRIDE, 0u)
+                          : 0u;
 #pragma unroll
-    for (int m = 0; m < RT_MAX_BATCH; m++) {
-        if (m >= poses) break;
-        const uint32_t s = wave_sum_u32(part[m]);
-        if (lane == 0 && hc) {
-            if (store) __hip_atomic_store(hc + m, (unsigned long long)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else if (s) atomicAdd(hc + m, (unsigned long long)s);
+        for (int k = 0; k < kFold; k++) {
+            const uint32_t s = wave_sum_u32(part[k]);
+            if (m0 + k < poses && lane == 0 && hc) {
+                if (store)
+                    __hip_atomic_store(hc + m0 + k, (unsigned long long)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (s)
+                    atomicAdd(hc + m0 + k, (unsigned long long)s);
+            }
         }
     }
     if (lane < RT_QUEUES) {
@@ -1323,6 +1350,10 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
         (void)atomicExch(ctr + RT_EXIT_COUNT, 0u);
     }
 }
+
+#ifndef RT_SCRATCH_PAD
+#define RT_SCRATCH_PAD 4096
+#endif
 
 // JOB: the launch carries a side de-interleave job (RtLaunchAux::job_*; its
 // own instantiation, so the kernels without one keep their registers).
@@ -1440,6 +1471,21 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
                   hacc);
     if constexpr (FUSED)
         if (kword(&launder(A)->aux.self_fix)) packet_exit<W, K, COUNT>(A, cands[wv], lane);
+#if RT_SCRATCH_PAD > 0
+    // RT_SCRATCH_PAD bytes of private segment per lane, touched only on a
+    // path no launch takes.  The HIP runtime manages a dispatch's scratch by
+    // its size: with the kernel's own 408 B (or 20 B in a 6-wave build) two
+    // streams' overlapped launches slowed the device 4-70x in most runs (31
+    // of 37, round 6); with 4.5 KB per lane — round 5's frame size, which
+    // round 5 had by accident — 6 of 6 ran at full speed, with or without
+    // a zero fill between launches.  Never read or written in
+    // a real launch: the cost is the runtime's scratch reservation only.
+    if (kword(&launder(A)->fp.W) == -12345) {
+        volatile uint32_t pad[RT_SCRATCH_PAD / 4];
+        pad[lane % (RT_SCRATCH_PAD / 4)] = (uint32_t)lane;
+        pad[(lane * 7) % (RT_SCRATCH_PAD / 4)] += 1u;
+    }
+#endif
 }
 
 // v_mbcnt_lo_u32_b32: bits of m set below this lane (lanes 0-31; m = ~0: the

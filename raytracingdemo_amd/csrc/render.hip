@@ -1248,6 +1248,16 @@ __global__ void __launch_bounds__(256) k_deinterleave(RtLaunchAux a) {
     }
 }
 
+// The overlap gate (rt_api.cpp launch): one wave that asks for 32 VGPRs per
+// lane and does nothing.  Issued on a stream right before a persistent
+// traversal grid while another stream's grid may still hold the device, it
+// cannot start until a wave of that grid has exited (7 traversal waves per
+// SIMD leave 8 of the 512 VGPRs free), so the new grid is dispatched into the
+// other one's tail instead of beside all of it (two whole
+// persistent grids resident at once on two queues slowed the device 4-70x in
+// most runs).
+__global__ void __launch_bounds__(64) k_gate() { asm volatile("v_mov_b32 v31, 0" ::: "v31"); }
+
 // Per-frame hit counts of the G shards (u64 [F] at cnt_off of each block) added
 // to the caller's counters (store: written over them, RT_FLAG_COUNTS_STORE).
 __global__ void k_sum_counts(const uint8_t* __restrict__ gather, uint64_t block, uint64_t cnt_off, int G, int F,
@@ -1279,6 +1289,11 @@ hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_
 hipError_t launch_job(const RtLaunchAux& a, hipStream_t s) {
     if (!a.job_src || a.job_F <= 0 || a.job_H <= 0 || a.job_W <= 0 || a.job_G <= 0 || a.job_eb <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)((uint64_t)a.job_F * a.job_H)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gate(hipStream_t s) {
+    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, s);
     return hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ hipError_t launch_deinterleave(const void* gather, uint64_t block, uint64_t sec_
 hipError_t launch_sum_counts(const void* gather, uint64_t block, uint64_t cnt_off, int G, int F,
                              unsigned long long* out, bool store, hipStream_t s);
 hipError_t launch_job(const RtLaunchAux& a, hipStream_t s);
+hipError_t launch_gate(hipStream_t s);
 }
 
 namespace {
@@ -733,6 +734,16 @@ void launch(const rt_scene* s, Replica& r, Slot& q, const RtFrameParams& fp, int
     // RT_FLAG_SIDE_SLOT: one workgroup slot per CU left to other streams
     if (side_slot && r.pgrid > r.cus) a.pgrid = r.pgrid - r.cus;
     set_job(a, job);
+    // The overlap gate: when the replica's other slot last launched on
+    // another stream, its persistent grid may still hold every CU; a gate
+    // kernel on this stream first lets this launch's grid start only in that
+    // grid's tail (render.hip k_gate).  RT_OVERLAP_GATE=0
+    // (read per call) turns it off.
+    {
+        const Slot& other = &q == &r.slot[0] ? r.slot[1] : r.slot[0];
+        const char* g = std::getenv("RT_OVERLAP_GATE");
+        if (other.used && other.last != st && !(g && g[0] == '0')) HIP_TRY(rt::launch_gate(st));
+    }
     if (a.job_src) {
         const bool empty = fp.W <= 0 || fp.nrows <= 0 || fp.nframes <= 0;
         (!empty && rt::packet_takes_job(r.dev, fp, mode, count) ? r.jobs_fused : r.jobs_kernel)++;

@@ -87,10 +87,27 @@ for s in $STEPS; do
                for rep in $(seq 1 ${VAB_REPS:-2}); do
                    for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
                        n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}
-                       RT_LIB=${v:+$PWD/$v} run "vab_${n}_$rep" 300 python bench.py --no-cpu --no-dropin --steps ${AB_STEPS:-20} \
+                       RT_LIB=${v:+$PWD/$v} run "vab${VAB_TAG:-}_${n}_$rep" 300 python bench.py --no-cpu --no-dropin --steps ${AB_STEPS:-20} \
                            --shard-of ${AB_SHARD:-1} || exit 1
-                       python -c "import json; l=[x for x in open('gpurun_out/vab_${n}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']; print('RESULT', '$n', $rep, d['value'], d['ms_per_step'], r['kernel_ms_avg'], r['kernel_ms_span_avg'])" || true
+                       python -c "import json; l=[x for x in open('gpurun_out/vab${VAB_TAG:-}_${n}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']; print('RESULT', '${VAB_TAG:-}', '$n', $rep, d['value'], d['ms_per_step'], r['kernel_ms_avg'], r['kernel_ms_span_avg'])" || true
                    done
+               done ;;
+        stall) # stall hunt: STALL_RUNS entries "label|env|args" (env/args may be empty), STALL_REPS rounds
+               IFS=';' read -ra cfgs <<< "${STALL_RUNS:?}"
+               for rep in $(seq 1 ${STALL_REPS:-3}); do
+                   for c in "${cfgs[@]}"; do
+                       IFS='|' read -r lab envs args <<< "$c"
+                       env $envs timeout -k 10 300 python bench.py --no-cpu --no-dropin --steps ${AB_STEPS:-20} $args \
+                           > gpurun_out/stall_${lab}_$rep.log 2>&1
+                       rc=$?; echo "stall_${lab}_$rep exit=$rc"; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/stall_${lab}_$rep.log; exit $rc; }
+                       python -c "import json; l=[x for x in open('gpurun_out/stall_${lab}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); print('RESULT', '$lab', $rep, d['value'], d['ms_per_step'], d['settle_steps'])" || true
+                   done
+               done ;;
+        cold)  # first-launch cost in fresh processes: the shipped library and every variant (tools/cold_launch.py)
+               for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
+                   n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}
+                   RT_LIB=${v:+$PWD/$v} run "cold_$n" 600 python tools/cold_launch.py --reps ${COLD_REPS:-4} \
+                       --out gpurun_out/cold_$n.json || exit 1
                done ;;
         vshards) for v in raytracingdemo_amd/variants/librtmi355x_*.so; do
                       n=$(basename "$v" .so); RT_LIB=$PWD/$v run "bench_${n#librtmi355x_}_s8" 300 \

@@ -167,6 +167,46 @@ __device__ __forceinline__ uint32_t q_append(const PathQs& q, int k, int x, int 
     return slot;
 }
 
+// RT_Q_NR_LDS (k_q_segment): the bounce ray's vertex and direction cross
+// q_append's atomic in the lane's LDS ring (entries 0-5) rather than in
+// registers; q_append_ring<true> writes the entry from there.
+#ifndef RT_Q_NR_LDS
+#define RT_Q_NR_LDS 1
+#endif
+__device__ __forceinline__ uint2 dbits(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    return make_uint2((uint32_t)u, (uint32_t)(u >> 32));
+}
+__device__ __forceinline__ double bitsd(uint2 v) {
+    return __longlong_as_double((long long)(((unsigned long long)v.y << 32) | v.x));
+}
+// (ends the live ranges of values already stashed: nothing is carried in
+// registers across the barrier the compiler could not see through)
+__device__ __forceinline__ void opaque_regs() { asm volatile("" ::: "memory"); }
+template <bool RING>
+__device__ __forceinline__ uint32_t q_append_ring(const PathQs& q, int k, int x, int b, bool emit, const Ray64& nr,
+                                                  uint32_t path, uint2 (*ring)[256], int tid) {
+    if constexpr (!RING) {
+        return q_append(q, k, x, b, emit, nr, path);
+    } else {
+        const uint64_t em = __ballot(emit);
+        if (em == 0) return 0;
+        const int lane = (int)(threadIdx.x & 63);
+        const int leader = __builtin_ctzll(em);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(qc_emit(q, b, x), (uint32_t)__builtin_popcountll(em));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader) + (uint32_t)x * q.pcap;
+        const uint32_t slot = base + (uint32_t)__builtin_popcountll(em & ((1ull << lane) - 1ull));
+        if (emit) {
+            RT_G double* p = q_entry(q, k, slot);
+#pragma unroll
+            for (int c = 0; c < 6; c++) p[c] = bitsd(ring[c][tid]);
+            p[9] = __longlong_as_double((long long)path);
+        }
+        return slot;
+    }
+}
+
 // q_append for one lane (the fall-back kernel: lanes of a wave append to
 // different partitions, ~1e-4 of the rays).
 __device__ __forceinline__ uint32_t q_append_lane(const PathQs& q, int k, int x, int b, bool emit, const Ray64& nr,
@@ -219,6 +259,35 @@ __device__ __forceinline__ void q_bounce(const RtDevScene& sc, const RtFramePara
     nr.ox = px;
     nr.oy = py;
     nr.oz = pz;
+}
+
+// q_bounce with RING: the hit point goes to the lane's LDS ring (entries 0-2)
+// as soon as it is known and the bounce direction after it (3-5), for
+// q_append_ring<true>; px, py, pz are reloaded from the ring by the caller.
+template <bool RING>
+__device__ __forceinline__ void q_bounce_ring(const RtDevScene& sc, const RtFrameParams& fp, uint32_t frame, int b,
+                                              int bounces, const Ray64& ray, const Win& win, uint32_t path,
+                                              double& px, double& py, double& pz, bool& emit, Ray64& nr,
+                                              uint2 (*ring)[256], int tid) {
+    if constexpr (!RING) {
+        q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
+    } else {
+        double hx, hy, hz;
+        (void)hit_dist(ray, win.t, hx, hy, hz);
+        ring[0][tid] = dbits(hx);
+        ring[1][tid] = dbits(hy);
+        ring[2][tid] = dbits(hz);
+        emit = b < bounces;
+        if (!emit) return;
+        const RT_G double* T = sc.tri64 + RT_TRI64_DOUBLES * (size_t)win.tri;
+        const uint32_t seed = q_seed(fp, frame, path);
+        double dx, dy, dz;
+        bounce_dir(T[RT_T64_NORMAL], T[RT_T64_NORMAL + 1], T[RT_T64_NORMAL + 2], ray.dx, ray.dy, ray.dz,
+                   path_u(seed, 2u + 2u * (uint32_t)b), path_u(seed, 3u + 2u * (uint32_t)b), dx, dy, dz);
+        ring[3][tid] = dbits(dx);
+        ring[4][tid] = dbits(dy);
+        ring[5][tid] = dbits(dz);
+    }
 }
 
 // Second half: the vertex adds 0.5^b of its shadeScreen colour to the path's
@@ -991,13 +1060,32 @@ __global__ void __launch_bounds__(256) RT_Q_ATTR k_q_segment(RtDevScene sc, RtFr
                 qs.Lfin[3 * (size_t)e] = win.t + win.tri + (fall ? 1.0 : 0.0);
                 continue;
             }
+            if constexpr (RT_Q_NR_LDS != 0) {
+                // the vertex (and below, the bounce direction) wait out the
+                // bounce direction's divisions and q_append's atomic in the
+                // lane's LDS stack ring (free once the walk is over: entries
+                // 0-5 of its column) instead of in registers — at 80 VGPRs the
+                // compiler spilled them to scratch there, once per ray
+                lds[0][tid] = dbits(0.0);
+                lds[1][tid] = dbits(0.0);
+                lds[2][tid] = dbits(0.0);
+            }
             if (fall) {
                 qs.fb[qin * (size_t)qs.cap + atomicAdd(qc_fb(qs, b), 1u)] = fe;
             } else if (win.tri >= 0) {
-                q_bounce(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr);
+                q_bounce_ring<RT_Q_NR_LDS != 0>(sc, fp, frame, b, bounces, ray, win, path, px, py, pz, emit, nr, lds,
+                                                tid);
             }
         }
-        const uint32_t slot = q_append(qs, qout, x, b, emit, nr, path);
+        if constexpr (RT_Q_NR_LDS != 0) opaque_regs();
+        const uint32_t slot = q_append_ring<RT_Q_NR_LDS != 0>(qs, qout, x, b, emit, nr, path, lds, tid);
+        if constexpr (RT_Q_NR_LDS != 0) {
+            if (act) {
+                px = bitsd(lds[0][tid]);
+                py = bitsd(lds[1][tid]);
+                pz = bitsd(lds[2][tid]);
+            }
+        }
         bool qd = false;
         uint32_t dst = 0;
         if (act && !fall)

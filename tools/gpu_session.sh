@@ -103,6 +103,13 @@ for s in $STEPS; do
                        python -c "import json; l=[x for x in open('gpurun_out/stall_${lab}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); print('RESULT', '$lab', $rep, d['value'], d['ms_per_step'], d['settle_steps'])" || true
                    done
                done ;;
+        pwrite) # c5 WRITE_SIZE per kernel (one counted + 2 timed poses) for the shipped library and every variant
+               for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
+                   n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}
+                   RT_LIB=${v:+$PWD/$v} run "pw_$n" 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pw_$n \
+                       -o w -- python bench.py --paths --steps 1 --warmup 0 --no-cpu || exit 1
+                   python tools/pmc_kernels.py gpurun_out/pw_$n/w_counter_collection.csv --per 2 > gpurun_out/pw_$n.txt || true
+               done ;;
         cold)  # first-launch cost in fresh processes: the shipped library and every variant (tools/cold_launch.py)
                for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
                    n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}

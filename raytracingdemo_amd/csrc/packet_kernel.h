@@ -627,6 +627,21 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
 #pragma unroll
                     for (int c = 0; c < W; c++) rs[c] = ch[c].pad;  // ref | meta << 24 (bvh_build.cpp flatten)
                     mask = node_mask<W, OCT>(bx, q, nox, noy, noz, tcull, nv);
+#if defined(RT_DBL_NODE) && RT_DBL_NODE
+                    {   // (measurement build: the child test twice, the second on an
+                        // opaque copy of tcull so it is not merged; its cost is the
+                        // node test's dynamic instruction count, tools/phase_counts.py)
+                        // (opaque copies of every lane input: no part of the
+                        // second test can be shared with the first)
+                        float t2 = tcull;
+                        Ray32 q2 = q;
+                        f2 nx2 = nox, ny2 = noy, nz2 = noz;
+                        asm volatile("" : "+v"(t2), "+v"(q2.ix), "+v"(q2.iy), "+v"(q2.iz), "+v"(nx2), "+v"(ny2),
+                                     "+v"(nz2));
+                        const uint32_t m2 = node_mask<W, OCT>(bx, q2, nx2, ny2, nz2, t2, nv);
+                        asm volatile("" ::"s"(m2));
+                    }
+#endif
                 }
                 if (COUNT) w_empty += mask == 0;
                 if (mask != 0) {
@@ -687,6 +702,18 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                         const int cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz,
                                                              q.co, tcull, tl, tu)
                                               : 0;
+#if defined(RT_DBL_LEAF) && RT_DBL_LEAF
+                        {   // (measurement build: the triangle filter twice, tools/phase_counts.py)
+                            float t2 = tcull, tl2 = 0.f, tu2 = 0.f;
+                            float ox2 = q.ox, oy2 = q.oy, oz2 = q.oz, dx2 = q.dx, dy2 = q.dy, dz2 = q.dz, co2 = q.co;
+                            asm volatile("" : "+v"(t2), "+v"(ox2), "+v"(oy2), "+v"(oz2), "+v"(dx2), "+v"(dy2), "+v"(dz2),
+                                         "+v"(co2));
+                            const int c2 = valid ? tri_classify(TA[t], TB[t], TC[t], ox2, oy2, oz2, dx2, dy2, dz2, co2,
+                                                                t2, tl2, tu2)
+                                                 : 0;
+                            asm volatile("" ::"v"(c2), "v"(tl2), "v"(tu2));
+                        }
+#endif
                         if (__ballot(cls != 0) == 0) continue;
                         if (cls != 0) {
                             // dist of a certain hit <= (tu + slack)(1 + 2^-20)

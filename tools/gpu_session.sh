@@ -103,6 +103,21 @@ for s in $STEPS; do
                        python -c "import json; l=[x for x in open('gpurun_out/stall_${lab}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); print('RESULT', '$lab', $rep, d['value'], d['ms_per_step'], d['settle_steps'])" || true
                    done
                done ;;
+        phases) # dynamic per-phase instruction counts (tools/phase_counts.py): shipped, split walk, and the
+               # phase-doubled measurement builds variants/librtmi355x_dblnode.so / _dblleaf.so
+               PMC="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_WAVES GRBM_GUI_ACTIVE"
+               for cfg in base split dblnode dblleaf; do
+                   case $cfg in
+                       base) e="X=1" ;; split) e="RT_RESOLVE=split" ;;
+                       *) e="RT_LIB=$PWD/raytracingdemo_amd/variants/librtmi355x_$cfg.so" ;;
+                   esac
+                   env $e timeout -k 10 600 rocprofv3 --pmc $PMC --output-format csv -d gpurun_out/ph_$cfg -o p \
+                       -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin > gpurun_out/ph_$cfg.log 2>&1
+                   rc=$?; echo "ph_$cfg exit=$rc"; [ $rc -ne 0 ] && { tail -n 5 gpurun_out/ph_$cfg.log; exit $rc; }
+               done
+               python tools/phase_counts.py gpurun_out/phase_counts.txt base=gpurun_out/ph_base/p_counter_collection.csv \
+                   split=gpurun_out/ph_split/p_counter_collection.csv dblnode=gpurun_out/ph_dblnode/p_counter_collection.csv \
+                   dblleaf=gpurun_out/ph_dblleaf/p_counter_collection.csv --stats=gpurun_out/ph_base.log ;;
         pwrite) # c5 WRITE_SIZE per kernel (one counted + 2 timed poses) for the shipped library and every variant
                for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
                    n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}

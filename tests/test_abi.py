@@ -56,7 +56,7 @@ def test_status_codes_match_header():
     src = open(HEADER).read()
     for name in ("RT_OK", "RT_ERR_INVALID_ARGUMENT", "RT_ERR_OUT_OF_RANGE", "RT_ERR_RUNTIME", "RT_ERR_HIP",
                  "RT_ERR_NO_DEVICE", "RT_MODE_EXACT", "RT_MODE_FP64", "RT_FLAG_COUNT", "RT_FLAG_TIMING",
-                 "RT_FLAG_SHADOW", "RT_FLAG_SIDE_SLOT"):
+                 "RT_FLAG_SHADOW", "RT_FLAG_SIDE_SLOT", "RT_FLAG_COUNTS_STORE"):
         v = int(re.search(rf"#define {name} (\d+)", src).group(1))
         assert getattr(N, name) == v, name
 

@@ -173,6 +173,7 @@ __device__ __forceinline__ uint32_t q_append(const PathQs& q, int k, int x, int 
 #ifndef RT_Q_NR_LDS
 #define RT_Q_NR_LDS 1
 #endif
+static_assert(RT_Q_NR_LDS == 0 || RT_Q_STACK >= 6, "the bounce stash takes entries 0-5 of the LDS ring");
 __device__ __forceinline__ uint2 dbits(double v) {
     const unsigned long long u = (unsigned long long)__double_as_longlong(v);
     return make_uint2((uint32_t)u, (uint32_t)(u >> 32));

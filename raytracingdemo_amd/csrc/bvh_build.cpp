@@ -523,9 +523,21 @@ struct Flattener {
     uint32_t alloc_node() {
         uint32_t id = (uint32_t)f.n_wide++;
         f.wide.resize(f.n_wide * nb, 0);
-        // empty slot: zero box, ref RT_INVALID_REF (the kernels mask it out)
+        // empty slot: an inverted box (lo = +inf, hi = -inf on every axis)
+        // and ref RT_INVALID_REF.  A slab test that takes each axis's near
+        // plane by the ray's direction sign (the packet walks' per-octant
+        // tests) fails it for every ray, so those walks need not mask the
+        // slots past the node's valid count; the general test and the
+        // per-lane walks still check the count or the ref
         uint32_t* p = reinterpret_cast<uint32_t*>(f.wide.data() + (size_t)id * nb);
-        for (int c = 0; c < W; c++) p[8 * c + RT_CHILD_REF] = RT_INVALID_REF;
+        for (int c = 0; c < W; c++) {
+            float* b = reinterpret_cast<float*>(p + 8 * c);
+            for (int a = 0; a < 3; a++) {
+                b[2 * a] = std::numeric_limits<float>::infinity();
+                b[2 * a + 1] = -std::numeric_limits<float>::infinity();
+            }
+            p[8 * c + RT_CHILD_REF] = RT_INVALID_REF;
+        }
         return id;
     }
     // one 32-B child record: lo.x hi.x lo.y hi.y lo.z hi.z ref pad

@@ -157,6 +157,57 @@ __device__ __forceinline__ int tri_classify(const float4 A, const float4 B, cons
     return 2;
 }
 
+// tri_classify with one divergent branch instead of a nest: the same
+// expressions and the same class / bounds (every class-1 and class-2 lane
+// computes what tri_classify computes for it; a class-0 lane's tl / tu are
+// unused).  The rejection tests are evaluated for every lane, the bounds
+// only under `any lane survives`; the certain / borderline split is a
+// select.  For the packet walk, where a wave skips a triangle as a whole
+// only when all 64 rays reject it, each nested level of tri_classify cost
+// an exec save, a branch and an exec restore per triangle record.
+__device__ __forceinline__ int tri_classify_flat(const float4 A, const float4 B, const float4 C, float ox, float oy,
+                                                 float oz, float dx, float dy, float dz, float co, float tcull,
+                                                 float& tl, float& tu) {
+    const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = C.x;
+    const float M1 = C.y, M2 = C.z, Cv = C.w;
+    const float sx = ox - A.x, sy = oy - A.y, sz = oz - A.z;
+    const float hx = __builtin_fmaf(dy, e2z, -dz * e2y);
+    const float hy = __builtin_fmaf(dz, e2x, -dx * e2z);
+    const float hz = __builtin_fmaf(dx, e2y, -dy * e2x);
+    const float a = __builtin_fmaf(e1x, hx, __builtin_fmaf(e1y, hy, e1z * hz));
+    const float U = __builtin_fmaf(sx, hx, __builtin_fmaf(sy, hy, sz * hz));
+    const float qx = __builtin_fmaf(sy, e1z, -sz * e1y);
+    const float qy = __builtin_fmaf(sz, e1x, -sx * e1z);
+    const float qz = __builtin_fmaf(sx, e1y, -sy * e1x);
+    const float V = __builtin_fmaf(dx, qx, __builtin_fmaf(dy, qy, dz * qz));
+    const float T = __builtin_fmaf(e2x, qx, __builtin_fmaf(e2y, qy, e2z * qz));
+    const float Ms = fmaxf(fmaxf(__builtin_fabsf(sx), __builtin_fabsf(sy)), __builtin_fabsf(sz));
+    const float u = 0x1p-24f;
+    const float G = __builtin_fmaf(256.f, Ms, 64.f * (co + Cv));
+    const float errA = 256.f * u * M1 * M2;
+    const float errU = u * M2 * G, errV = u * M1 * G, errT = u * M1 * M2 * G;
+    const float aa = __builtin_fabsf(a);
+    const bool sure = aa > errA;  // else the sign of the determinant is uncertain: class 1
+    const float sg = a > 0.f ? 1.f : -1.f;
+    const float Us = sg * U, Vs = sg * V, Ts = sg * T;
+    // (bitwise & and |: no short-circuit branches)
+    const bool rej = sure & ((Us < -errU) | (Vs < -errV) | (Ts < -errT) | (Us + Vs > aa + errU + errV + errA) |
+                             (Ts - errT > tcull * (aa + errA)));
+    tl = 0.f;
+    tu = __builtin_huge_valf();
+    int cls = rej ? 0 : 1;
+    if (sure & !rej) {
+        tl = fmaxf((Ts - errT) * __builtin_amdgcn_rcpf(aa + errA), 0.f) * (1.f - 0x1p-20f);
+        const float EPS = 1e-8f;
+        const bool certain = (Us >= errU) & (Vs >= errV) & (Us + Vs <= aa - errU - errV - errA) &
+                             (aa - errA >= 2.f * EPS) & (Ts - errT >= 2.f * EPS * (aa + errA));
+        const float tuv = (Ts + errT) * __builtin_amdgcn_rcpf(aa - errA) * (1.f + 0x1p-20f);
+        tu = certain ? tuv : tu;
+        cls = certain ? 2 : 1;
+    }
+    return cls;
+}
+
 // Pose of sample frame f with its sub-pixel offset: sample q = f mod spp of
 // an n x n pattern at ((q mod n) + 0.5) / n, ((q div n) + 0.5) / n — the
 // host's expressions (rt_api.cpp frame_params), so the doubles are the same;

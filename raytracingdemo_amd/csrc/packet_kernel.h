@@ -332,6 +332,11 @@ __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32&
 #ifndef RT_EMPTY_INVERTED
 #define RT_EMPTY_INVERTED 1
 #endif
+// The leaf filter as tri_classify_flat (kernels_common.h: one divergent
+// branch per triangle record instead of a nest of five).  0: tri_classify.
+#ifndef RT_FLAT_CLASSIFY
+#define RT_FLAT_CLASSIFY 1
+#endif
 template <int W, int OCT>
 __device__ __forceinline__ uint32_t node_mask(const float (&bx)[W][6], const Ray32& q, const f2 nox, const f2 noy,
                                               const f2 noz, float tcull, uint32_t nv) {
@@ -738,9 +743,18 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                         if (k >= end) break;
                         if (COUNT) n_pre += valid;
                         float tl, tu;
-                        const int cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz,
-                                                             q.co, tcull, tl, tu)
-                                              : 0;
+                        int cls;
+                        if constexpr (RT_FLAT_CLASSIFY != 0) {
+                            // (an invalid lane holds pixel 0's finite ray: its
+                            // class is computed and dropped by a select, not
+                            // branched around)
+                            cls = tri_classify_flat(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co,
+                                                    tcull, tl, tu);
+                            cls = valid ? cls : 0;
+                        } else
+                            cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co,
+                                                       tcull, tl, tu)
+                                        : 0;
 #if defined(RT_DBL_LEAF) && RT_DBL_LEAF
                         {   // (measurement build: the triangle filter twice, tools/phase_counts.py)
                             float t2 = tcull, tl2 = 0.f, tu2 = 0.f;
@@ -753,7 +767,8 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                             asm volatile("" ::"v"(c2), "v"(tl2), "v"(tu2));
                         }
 #endif
-                        if (__ballot(cls != 0) == 0) continue;
+                        // (no `continue`: in the unrolled chunk loop each one
+                        // cost the structurizer a flow variable and its tests)
                         if (cls != 0) {
                             // dist of a certain hit <= (tu + slack)(1 + 2^-20)
                             if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
@@ -761,25 +776,25 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                             if (nc < K) {
                                 cand[nc * 64 + lane] = make_uint2(k, __float_as_uint(tl));
                                 nc++;
-                                continue;
-                            }
-                            // LDS list full: append to the lane's overflow
-                            // chunk, taking one from the pool on first need
-                            const args_p A2 = launder(A);  // (A itself stays uniform)
-                            if (chunk == kNoChunk) {
-                                const uint32_t c = atomicAdd(kload(&A2->aux.tile_ctr) + RT_POOL_COUNT, 1u);
-                                chunk = c < kword(&A2->aux.pool_chunks) ? c : kPoolDry;
-                            }
-                            if (chunk != kPoolDry && nsp < RT_POOL_CHUNK) {
-                                RT_G uint2* const pool = reinterpret_cast<RT_G uint2*>(kload(&A2->aux.pool));
-                                pool[(size_t)chunk * RT_POOL_CHUNK + nsp] = make_uint2(k, __float_as_uint(tl));
-                                nsp++;
                             } else {
-                                // full: keep the K smallest lower bounds, remember
-                                // the smallest bound dropped (the resolve certifies
-                                // the winner against it, else the pixel is redone
-                                // exactly)
-                                drop = fminf(drop, keep_nearest<K>(cand, lane, k, tl));
+                                // LDS list full: append to the lane's overflow
+                                // chunk, taking one from the pool on first need
+                                const args_p A2 = launder(A);  // (A itself stays uniform)
+                                if (chunk == kNoChunk) {
+                                    const uint32_t c = atomicAdd(kload(&A2->aux.tile_ctr) + RT_POOL_COUNT, 1u);
+                                    chunk = c < kword(&A2->aux.pool_chunks) ? c : kPoolDry;
+                                }
+                                if (chunk != kPoolDry && nsp < RT_POOL_CHUNK) {
+                                    RT_G uint2* const pool = reinterpret_cast<RT_G uint2*>(kload(&A2->aux.pool));
+                                    pool[(size_t)chunk * RT_POOL_CHUNK + nsp] = make_uint2(k, __float_as_uint(tl));
+                                    nsp++;
+                                } else {
+                                    // full: keep the K smallest lower bounds, remember
+                                    // the smallest bound dropped (the resolve certifies
+                                    // the winner against it, else the pixel is redone
+                                    // exactly)
+                                    drop = fminf(drop, keep_nearest<K>(cand, lane, k, tl));
+                                }
                             }
                         }
                     }

@@ -92,6 +92,15 @@ for s in $STEPS; do
                        python -c "import json; l=[x for x in open('gpurun_out/vab${VAB_TAG:-}_${n}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']; print('RESULT', '${VAB_TAG:-}', '$n', $rep, d['value'], d['ms_per_step'], r['kernel_ms_avg'], r['kernel_ms_span_avg'])" || true
                    done
                done ;;
+        pab)   # config c5 A/B, interleaved: the shipped library and every variant, VAB_REPS rounds
+               for rep in $(seq 1 ${VAB_REPS:-2}); do
+                   for v in "" raytracingdemo_amd/variants/librtmi355x_*.so; do
+                       n=$(basename "${v:-librtmi355x_base}" .so); n=${n#librtmi355x_}
+                       RT_LIB=${v:+$PWD/$v} run "pab${VAB_TAG:-}_${n}_$rep" 300 python bench.py --paths --no-cpu --steps 3 \
+                           --warmup 1 || exit 1
+                       python -c "import json; l=[x for x in open('gpurun_out/pab${VAB_TAG:-}_${n}_$rep.log') if x.startswith('{')][-1]; d=json.loads(l); print('RESULT paths', '$n', $rep, d['value'], d['ms_per_step'])" || true
+                   done
+               done ;;
         stall) # stall hunt: STALL_RUNS entries "label|env|args" (env/args may be empty), STALL_REPS rounds
                IFS=';' read -ra cfgs <<< "${STALL_RUNS:?}"
                for rep in $(seq 1 ${STALL_REPS:-3}); do

@@ -135,7 +135,7 @@ def main():
     node_start = first_node
     while node_start > 0 and ins[node_start - 1][1] in ("s_lshl_b32", "s_cbranch_scc1", "s_cmp_lt_i32"):
         node_start -= 1
-    first_leaf = next(k for k in range(node_end, len(ins)) if ins[k][1] == "s_load_dwordx16" and phase_of[k] == 1)
+    first_leaf = next(k for k in range(node_end, len(ins)) if ins[k][1].startswith("s_load_dword") and phase_of[k] == 1)
     # the leaf loop of copy 0 runs to the next priority change (the return
     # to the node steps)
     leaf_end = next(k for k in range(first_leaf, len(ins)) if ins[k][1] == "s_setprio") - 1

@@ -116,9 +116,9 @@ __device__ __forceinline__ bool tri_prefilter(const float4 A, const float4 B, co
 //      budget beyond the real value — far above fp64 rounding), so the true
 //      hit parameter is <= tu and tu may tighten the culling distance.
 // tl / tu bound the true t = T/a from below / above whenever class != 0.
-__device__ __forceinline__ int tri_classify(const float4 A, const float4 B, const float4 C, float ox, float oy,
-                                            float oz, float dx, float dy, float dz, float co, float tcull, float& tl,
-                                            float& tu) {
+__device__ __forceinline__ int tri_classify_nest(const float4 A, const float4 B, const float4 C, float ox,
+                                                 float oy, float oz, float dx, float dy, float dz, float co,
+                                                 float tcull, float& tl, float& tu) {
     const float e1x = A.w, e1y = B.x, e1z = B.y, e2x = B.z, e2y = B.w, e2z = C.x;
     const float M1 = C.y, M2 = C.z, Cv = C.w;
     const float sx = ox - A.x, sy = oy - A.y, sz = oz - A.z;
@@ -206,6 +206,21 @@ __device__ __forceinline__ int tri_classify_flat(const float4 A, const float4 B,
         cls = certain ? 2 : 1;
     }
     return cls;
+}
+
+// The per-lane walks' filter (render.hip LaneWalk, path_kernel.h,
+// queue_paths.h): tri_classify_flat unless RT_CLASSIFY_FLAT=0 (the nest).
+// The packet walk picks its own (packet_kernel.h RT_FLAT_CLASSIFY).
+#ifndef RT_CLASSIFY_FLAT
+#define RT_CLASSIFY_FLAT 1
+#endif
+__device__ __forceinline__ int tri_classify(const float4 A, const float4 B, const float4 C, float ox, float oy,
+                                            float oz, float dx, float dy, float dz, float co, float tcull, float& tl,
+                                            float& tu) {
+    if constexpr (RT_CLASSIFY_FLAT != 0)
+        return tri_classify_flat(A, B, C, ox, oy, oz, dx, dy, dz, co, tcull, tl, tu);
+    else
+        return tri_classify_nest(A, B, C, ox, oy, oz, dx, dy, dz, co, tcull, tl, tu);
 }
 
 // Pose of sample frame f with its sub-pixel offset: sample q = f mod spp of

@@ -333,7 +333,7 @@ __device__ __forceinline__ void child_hits(const float (&bx)[W][6], const Ray32&
 #define RT_EMPTY_INVERTED 1
 #endif
 // The leaf filter as tri_classify_flat (kernels_common.h: one divergent
-// branch per triangle record instead of a nest of five).  0: tri_classify.
+// branch per triangle record instead of a nest of five).  0: the nest.
 #ifndef RT_FLAT_CLASSIFY
 #define RT_FLAT_CLASSIFY 1
 #endif
@@ -752,8 +752,8 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                                                     tcull, tl, tu);
                             cls = valid ? cls : 0;
                         } else
-                            cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co,
-                                                       tcull, tl, tu)
+                            cls = valid ? tri_classify_nest(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz,
+                                                            q.co, tcull, tl, tu)
                                         : 0;
 #if defined(RT_DBL_LEAF) && RT_DBL_LEAF
                         {   // (measurement build: the triangle filter twice, tools/phase_counts.py)

@@ -229,25 +229,27 @@ __device__ __forceinline__ void wave_walk(const RtDevScene& sc, const RtFramePar
                         if (k >= end) break;
                         if (COUNT) lc.pre += valid;
                         float tl, tu;
-                        const int cls = valid ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz,
-                                                             q.co, tcull, tl, tu)
-                                              : 0;
-                        if (__ballot(cls != 0) == 0) continue;
-                        if (cls == 0) continue;
-                        if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
-                        if (nc == K) {
-                            int m = 0;
-                            for (int c = 0; c < K; c++) {
-                                const uint2 e = cand[c][tid];
-                                if (__uint_as_float(e.y) <= tcull) cand[m++][tid] = e;
+                        // (an invalid lane's class is computed and dropped by a
+                        // select; no `continue` in the unrolled chunk loop)
+                        int cls = tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull,
+                                               tl, tu);
+                        cls = valid ? cls : 0;
+                        if (cls != 0) {
+                            if (cls == 2) tcull = fminf(tcull, (tu + tsl) * (1.f + 0x1p-20f));
+                            if (nc == K) {
+                                int m = 0;
+                                for (int c = 0; c < K; c++) {
+                                    const uint2 e = cand[c][tid];
+                                    if (__uint_as_float(e.y) <= tcull) cand[m++][tid] = e;
+                                }
+                                nc = m;
                             }
-                            nc = m;
-                        }
-                        if (nc < K) {
-                            cand[nc][tid] = make_uint2(k, __float_as_uint(tl));
-                            nc++;
-                        } else {
-                            over = true;
+                            if (nc < K) {
+                                cand[nc][tid] = make_uint2(k, __float_as_uint(tl));
+                                nc++;
+                            } else {
+                                over = true;
+                            }
                         }
                     }
                 }

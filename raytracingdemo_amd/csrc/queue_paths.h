@@ -635,19 +635,21 @@ __device__ __forceinline__ bool wave_anyhit(const RtDevScene& sc, const RtFrameC
                         const uint32_t k = k0 + t;
                         if (k >= end) break;
                         float tl, tu;
-                        const int cls = tcull >= 0.f ? tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy,
-                                                                    q.dz, q.co, tcull, tl, tu)
-                                                     : 0;
-                        if (__ballot(cls != 0) == 0) continue;
-                        if (cls == 0) continue;
-                        bool hit = cls == 2 && tu < tcert;
-                        if (!hit) {
-                            double t, l2;
-                            hit = mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, ray_of(l2), t) && t < tmax;
-                        }
-                        if (hit) {
-                            occ = true;
-                            tcull = -1.f;  // this lane enters no box from now on
+                        // (an occluded lane's class is computed and dropped by
+                        // a select; no `continue` in the unrolled chunk loop)
+                        int cls = tri_classify(TA[t], TB[t], TC[t], q.ox, q.oy, q.oz, q.dx, q.dy, q.dz, q.co, tcull,
+                                               tl, tu);
+                        cls = tcull >= 0.f ? cls : 0;
+                        if (cls != 0) {
+                            bool hit = cls == 2 && tu < tcert;
+                            if (!hit) {
+                                double t, l2;
+                                hit = mt64(sc.tri64 + RT_TRI64_DOUBLES * (size_t)k, ray_of(l2), t) && t < tmax;
+                            }
+                            if (hit) {
+                                occ = true;
+                                tcull = -1.f;  // this lane enters no box from now on
+                            }
                         }
                     }
                 }

@@ -114,6 +114,7 @@ constexpr uint32_t kSampRedo = 0x80;
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;   // lane has no overflow chunk (yet)
 constexpr uint32_t kPoolDry = 0xFFFFFFFEu;   // the pool ran out: drop with a certified bound
 static_assert(kLeafChunk <= RT_TRI32_PAD, "tri32 padding must cover a leaf chunk");
+static_assert((RT_MAX_TRIS + (uint64_t)RT_TRI32_PAD) * 48u < (1ull << 32), "tri32 byte offsets are 32-bit");
 
 // Forces uniform values to be materialised (their loads waited on) here, so
 // a chunk's loads are all in flight before the first use.
@@ -726,8 +727,14 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                 // scalar loads are issued, then waited on once (tri32 carries
                 // padding records, so reading past a leaf is safe)
                 const uint32_t end = first + cnt;
-                for (uint32_t k0 = first; k0 < end; k0 += kLeafChunk) {
-                    const cfloat_p R = (cfloat_p)(tri32 + 12 * (size_t)k0);
+                // (a leaf holds >= 1 record: a do-while; the records' byte
+                // offset is 32-bit — the host caps the scene at 2^32 / 48
+                // records, rt_api.cpp — so the loads take it as an SGPR
+                // offset, with no 64-bit address arithmetic per chunk)
+                uint32_t k0 = first, kb = first * 48u;
+                do {
+                    __builtin_assume(kb < 0xFFFFFFF0u);
+                    const cfloat_p R = (cfloat_p)(tri32 + (size_t)(kb >> 2));
                     float4 TA[kLeafChunk], TB[kLeafChunk], TC[kLeafChunk];
 #pragma unroll
                     for (int t = 0; t < kLeafChunk; t++) {
@@ -740,7 +747,7 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
 #pragma unroll
                     for (int t = 0; t < kLeafChunk; t++) {
                         const uint32_t k = k0 + t;
-                        if (k >= end) break;
+                        if (t > 0 && k >= end) break;  // (record k0 < end: the do-while)
                         if (COUNT) n_pre += valid;
                         float tl, tu;
                         int cls;
@@ -798,7 +805,9 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                             }
                         }
                     }
-                }
+                    k0 += kLeafChunk;
+                    kb += 48u * kLeafChunk;
+                } while (k0 < end);
             }
             if constexpr (RT_LEAF_PRIO > 0) __builtin_amdgcn_s_setprio(0);
             if (sp == 0) break;

@@ -1063,7 +1063,7 @@ static int scene_create(const double* tri_v, uint64_t n, int algo, int k, int co
     *out = nullptr;
     if (algo < 0 || algo > 2) return fail(RT_ERR_OUT_OF_RANGE, "Unknown algorithm");
     if (!(k == 2 || k == 4 || k == 8 || k == 16)) return fail(RT_ERR_INVALID_ARGUMENT, "Unsupported bvh degree");
-    if (n > RT_LEAF_MAX_FIRST) return fail(RT_ERR_INVALID_ARGUMENT, "too many triangles");
+    if (n > RT_LEAF_MAX_FIRST || n > RT_MAX_TRIS) return fail(RT_ERR_INVALID_ARGUMENT, "too many triangles");
     try {
         using clk = std::chrono::steady_clock;
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };

@@ -23,6 +23,9 @@
 #define RT_INVALID_REF 0xFFFFFFFFu
 #define RT_LEAF_FIRST_MASK 0x07FFFFFFu
 #define RT_LEAF_MAX_FIRST 0x07FFFFFFu
+// scene triangle cap: the packet walk addresses tri32 records (48 B) with
+// 32-bit byte offsets (packet_kernel.h leaf loop), padding included
+#define RT_MAX_TRIS 0x05000000u
 #define RT_CHILD_REF 6       // u32 slot of the child ref in a 32-B child record
 // fp64 triangle record, one 128-B line in BVH order: everything k_resolve
 // needs for a candidate in one round trip.

@@ -361,6 +361,11 @@ __device__ __forceinline__ uint32_t node_mask(const float (&bx)[W][6], const Ray
     return mask & ((1u << nv) - 1u);
 }
 
+// RT_NEAR_ASM (default): the near child's index and the tile's direction
+// along the node's sort axis in one inline-asm block (node step); 0: C.
+#ifndef RT_NEAR_ASM
+#define RT_NEAR_ASM 1
+#endif
 // RT_NEAR_TREE (default): the near child's ref picked by a select tree on
 // the index bits instead of a compare-and-select chain; 0: the chain.
 // Round 6, three interleaved 20-step pairs on one box (the compiler's own
@@ -671,18 +676,59 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
                     // children are sorted along `axis`: walk them front to back
                     // for the tile's direction (lowest index first when the
                     // tile looks along +axis)
-                    const bool rev = (dsg >> (meta & 3u)) & 1u;
-                    const int near_c = rev ? 31 - __builtin_clz(mask) : __builtin_ctz(mask);
+                    int near_c;
+                    uint64_t revm;  // all ones when the tile looks along -axis (RT_NEAR_ASM)
+                    bool rev = false;
+                    if constexpr (RT_NEAR_ASM != 0) {
+                        // the near index and the direction as one SCC: 7
+                        // scalar instructions instead of 10 (the compiler's
+                        // form re-tests the bit and ANDs the lane mask with exec)
+                        // (a per-octant walk's direction bits are OCT itself:
+                        // an inline constant, no register)
+                        uint32_t n, l, ax;
+#define RT_NEAR_ASM_BODY                                      \
+    "s_ff1_i32_b32 %[n], %[m]\n\t"                             \
+    "s_flbit_i32_b32 %[l], %[m]\n\t"                           \
+    "s_sub_u32 %[l], 31, %[l]\n\t"                             \
+    "s_bfe_u32 %[ax], %[cur], 0x20018\n\t" /* meta & 3 */      \
+    "s_bitcmp1_b32 %[d], %[ax]\n\t"                            \
+    "s_cselect_b64 %[rv], -1, 0\n\t"                           \
+    "s_cselect_b32 %[n], %[l], %[n]"
+                        if constexpr (OCT >= 0)
+                            asm(RT_NEAR_ASM_BODY
+                                : [n] "=&s"(n), [l] "=&s"(l), [ax] "=&s"(ax), [rv] "=&s"(revm)
+                                : [m] "s"(mask), [cur] "s"(cur), [d] "i"(OCT)
+                                : "scc");
+                        else
+                            asm(RT_NEAR_ASM_BODY
+                                : [n] "=&s"(n), [l] "=&s"(l), [ax] "=&s"(ax), [rv] "=&s"(revm)
+                                : [m] "s"(mask), [cur] "s"(cur), [d] "s"(dsg)
+                                : "scc");
+#undef RT_NEAR_ASM_BODY
+                        near_c = (int)n;
+                    } else {
+                        rev = (dsg >> (meta & 3u)) & 1u;
+                        near_c = rev ? 31 - __builtin_clz(mask) : __builtin_ctz(mask);
+                        revm = 0;
+                    }
                     const uint32_t pm = mask & ~(1u << near_c);
                     if (pm != 0) {
                         // lane c: child c's ref (built only for nodes that push)
                         const uint32_t refv = lanes_of<W>(rs);
-                        // the rest go on the stack so that they pop in order
-                        const uint32_t below = pm & ((1u << (lane & 31)) - 1u);
-                        const uint32_t above = (pm >> (lane & 31)) >> 1;
-                        const int slot = (int)__builtin_popcount(rev ? below : above);
-                        if ((pm >> (lane & 31)) & 1u & (lane < W)) wstack[sp + slot] = refv;
-                        sp += __builtin_popcount(pm);
+                        // the rest go on the stack so that they pop in order:
+                        // lane c < W holds child c; `below` counts pm's bits
+                        // under it (v_mbcnt), the 64-bit shift is 0 for every
+                        // lane >= W (pm < 2^W), so no lane-range mask
+                        const uint32_t np = (uint32_t)__builtin_popcount(pm);
+                        const uint32_t below = __builtin_amdgcn_mbcnt_lo(pm, 0u);
+                        int slot;
+                        if constexpr (RT_NEAR_ASM != 0)
+                            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(slot) : "v"(np - 1u - below), "v"(below),
+                                "s"(revm));
+                        else
+                            slot = (int)(rev ? below : np - 1u - below);
+                        if (((uint64_t)pm >> lane) & 1u) wstack[sp + slot] = refv;
+                        sp += np;
                     }
                     // the near child's ref, picked on the scalar unit (a
                     // readlane from the lanes measured 0.5% slower, a scalar

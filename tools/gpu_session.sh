@@ -204,7 +204,7 @@ for s in $STEPS; do
                        -- python bench.py --steps 1 --warmup 0 --frames 36 --no-cpu --no-dropin || exit 1
                done
                python tools/pmc_summary.py gpurun_out/sq_$t/sq*_counter_collection.csv > gpurun_out/sq_summary_$t.txt ;;
-        pab)   # paths A/B: PAB_ENVS="A=1;RT_LIB=...;..." (one paths bench per entry)
+        pabenv) # paths A/B: PAB_ENVS="A=1;RT_LIB=...;..." (one paths bench per entry)
                i=0; IFS=';' read -ra cfgs <<< "${PAB_ENVS:-}"
                for c in "${cfgs[@]}"; do i=$((i+1))
                    env $c timeout -k 10 300 python bench.py --paths --no-cpu --steps 3 --warmup 1 > gpurun_out/pab$i.log 2>&1

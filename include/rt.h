@@ -236,7 +236,9 @@ int rt_camera_path(const double scene_center[3], int resolution, int step, doubl
 /* StackBVH::build(prims, partitionFn) (+ collapse passes for the "-c"
  * variants: 2-way partition then log2(k)-1 collapse passes, main.cpp:208,
  * 219-221).  algo = RT_ALGO_*, k in {2,4,8,16}.  The tree is identical to the
- * reference's.  The scene is host-only until rt_scene_upload. */
+ * reference's.  The scene is host-only until rt_scene_upload.  At most
+ * 83,886,080 triangles (the packet walk's 32-bit record offsets): more is
+ * RT_ERR_INVALID_ARGUMENT "too many triangles". */
 int rt_scene_create(const double *tri_v, uint64_t n_tris, int algo, int k, int collapse, rt_scene **out);
 
 /* rt_scene_create with the walk tree (the SAH tree the device traverses,

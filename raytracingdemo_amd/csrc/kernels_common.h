@@ -165,6 +165,11 @@ __device__ __forceinline__ int tri_classify_nest(const float4 A, const float4 B,
 // select.  For the packet walk, where a wave skips a triangle as a whole
 // only when all 64 rays reject it, each nested level of tri_classify cost
 // an exec save, a branch and an exec restore per triangle record.
+// RT_REJ_MAX=1: the five rejection tests of tri_classify_flat as one max and
+// one compare (fewer scalar mask ORs, more VALU); 0: five compares.
+#ifndef RT_REJ_MAX
+#define RT_REJ_MAX 0
+#endif
 __device__ __forceinline__ int tri_classify_flat(const float4 A, const float4 B, const float4 C, float ox, float oy,
                                                  float oz, float dx, float dy, float dz, float co, float tcull,
                                                  float& tl, float& tu) {
@@ -191,8 +196,19 @@ __device__ __forceinline__ int tri_classify_flat(const float4 A, const float4 B,
     const float sg = a > 0.f ? 1.f : -1.f;
     const float Us = sg * U, Vs = sg * V, Ts = sg * T;
     // (bitwise & and |: no short-circuit branches)
-    const bool rej = sure & ((Us < -errU) | (Vs < -errV) | (Ts < -errT) | (Us + Vs > aa + errU + errV + errA) |
-                             (Ts - errT > tcull * (aa + errA)));
+    bool rej;
+    if constexpr (RT_REJ_MAX != 0) {
+        // the same five tests as one compare: fl(b - a) > 0 exactly when
+        // b > a (a rounded difference is 0 only for a == b and keeps the
+        // sign otherwise), and a NaN term drops out of the max as its
+        // compare drops out of the OR
+        const float m = fmaxf(fmaxf(fmaxf(-errU - Us, -errV - Vs), -errT - Ts),
+                              fmaxf((Us + Vs) - (aa + errU + errV + errA), (Ts - errT) - tcull * (aa + errA)));
+        rej = sure & (m > 0.f);
+    } else {
+        rej = sure & ((Us < -errU) | (Vs < -errV) | (Ts < -errT) | (Us + Vs > aa + errU + errV + errA) |
+                      (Ts - errT > tcull * (aa + errA)));
+    }
     tl = 0.f;
     tu = __builtin_huge_valf();
     int cls = rej ? 0 : 1;

@@ -558,7 +558,11 @@ __device__ __forceinline__ TileOut trace_packet(args_p A, int f, int i, int r, b
     double kd[3];  // kKeepDir: the fp64 direction, kept for the resolve
     {
         const RtFrameParams fp = kload(&A->fp);
-        RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[f / fp.spp]), fp, f);  // this tile's frame
+        // (the pose of sample frame f: a uniform branch skips the integer
+        // division at 1 spp)
+        int pose = f;
+        if (fp.spp != 1) pose = f / fp.spp;
+        RtFrameCam cam = frame_cam_of(kload(&A->fp.pose[pose]), fp, f);  // this tile's frame
 #if !defined(RT_QPV_DIAG) || RT_QPV_DIAG < 2
         if constexpr (PATHS) q_primary_offset<W>(A, f, i, r, cam.ox, cam.oy);  // the path sample's jitter
 #endif
@@ -1491,6 +1495,35 @@ __device__ __forceinline__ void packet_exit(args_p A, uint2* ring, int lane) {
 #define RT_SCRATCH_PAD 4096
 #endif
 
+// The launch's tile geometry, computed once per block into LDS (RT_TILE_GEOM,
+// default): the per-tile claim then divides by the tiles per frame and per
+// tile row with a multiply-high and a shift instead of two runtime integer
+// divisions (a float-reciprocal sequence each, ~50 scalar instructions per
+// tile with the signed divisions by constants).
+#ifndef RT_TILE_GEOM
+#define RT_TILE_GEOM 1
+#endif
+struct TileGeom {
+    uint32_t tiles_x, tiles_f, tiles, claim;
+    uint32_t mf, sf, mx, sx;  // n / tiles_f = (n * mf) >> sf, n / tiles_x = (n * mx) >> sx, for n < 2^31
+};
+// m = ceil(2^(31+l) / d), l = ceil(log2 d): for n < 2^31, floor(n m / 2^(31+l))
+// = floor(n / d), since m d - 2^(31+l) < d <= 2^l and n < 2^31 (m < 2^32)
+__device__ __forceinline__ void div_magic(uint32_t d, uint32_t& m, uint32_t& sh) {
+    const uint32_t l = d > 1u ? 32u - (uint32_t)__builtin_clz(d - 1u) : 0u;
+    const uint64_t P = 1ull << (31u + l);
+    // (an fp64 quotient within one of P / d, then the exact ceiling by
+    // multiplies: no 64-bit integer division)
+    uint32_t q = (uint32_t)fmin((double)P / (double)d, 4294967295.0);
+    while ((uint64_t)q * d < P) q++;
+    while (q > 1u && (uint64_t)(q - 1u) * d >= P) q--;
+    m = q;
+    sh = 31u + l;
+}
+__device__ __forceinline__ uint32_t div_by(uint32_t n, uint32_t m, uint32_t sh) {
+    return (uint32_t)(((uint64_t)n * m) >> sh);
+}
+
 // JOB: the launch carries a side de-interleave job (RtLaunchAux::job_*; its
 // own instantiation, so the kernels without one keep their registers).
 template <int W, int SP, int K, bool COUNT, bool FUSED, bool PACK = false, bool JOB = false, bool PATHS = false>
@@ -1498,14 +1531,37 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     __shared__ uint32_t stacks[kPacketWaves][SP];
     __shared__ uint2 cands[kPacketWaves][K * 64];
     __shared__ PacketArgs s_args;
+    __shared__ TileGeom s_geom;
+    constexpr bool pack = FUSED && PACK;  // (launched only when fp.pack)
     {
         const __attribute__((address_space(4))) uint32_t* src =
             (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
         uint32_t* dst = reinterpret_cast<uint32_t*>(&s_args);
         for (unsigned w = threadIdx.x; w < sizeof(PacketArgs) / 4; w += blockDim.x) dst[w] = src[w];
+        if constexpr (RT_TILE_GEOM != 0) {
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                // fp.pack: a tile is ts x ts pixels of one pose with all spp
+                // samples (ts = 8 / n), else 8 x 8 pixels of one sample frame
+                // (from the LDS copy: the kernel argument itself stays unread)
+                const RtFrameParams& f = s_args.fp;
+                const uint32_t ts = pack ? 8u / (uint32_t)f.spp_n : (uint32_t)RT_TILE_W;
+                const uint32_t th = pack ? ts : 64u / RT_TILE_W;
+                TileGeom g;
+                g.tiles_x = ((uint32_t)f.W + ts - 1u) / ts;
+                g.tiles_f = g.tiles_x * (((uint32_t)f.nrows + th - 1u) / th);  // tiles per frame (pose when packed)
+                g.tiles = g.tiles_f * (uint32_t)(pack ? f.nframes / f.spp : f.nframes);
+                g.claim = g.tiles >= 64u * gridDim.x * kPacketWaves ? 2u : 1u;
+                div_magic(g.tiles_f, g.mf, g.sf);
+                div_magic(g.tiles_x, g.mx, g.sx);
+                s_geom = g;
+            }
+        }
         __syncthreads();
     }
     args_p A = (args_p)&s_args;
+    typedef const __attribute__((address_space(3))) TileGeom* geom_p;
+    geom_p G = (geom_p)&s_geom;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     // tile scheduling: one queue per XCD (blocks are dealt to the 8 XCDs
@@ -1527,17 +1583,27 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
     bool job = JOB;  // rows of the side job may be left
     for (;;) {
         A = launder(A);
+        // (laundered like A: the geometry is re-read per tile, not held in
+        // SGPRs across the walk)
+        asm volatile("" : "+s"(G));
         const int W_ = kword(&A->fp.W), nrows = kword(&A->fp.nrows);
         // fp.pack: a tile is ts x ts pixels of one pose with all spp samples
         // (ts = 8 / n), else 8 x 8 pixels of one sample frame
-        constexpr bool pack = FUSED && PACK;  // (launched only when fp.pack)
         const int spp = kword(&A->fp.spp);
         const int ts = pack ? 8 / kword(&A->fp.spp_n) : RT_TILE_W;
-        const int th = pack ? ts : 64 / RT_TILE_W;
-        const int tiles_x = (W_ + ts - 1) / ts;
-        const int tiles_f = tiles_x * ((nrows + th - 1) / th);  // tiles per frame (pose when packed)
-        const int tiles = tiles_f * (pack ? kword(&A->fp.nframes) / spp : kword(&A->fp.nframes));
-        claim = tiles >= 64 * (int)(gridDim.x * kPacketWaves) ? 2 : 1;
+        int tiles_x, tiles_f, tiles;
+        if constexpr (RT_TILE_GEOM != 0) {
+            tiles_x = (int)kword(&G->tiles_x);
+            tiles_f = (int)kword(&G->tiles_f);
+            tiles = (int)kword(&G->tiles);
+            claim = (int)kword(&G->claim);
+        } else {
+            const int th = pack ? ts : 64 / RT_TILE_W;
+            tiles_x = (W_ + ts - 1) / ts;
+            tiles_f = tiles_x * ((nrows + th - 1) / th);  // tiles per frame (pose when packed)
+            tiles = tiles_f * (pack ? kword(&A->fp.nframes) / spp : kword(&A->fp.nframes));
+            claim = tiles >= 64 * (int)(gridDim.x * kPacketWaves) ? 2 : 1;
+        }
         int s = 0;
         bool claimed = false;
         if (pend >= 0) {  // the rest of the last claim
@@ -1562,15 +1628,26 @@ __global__ void __launch_bounds__(64 * kPacketWaves) RT_PACKET_ATTR k_trace_pack
             pend_n = 1;
         }
         // (increasing with the slot: the first tile past the end ends the queue)
-        const int tile = ((slot / RT_TILE_RUN) * RT_QUEUES + (int)xq) * RT_TILE_RUN + slot % RT_TILE_RUN;
+        // (slot >= 0: unsigned arithmetic, shifts for the constant divisors)
+        const int tile = (int)((((uint32_t)slot / RT_TILE_RUN) * RT_QUEUES + xq) * RT_TILE_RUN +
+                               (uint32_t)slot % RT_TILE_RUN);
         if (tile >= tiles) {
             if constexpr (JOB)
                 while (job) job = side_copy(A, lane, xq);  // the job's rows the tiles left
             break;
         }
-        const int fr = tile / tiles_f;  // frame of the batch (pose when packed)
-        const int ft = tile - fr * tiles_f;
-        const int ty = ft / tiles_x, tx = ft - ty * tiles_x;
+        int fr, ft, ty, tx;
+        if constexpr (RT_TILE_GEOM != 0) {  // (tile < tiles < 2^31)
+            fr = (int)div_by((uint32_t)tile, kword(&G->mf), kword(&G->sf));  // frame of the batch (pose when packed)
+            ft = tile - fr * tiles_f;
+            ty = (int)div_by((uint32_t)ft, kword(&G->mx), kword(&G->sx));
+            tx = ft - ty * tiles_x;
+        } else {
+            fr = tile / tiles_f;  // frame of the batch (pose when packed)
+            ft = tile - fr * tiles_f;
+            ty = ft / tiles_x;
+            tx = ft - ty * tiles_x;
+        }
         int f = fr, i, r;
         if constexpr (pack) {  // lane = pixel * spp + sample
             const int pl = lane / spp;

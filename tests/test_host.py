@@ -305,3 +305,34 @@ def test_import_orders_exit_cleanly_with_one_rccl(order):
     assert len(mapped) == 1, mapped           # never two copies
     torch_rccl = os.path.realpath(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
     assert os.path.realpath(path) == torch_rccl  # the process's (PyTorch's) copy
+
+
+def test_tile_division_magic():
+    """packet_kernel.h div_magic / div_by (the per-tile division by the tiles
+    per frame and per tile row): the multiply-high form equals integer
+    division for every n < 2^31, here over divisors 1..4096, large and
+    power-of-two ones, and the n that stress each (multiples, their
+    neighbours, 2^31 - 1)."""
+    import random
+
+    def magic(d):  # the device code's arithmetic, step for step
+        l = (d - 1).bit_length() if d > 1 else 0
+        P = 1 << (31 + l)
+        q = min(int(float(P) / float(d)), 0xFFFFFFFF)
+        while q * d < P:
+            q += 1
+        while q > 1 and (q - 1) * d >= P:
+            q -= 1
+        assert q < 1 << 32
+        return q, 31 + l
+
+    rng = random.Random(7)
+    ds = list(range(1, 4097)) + [240 * 135, 480 * 270, 32400 * 36, (1 << 31) - 1, 1 << 30, 3 << 29]
+    ds += [rng.randrange(1, 1 << 31) for _ in range(200)]
+    for d in ds:
+        m, sh = magic(d)
+        ns = [0, 1, d - 1, d, d + 1, (1 << 31) - 1, ((1 << 31) - 1) // d * d, ((1 << 31) - 1) // d * d - 1]
+        ns += [rng.randrange(0, 1 << 31) for _ in range(20)]
+        for n in ns:
+            if 0 <= n < 1 << 31:
+                assert (n * m) >> sh == n // d, (d, n)
